@@ -1,0 +1,160 @@
+"""Deterministic synthetic weights and crops for CLIP-EBC (ViT-B/16 + deep VPT).
+
+There are no CLIP checkpoints offline (the reference downloads them on import,
+`models/clip/_clip/__init__.py:31-36`), so parity and benchmarking run on weights
+generated here from a seed.  Every tensor is drawn from its own
+`numpy.random.Generator(PCG64([seed, crc32(key)]))`, so a key's values do not depend
+on which other keys exist or on their order; the GPU box regenerates exactly the same
+arrays as this container.
+
+Key names are the reference's `CLIP_EBC.state_dict()` keys:
+`image_encoder.*`, `vpt_{l}`, `image_decoder.0.*`, `projection.*`, `text_encoder.*`,
+`logit_scale`.
+
+Synthetic crops follow BASELINE.md: pixels U[0,1) normalised by the ImageNet mean/std
+(`datasets/crowd.py:64`), point counts lognormal(ln 20, 1.2) clipped to [0, 2048],
+coordinates U[0, S)^2, density = point map (`datasets/utils.py:11-28`, sigma=None).
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+WIDTH = 768          # ViT-B/16 width
+HEADS = 12
+PATCH = 16
+EMBED = 512          # CLIP joint embedding
+TEXT_WIDTH = 512
+TEXT_HEADS = 8
+TEXT_CTX = 77
+VOCAB = 49408
+NUM_VPT = 32
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def _rng(seed: int, key: str) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64([seed, zlib.crc32(key.encode())]))
+
+
+def _normal(seed, key, shape, std, mean=0.0):
+    return (mean + std * _rng(seed, key).standard_normal(shape)).astype(np.float32)
+
+
+def _uniform(seed, key, shape, lo, hi):
+    return _rng(seed, key).uniform(lo, hi, shape).astype(np.float32)
+
+
+def _block(sd, seed, prefix, width):
+    s = 1.0 / math.sqrt(width)
+    sd[prefix + "attn.in_proj_weight"] = _normal(seed, prefix + "attn.in_proj_weight", (3 * width, width), s)
+    sd[prefix + "attn.in_proj_bias"] = _normal(seed, prefix + "attn.in_proj_bias", (3 * width,), 0.02)
+    sd[prefix + "attn.out_proj.weight"] = _normal(seed, prefix + "attn.out_proj.weight", (width, width), 0.5 * s)
+    sd[prefix + "attn.out_proj.bias"] = _normal(seed, prefix + "attn.out_proj.bias", (width,), 0.02)
+    for ln in ("ln_1", "ln_2"):
+        sd[prefix + ln + ".weight"] = _normal(seed, prefix + ln + ".weight", (width,), 0.05, 1.0)
+        sd[prefix + ln + ".bias"] = _normal(seed, prefix + ln + ".bias", (width,), 0.05)
+    sd[prefix + "mlp.c_fc.weight"] = _normal(seed, prefix + "mlp.c_fc.weight", (4 * width, width), s)
+    sd[prefix + "mlp.c_fc.bias"] = _normal(seed, prefix + "mlp.c_fc.bias", (4 * width,), 0.02)
+    sd[prefix + "mlp.c_proj.weight"] = _normal(seed, prefix + "mlp.c_proj.weight", (width, 4 * width), 0.5 / math.sqrt(4 * width))
+    sd[prefix + "mlp.c_proj.bias"] = _normal(seed, prefix + "mlp.c_proj.bias", (width,), 0.02)
+
+
+def vit_state(seed: int = 0, layers: int = 12, input_size: int = 224) -> Dict[str, np.ndarray]:
+    """Frozen CLIP ViT-B/16 visual tower (`image_encoder.py:118-161`), features_only."""
+    g = input_size // PATCH
+    sd: Dict[str, np.ndarray] = {}
+    p = "image_encoder."
+    sd[p + "conv1.weight"] = _normal(seed, p + "conv1.weight", (WIDTH, 3, PATCH, PATCH), 1.0 / math.sqrt(3 * PATCH * PATCH))
+    sd[p + "class_embedding"] = _normal(seed, p + "class_embedding", (WIDTH,), WIDTH ** -0.5)
+    sd[p + "positional_embedding"] = _normal(seed, p + "positional_embedding", (g * g + 1, WIDTH), WIDTH ** -0.5)
+    for ln in ("ln_pre", "ln_post"):
+        sd[p + ln + ".weight"] = _normal(seed, p + ln + ".weight", (WIDTH,), 0.05, 1.0)
+        sd[p + ln + ".bias"] = _normal(seed, p + ln + ".bias", (WIDTH,), 0.05)
+    for i in range(layers):
+        _block(sd, seed, f"{p}transformer.resblocks.{i}.", WIDTH)
+    return sd
+
+
+def text_state(seed: int = 0, layers: int = 12) -> Dict[str, np.ndarray]:
+    """Frozen CLIP text tower (`text_encoder.py:7-53`)."""
+    sd: Dict[str, np.ndarray] = {}
+    p = "text_encoder."
+    sd[p + "token_embedding.weight"] = _normal(seed, p + "token_embedding.weight", (VOCAB, TEXT_WIDTH), 0.02)
+    sd[p + "positional_embedding"] = _normal(seed, p + "positional_embedding", (TEXT_CTX, TEXT_WIDTH), 0.01)
+    for i in range(layers):
+        _block(sd, seed, f"{p}transformer.resblocks.{i}.", TEXT_WIDTH)
+    sd[p + "ln_final.weight"] = _normal(seed, p + "ln_final.weight", (TEXT_WIDTH,), 0.05, 1.0)
+    sd[p + "ln_final.bias"] = _normal(seed, p + "ln_final.bias", (TEXT_WIDTH,), 0.05)
+    sd[p + "text_projection"] = _normal(seed, p + "text_projection", (TEXT_WIDTH, EMBED), TEXT_WIDTH ** -0.5)
+    return sd
+
+
+def trainable_state(seed: int = 0, layers: int = 12, deep_vpt: bool = True) -> Dict[str, np.ndarray]:
+    """VPT tokens, BasicBlock decoder, projection, logit_scale.
+
+    Init laws follow the reference: VPT U(+-sqrt(6/(3*16+768))) (`models/clip/model.py:70-75`),
+    conv kaiming_normal(fan_out, relu) and BN (1, 0) (`models/utils.py:366-379`),
+    logit_scale = ln(1/0.07) (`models/clip/model.py:117`).
+    """
+    sd: Dict[str, np.ndarray] = {}
+    val = math.sqrt(6.0 / float(3 * PATCH + WIDTH))
+    for i in range(layers if deep_vpt else 1):
+        sd[f"vpt_{i}"] = _uniform(seed, f"vpt_{i}", (NUM_VPT, WIDTH), -val, val)
+    d = "image_decoder.0."
+    std = math.sqrt(2.0 / (WIDTH * 9))
+    for c, bn in (("conv1", "bn1"), ("conv2", "bn2")):
+        sd[d + c + ".weight"] = _normal(seed, d + c + ".weight", (WIDTH, WIDTH, 3, 3), std)
+        sd[d + bn + ".weight"] = np.ones(WIDTH, np.float32)
+        sd[d + bn + ".bias"] = np.zeros(WIDTH, np.float32)
+        sd[d + bn + ".running_mean"] = np.zeros(WIDTH, np.float32)
+        sd[d + bn + ".running_var"] = np.ones(WIDTH, np.float32)
+        sd[d + bn + ".num_batches_tracked"] = np.zeros((), np.int64)
+    sd["projection.weight"] = _normal(seed, "projection.weight", (EMBED, WIDTH, 1, 1), math.sqrt(2.0 / EMBED))
+    sd["projection.bias"] = np.zeros(EMBED, np.float32)
+    sd["logit_scale"] = np.array(math.log(1 / 0.07), np.float32)
+    return sd
+
+
+def full_state(seed: int = 0, layers: int = 12, text_layers: int = 12, input_size: int = 224,
+               include_text: bool = True) -> Dict[str, np.ndarray]:
+    sd = vit_state(seed, layers, input_size)
+    sd.update(trainable_state(seed, layers))
+    if include_text:
+        sd.update(text_state(seed, text_layers))
+    return sd
+
+
+def crop_rng(seed: int) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def synthetic_crops(batch: int, size: int = 224, seed: int = 1000, max_points: int = 2048,
+                    counts: List[int] | None = None) -> Tuple[np.ndarray, List[np.ndarray], np.ndarray]:
+    """Return (images [B,3,S,S] f32 normalised, points list of [n_i,2] (x,y) f32, density [B,1,S,S])."""
+    g = crop_rng(seed)
+    img = g.random((batch, 3, size, size), dtype=np.float32)
+    mean = np.asarray(IMAGENET_MEAN, np.float32).reshape(1, 3, 1, 1)
+    std = np.asarray(IMAGENET_STD, np.float32).reshape(1, 3, 1, 1)
+    img = (img - mean) / std
+    if counts is None:
+        counts = np.clip(np.floor(g.lognormal(math.log(20.0), 1.2, batch)), 0, max_points).astype(int).tolist()
+    points = [(g.random((n, 2)) * size).astype(np.float32) for n in counts]
+    density = np.zeros((batch, 1, size, size), np.float32)
+    for b, p in enumerate(points):
+        density[b, 0] = point_map(p, size, size)
+    return img.astype(np.float32), points, density
+
+
+def point_map(points: np.ndarray, height: int, width: int) -> np.ndarray:
+    """Dot-annotation map: 1.0 at each (clamped, truncated) point (`datasets/utils.py:11-22`)."""
+    m = np.zeros((height, width), np.float32)
+    if len(points):
+        p = points.astype(np.int64)  # .long() truncates toward zero
+        x = np.clip(p[:, 0], 0, width - 1)
+        y = np.clip(p[:, 1], 0, height - 1)
+        m[y, x] = 1.0
+    return m

@@ -1,0 +1,204 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+torch-fp32 CPU restatement of the CLIP-EBC ViT-B/16 + deep-VPT training step.
+Each function cites the reference lines it restates.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def oracle_lib() -> ctypes.CDLL:
+    """The compiled C restatement (built by `make -C oracle` / __graft_entry__.build())."""
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle_sinkhorn.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        lib = ctypes.CDLL(path)
+        f = lib.oracle_ot_crop
+        fp = ctypes.POINTER(ctypes.c_float)
+        dp = ctypes.POINTER(ctypes.c_double)
+        f.argtypes = [fp, ctypes.c_int, fp, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                      ctypes.c_float, ctypes.c_int, fp, fp, fp, fp, ctypes.POINTER(ctypes.c_int), fp, dp, dp, dp]
+        f.restype = ctypes.c_int
+        _LIB = lib
+    return _LIB
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def ot_crop(points: np.ndarray, pred_density: np.ndarray, size: int, reduction: int = 8, reg: float = 10.0,
+            max_iter: int = 100, stop_thr: float = 1e-9, eval_freq: int = 10) -> Dict[str, np.ndarray]:
+    """One crop of OTLoss.forward (losses/dm_loss.py:49-77) + sinkhorn (bregman_pytorch.py:11-144)."""
+    lib = oracle_lib()
+    g = size // reduction
+    M = g * g
+    n = len(points)
+    pts = np.ascontiguousarray(points, np.float32).reshape(-1)
+    pd = np.ascontiguousarray(pred_density, np.float32).reshape(-1)
+    assert pd.size == M
+    beta = np.zeros(M, np.float32); v = np.zeros(M, np.float32); grad = np.zeros(M, np.float32)
+    u = np.zeros(max(n, 1), np.float32); err = np.full(max_iter // eval_freq + 1, -1.0, np.float32)
+    ne = ctypes.c_int(0); wd = ctypes.c_double(0); obj = ctypes.c_double(0); loss = ctypes.c_double(0)
+    it = lib.oracle_ot_crop(_fp(pts), n, _fp(pd), size, reduction, reg, max_iter, stop_thr, eval_freq,
+                            _fp(beta), _fp(u), _fp(v), _fp(err), ctypes.byref(ne), _fp(grad),
+                            ctypes.byref(wd), ctypes.byref(obj), ctypes.byref(loss))
+    return dict(beta=beta, u=u[:n], v=v, err=err[:ne.value], ot_grad=grad, wd=wd.value, ot_obj=obj.value,
+                loss=loss.value, iters=abs(it), rolled_back=it < 0)
+
+
+# ----------------------------------------------------------------------------- loss
+def reshape_density(d: torch.Tensor, r: int) -> torch.Tensor:
+    """losses/utils.py:4-9 — r x r block sums."""
+    B, _, H, W = d.shape
+    return d.reshape(B, 1, H // r, r, W // r, r).sum(dim=(-1, -3))
+
+
+def bin_count(density: torch.Tensor, bins: Sequence[Tuple[float, float]]) -> torch.Tensor:
+    """losses/dace_loss.py:42-47 — inclusive bins, later bins win."""
+    cls = torch.zeros_like(density, dtype=torch.long)
+    for idx, (lo, hi) in enumerate(bins):
+        cls[(density >= lo) & (density <= hi)] = idx
+    return cls.squeeze(1)
+
+
+class _OTGrad(torch.autograd.Function):
+    """loss = sum(pred * grad.detach()) (dm_loss.py:76): its gradient w.r.t. pred is the OT gradient."""
+    @staticmethod
+    def forward(ctx, pred, grad):
+        ctx.save_for_backward(grad)
+        return (pred * grad).sum().reshape(1)
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return g * grad, None
+
+
+def dace_loss(pred_class: torch.Tensor, pred_density: torch.Tensor, target_density: torch.Tensor,
+              points: List[np.ndarray], bins, reduction: int = 8, input_size: int = 224,
+              weight_count_loss: float = 1.0, weight_ot: float = 0.1, weight_tv: float = 0.01):
+    """DACELoss(count_loss='dmcount').forward — dace_loss.py:49-70 with DMLoss dm_loss.py:99-124."""
+    if target_density.shape[-2:] != pred_density.shape[-2:]:
+        target_density = reshape_density(target_density, reduction)
+    target_class = bin_count(target_density, bins)
+    ce = F.cross_entropy(pred_class, target_class, reduction="none").sum(dim=(-1, -2)).mean()
+    B = pred_density.shape[0]
+    pred_count = pred_density.view(B, -1).sum(dim=1)
+    normed_pred = pred_density / (pred_count.view(-1, 1, 1, 1) + 1e-8)
+    target_count = torch.tensor([len(p) for p in points], dtype=torch.float32)
+    normed_target = target_density / (target_count.view(-1, 1, 1, 1) + 1e-8)
+    grads = np.zeros((B,) + tuple(pred_density.shape[1:]), np.float32)
+    pdn = pred_density.detach().cpu().numpy()
+    for b, p in enumerate(points):
+        if len(p) > 0:
+            grads[b] = ot_crop(p, pdn[b, 0], input_size, reduction)["ot_grad"].reshape(pdn.shape[1:])
+    ot_loss = _OTGrad.apply(pred_density, torch.from_numpy(grads))
+    tv = ((normed_pred - normed_target).abs().sum(dim=(1, 2, 3)) * target_count).mean()
+    cnt = (pred_count - target_count).abs().mean()
+    dm = ot_loss * weight_ot + tv * weight_tv + cnt
+    loss = ce + weight_count_loss * dm
+    info = {"loss": loss.detach(), "ot_loss": ot_loss.detach(), "tv_loss": tv.detach(),
+            "count_loss": cnt.detach(), "ce_loss": ce.detach()}
+    return loss, info
+
+
+# ----------------------------------------------------------------------------- model
+def layer_norm(x, w, b):
+    """blocks.py:8-14 — LayerNorm in fp32, eps 1e-5."""
+    return F.layer_norm(x if x.dtype == torch.float64 else x.float(), (x.shape[-1],), w, b, 1e-5)
+
+
+def block(x, p, pre, heads=12):
+    """ResidualAttentionBlock.forward (blocks.py:39-42); x is [B, L, D] (batch-first here)."""
+    B, L, D = x.shape
+    h = layer_norm(x, p[pre + "ln_1.weight"], p[pre + "ln_1.bias"])
+    qkv = F.linear(h, p[pre + "attn.in_proj_weight"], p[pre + "attn.in_proj_bias"])
+    q, k, v = qkv.split(D, dim=-1)
+    hd = D // heads
+    q = q.view(B, L, heads, hd).transpose(1, 2)
+    k = k.view(B, L, heads, hd).transpose(1, 2)
+    v = v.view(B, L, heads, hd).transpose(1, 2)
+    s = torch.matmul(q, k.transpose(-1, -2)) / math.sqrt(hd)
+    o = torch.matmul(s.softmax(-1), v).transpose(1, 2).reshape(B, L, D)
+    x = x + F.linear(o, p[pre + "attn.out_proj.weight"], p[pre + "attn.out_proj.bias"])
+    h = layer_norm(x, p[pre + "ln_2.weight"], p[pre + "ln_2.bias"])
+    a = F.linear(h, p[pre + "mlp.c_fc.weight"], p[pre + "mlp.c_fc.bias"])
+    a = a * torch.sigmoid(1.702 * a)                                  # QuickGELU blocks.py:17-19
+    return x + F.linear(a, p[pre + "mlp.c_proj.weight"], p[pre + "mlp.c_proj.bias"])
+
+
+def vit_vpt_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, layers: int, num_vpt: int = 32) -> torch.Tensor:
+    """CLIP_EBC._forward_vpt (models/clip/model.py:142-189), deep VPT, vpt_drop=0."""
+    B, _, H, W = x.shape
+    gh, gw = H // 16, W // 16
+    e = "image_encoder."
+    f = F.conv2d(x, p[e + "conv1.weight"], stride=16).reshape(B, 768, -1).permute(0, 2, 1)
+    cls = p[e + "class_embedding"].view(1, 1, -1).expand(B, 1, 768)
+    f = torch.cat([cls, f], dim=1) + p[e + "positional_embedding"]
+    f = layer_norm(f, p[e + "ln_pre.weight"], p[e + "ln_pre.bias"])
+    for l in range(layers):
+        vpt = p[f"vpt_{l}"].unsqueeze(0).expand(B, -1, -1)
+        f = torch.cat([f[:, :1], vpt, f[:, 1:]], dim=1)
+        f = block(f, p, f"{e}transformer.resblocks.{l}.")
+        f = torch.cat([f[:, :1], f[:, 1 + num_vpt:]], dim=1)
+    f = layer_norm(f, p[e + "ln_post.weight"], p[e + "ln_post.bias"])
+    return f[:, 1:].permute(0, 2, 1).reshape(B, 768, gh, gw)
+
+
+def batch_norm_train(x, w, b):
+    return F.batch_norm(x, None, None, w, b, training=True, momentum=0.1, eps=1e-5)
+
+
+def decoder(p, x):
+    """BasicBlock (models/utils.py:290-303) after bilinear x2 (models/clip/model.py:195-196)."""
+    x = F.interpolate(x, scale_factor=2.0, mode="bilinear")
+    d = "image_decoder.0."
+    o = F.conv2d(x, p[d + "conv1.weight"], padding=1)
+    o = F.relu(batch_norm_train(o, p[d + "bn1.weight"], p[d + "bn1.bias"]))
+    o = F.conv2d(o, p[d + "conv2.weight"], padding=1)
+    o = batch_norm_train(o, p[d + "bn2.weight"], p[d + "bn2.bias"])
+    return F.relu(o + x)
+
+
+def head(p, x, text_features, anchors):
+    """projection + similarity head (models/clip/model.py:198-212)."""
+    x = F.conv2d(x, p["projection.weight"], p["projection.bias"])
+    img = F.normalize(x.permute(0, 2, 3, 1), p=2, dim=-1)
+    txt = F.normalize(text_features, p=2, dim=-1)
+    logits = (p["logit_scale"].exp() * img @ txt.t()).permute(0, 3, 1, 2)
+    probs = logits.softmax(dim=1)
+    exp = (probs * torch.as_tensor(anchors, dtype=probs.dtype).view(1, -1, 1, 1)).sum(dim=1, keepdim=True)
+    return logits, exp
+
+
+TRAINABLE_PREFIXES = ("vpt_", "image_decoder.", "projection.", "logit_scale")
+
+
+def params_from_state(sd: Dict[str, np.ndarray], requires_grad: bool = True) -> Dict[str, torch.Tensor]:
+    out = {}
+    for k, v in sd.items():
+        t = torch.tensor(np.asarray(v))
+        if requires_grad and k.startswith(TRAINABLE_PREFIXES) and t.is_floating_point():
+            t.requires_grad_(True)
+        out[k] = t
+    return out
+
+
+def forward(p, x, text_features, anchors, layers: int):
+    feats = vit_vpt_forward(p, x, layers)
+    return head(p, decoder(p, feats), text_features, anchors) + (feats,)

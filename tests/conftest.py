@@ -1,0 +1,43 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+for p in (REPO, os.path.join(REPO, "clip-ebc_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+BINS = [(0.0, 0.0), (1.0, 1.0), (2.0, 2.0), (3.0, 3.0), (4.0, float("inf"))]
+ANCHORS_NWPU = [0.0, 1.0, 2.0, 3.0, 4.21931]
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device) and the built libebc_hip.so")
+
+
+def golden(name: str):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def rel_l2(a, b) -> float:
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def rel_max(a, b) -> float:
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def split_points(d):
+    offs = d["offsets"]; pts = d["points"]
+    return [pts[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+
+
+@pytest.fixture(scope="session")
+def gpu_available():
+    import torch
+    return torch.cuda.is_available()

@@ -1,0 +1,266 @@
+"""Generate the golden parity fixtures by running the REFERENCE (Yiming-M/CLIP-EBC) in this container.
+
+Run here only (it reads /root/reference, which does not exist on the GPU box):
+
+    python tests/golden/make_golden.py
+
+What it imports from the reference, and how:
+  * `losses/` (DACELoss, DMLoss, sinkhorn) - imported as a package, it only needs torch.
+  * the CLIP-EBC ViT path - `import models` would download CLIP weights on import
+    (`models/clip/_clip/__init__.py:31-36`), so stub parent packages are registered in
+    `sys.modules` and only the needed files are loaded by path: `models/utils.py`,
+    `models/clip/utils.py`, `models/clip/_clip/{blocks,image_encoder,text_encoder,simple_tokenizer}.py`,
+    `models/clip/model.py`.  `tokenize` is restated from `_clip/utils.py:209-249` (that file
+    imports torchvision, absent here); `ftfy.fix_text` is stubbed as identity (prompts are ASCII).
+  * `utils/eval_utils.py` loaded by path (its package `__init__` imports torchvision).
+
+Weights are the deterministic synthetic ones of `ebc_amd.synthetic` (regenerable on the GPU
+box); inputs are seeded.  Only inputs that cannot be regenerated cheaply and the outputs
+are written, as compressed .npz files next to this script.
+"""
+from __future__ import annotations
+
+import importlib.util
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, os.path.join(REPO, "clip-ebc_amd"))
+from ebc_amd import synthetic as syn  # noqa: E402
+
+BINS = [(0.0, 0.0), (1.0, 1.0), (2.0, 2.0), (3.0, 3.0), (4.0, float("inf"))]
+ANCHORS_NWPU = [0.0, 1.0, 2.0, 3.0, 4.21931]   # configs/reduction_8.json ["4"]["nwpu"]
+
+
+def _load(name: str, path: str):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _stub_pkg(name: str, path: str):
+    m = types.ModuleType(name)
+    m.__path__ = [path]
+    sys.modules[name] = m
+    return m
+
+
+def load_reference():
+    sys.modules.setdefault("ftfy", types.SimpleNamespace(fix_text=lambda s: s))
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import losses  # the reference's own package
+    from losses.bregman_pytorch import sinkhorn
+    models = _stub_pkg("models", f"{REF}/models")
+    mclip = _stub_pkg("models.clip", f"{REF}/models/clip")
+    _clip = _stub_pkg("models.clip._clip", f"{REF}/models/clip/_clip")
+    _load("models.utils", f"{REF}/models/utils.py")
+    _load("models.clip.utils", f"{REF}/models/clip/utils.py")
+    _load("models.clip._clip.blocks", f"{REF}/models/clip/_clip/blocks.py")
+    ie = _load("models.clip._clip.image_encoder", f"{REF}/models/clip/_clip/image_encoder.py")
+    te = _load("models.clip._clip.text_encoder", f"{REF}/models/clip/_clip/text_encoder.py")
+    st = _load("models.clip._clip.simple_tokenizer", f"{REF}/models/clip/_clip/simple_tokenizer.py")
+    tok = st.SimpleTokenizer()
+
+    def tokenize(texts, context_length=77):
+        # restated from models/clip/_clip/utils.py:209-249
+        if isinstance(texts, str):
+            texts = [texts]
+        sot, eot = tok.encoder["<|startoftext|>"], tok.encoder["<|endoftext|>"]
+        out = torch.zeros(len(texts), context_length, dtype=torch.int)
+        for i, t in enumerate(texts):
+            ids = [sot] + tok.encode(t) + [eot]
+            out[i, :len(ids)] = torch.tensor(ids)
+        return out
+
+    state = {"vit_layers": 12}
+    _clip.tokenize = tokenize
+    _clip.vit_b_16_img = lambda features_only=True, input_size=224, **kw: ie.VisionTransformer(
+        input_size, 16, 512, 768, state["vit_layers"], 12, features_only=features_only)
+    _clip.vit_b_16_txt = lambda: te.CLIPTextEncoder(512, 77, 49408, 512, 8, 12)
+    model_mod = _load("models.clip.model", f"{REF}/models/clip/model.py")
+    eval_utils = _load("ref_eval_utils", f"{REF}/utils/eval_utils.py")
+    return types.SimpleNamespace(losses=losses, sinkhorn=sinkhorn, model_mod=model_mod, state=state,
+                                 tokenize=tokenize, eval_utils=eval_utils)
+
+
+def build_ref_model(ref, layers: int, prompt_type: str = "word", anchors=ANCHORS_NWPU, seed: int = 0):
+    ref.state["vit_layers"] = layers
+    torch.manual_seed(0)
+    m = ref.model_mod._clip_ebc("vit_b_16", BINS, anchors, reduction=8, prompt_type=prompt_type,
+                                input_size=224, num_vpt=32, deep_vpt=True, vpt_drop=0.0)
+    sd = syn.full_state(seed, layers=layers)
+    missing, unexpected = m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, strict=False)
+    assert not unexpected, unexpected
+    assert all(k.endswith("num_batches_tracked") for k in missing) or not missing, missing
+    m._extract_text_features()
+    return m
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print("wrote", path, f"{os.path.getsize(path) / 1024:.0f} KiB")
+
+
+def pack_points(points):
+    offs = np.zeros(len(points) + 1, np.int32)
+    offs[1:] = np.cumsum([len(p) for p in points])
+    flat = np.concatenate([p.reshape(-1, 2) for p in points]).astype(np.float32) if offs[-1] else np.zeros((0, 2), np.float32)
+    return flat, offs
+
+
+def loss_case(ref, size: int, counts, seed: int):
+    """F1: DACE(dmcount) loss + Sinkhorn internals on a ragged crop batch."""
+    g = np.random.Generator(np.random.PCG64(seed))
+    B = len(counts)
+    h = size // 8
+    points = [(g.random((n, 2)) * size).astype(np.float32) for n in counts]
+    density = np.stack([syn.point_map(p, size, size)[None] for p in points])
+    pred_class = g.standard_normal((B, 5, h, h)).astype(np.float32)
+    pred_density = (g.random((B, 1, h, h)) * 1.5).astype(np.float32)
+    pc = torch.tensor(pred_class, requires_grad=True)
+    pd = torch.tensor(pred_density, requires_grad=True)
+    loss_fn = ref.losses.DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=size)
+    loss, info = loss_fn(pc, pd, torch.from_numpy(density), [torch.from_numpy(p) for p in points])
+    loss.backward()
+    out = dict(size=size, counts=np.asarray(counts), pred_class=pred_class, pred_density=pred_density,
+               grad_pred_class=pc.grad.numpy(), grad_pred_density=pd.grad.numpy())
+    flat, offs = pack_points(points)
+    out["points"], out["offsets"] = flat, offs
+    for k, v in info.items():
+        out["info_" + k] = v.detach().numpy().reshape(())
+    # sinkhorn internals per crop, with OTLoss's exact inputs (dm_loss.py:51-64)
+    ot = loss_fn.count_loss_fn.ot_loss
+    cood = ot.cood
+    pdt = torch.from_numpy(pred_density)
+    normed = pdt / (pdt.view(B, -1).sum(1).view(-1, 1, 1, 1) + 1e-8)
+    betas, us, vs, errs, grads, wds = [], [], [], [], [], []
+    for b, p in enumerate(points):
+        if len(p) == 0:
+            betas.append(np.zeros(h * h, np.float32)); us.append(np.zeros(0, np.float32))
+            vs.append(np.zeros(h * h, np.float32)); errs.append(np.zeros(10, np.float32) - 1)
+            grads.append(np.zeros(h * h, np.float32)); wds.append(0.0)
+            continue
+        pt = torch.from_numpy(p)
+        x = pt[:, 0].unsqueeze(1); y = pt[:, 1].unsqueeze(1)
+        xd = -2 * torch.matmul(x, cood) + x * x + cood * cood
+        yd = -2 * torch.matmul(y, cood) + y * y + cood * cood
+        dist = (yd.unsqueeze(2) + xd.unsqueeze(1)).view(len(p), -1)
+        a = torch.ones(len(p)) / len(p)
+        P, log = ref.sinkhorn(a, normed[b][0].view(-1), dist, 10.0, maxIter=100, log=True)
+        betas.append(log["beta"].numpy()); us.append(log["u"].numpy()); vs.append(log["v"].numpy())
+        e = np.full(10, -1.0, np.float32); e[:len(log["err"])] = log["err"]; errs.append(e)
+        sd = pdt[b][0].view(-1); sc = sd.sum()
+        grad = sc / (sc * sc + 1e-8) * log["beta"] - (sd * log["beta"]).sum() / (sc * sc + 1e-8)
+        grads.append(grad.numpy()); wds.append(float(torch.sum(dist * P)))
+        if len(p) <= 200:
+            out[f"P_{b}"] = P.numpy()
+    out.update(beta=np.stack(betas), v=np.stack(vs), err=np.stack(errs), ot_grad=np.stack(grads), wd=np.asarray(wds))
+    out["u_flat"] = np.concatenate(us) if us else np.zeros(0, np.float32)
+    return out
+
+
+def head_case(ref, seed: int = 5):
+    """F2: projection + similarity head on a given decoder output."""
+    m = build_ref_model(ref, layers=1)
+    m._forward_vpt = lambda x: x
+    m.reduction = m.encoder_reduction
+    m.image_decoder = torch.nn.Identity()
+    m.train()
+    g = np.random.Generator(np.random.PCG64(seed))
+    X = np.maximum(g.standard_normal((2, 768, 28, 28)), 0).astype(np.float32)
+    R1 = g.standard_normal((2, 5, 28, 28)).astype(np.float32)
+    R2 = g.standard_normal((2, 1, 28, 28)).astype(np.float32)
+    xt = torch.tensor(X, requires_grad=True)
+    logits, exp = m(xt)
+    L = (logits * torch.from_numpy(R1)).sum() + (exp * torch.from_numpy(R2)).sum()
+    L.backward()
+    return dict(seed=seed, logits=logits.detach().numpy(), exp=exp.detach().numpy(),
+                grad_x_sub=xt.grad.numpy()[:, ::7, ::3, ::3], grad_x_norm=np.linalg.norm(xt.grad.numpy()),
+                grad_proj_w_sub=m.projection.weight.grad.numpy()[::3, ::3], grad_proj_b=m.projection.bias.grad.numpy(),
+                grad_logit_scale=m.logit_scale.grad.numpy(), text_features=m.text_features.numpy())
+
+
+def e2e_case(ref, layers: int, seed: int = 7, B: int = 2, counts=(37, 5)):
+    """F3/F4: full CLIP-EBC forward + DACE loss + backward on synthetic crops."""
+    m = build_ref_model(ref, layers=layers)
+    img, points, density = syn.synthetic_crops(B, 224, seed=seed, counts=list(counts))
+    x = torch.from_numpy(img)
+    feats = {}
+    h = m.image_encoder.ln_post.register_forward_hook(lambda mod, i, o: feats.__setitem__("ln_post", o.detach()))
+    m.train()
+    logits, exp = m(x)
+    h.remove()
+    loss_fn = ref.losses.DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=224)
+    loss, info = loss_fn(logits, exp, torch.from_numpy(density), [torch.from_numpy(p) for p in points])
+    loss.backward()
+    out = dict(layers=layers, seed=seed, counts=np.asarray(counts), logits=logits.detach().numpy(),
+               exp=exp.detach().numpy(), enc_out_sub=feats["ln_post"].numpy()[:, 1::3, ::2],
+               grad_vpt_sub=np.stack([getattr(m, f"vpt_{i}").grad.numpy() for i in range(layers)])[:, :, ::4],
+               grad_vpt_norm=np.asarray([np.linalg.norm(getattr(m, f"vpt_{i}").grad.numpy()) for i in range(layers)]),
+               grad_proj_w_sub=m.projection.weight.grad.numpy()[::3, ::3], grad_proj_b=m.projection.bias.grad.numpy(),
+               grad_logit_scale=m.logit_scale.grad.numpy(),
+               grad_dec_conv1_sub=m.image_decoder[0].conv1.weight.grad.numpy()[::5, ::5],
+               grad_dec_conv2_sub=m.image_decoder[0].conv2.weight.grad.numpy()[::5, ::5],
+               grad_dec_bn1_w=m.image_decoder[0].bn1.weight.grad.numpy(),
+               grad_dec_bn2_b=m.image_decoder[0].bn2.bias.grad.numpy())
+    for k, v in info.items():
+        out["info_" + k] = v.detach().numpy().reshape(())
+    m.eval()
+    with torch.no_grad():
+        out["exp_eval"] = m(x).numpy()
+    return out
+
+
+def sliding_case(ref):
+    """F5: sliding-window tiling + overlap averaging with a stub model (utils/eval_utils.py:26-96)."""
+    class Stub(torch.nn.Module):
+        reduction = 8
+        def forward(self, x):
+            return torch.nn.functional.avg_pool2d(x.mean(1, keepdim=True).abs(), 8)
+    out = {}
+    for i, (H, W, win, stride) in enumerate([(500, 700, 224, 224), (500, 700, 224, 112), (224, 448, 224, 224), (232, 240, 224, 112)]):
+        # image regenerable: PCG64(11 + i) standard normal [1,3,H,W]
+        img = np.random.Generator(np.random.PCG64(11 + i)).standard_normal((1, 3, H, W)).astype(np.float32)
+        pred = ref.eval_utils.sliding_window_predict(Stub(), torch.from_numpy(img), win, stride)
+        out[f"pred_{i}"] = pred.numpy()
+        out[f"cfg_{i}"] = np.asarray([H, W, win, stride])
+    return out
+
+
+def text_case(ref):
+    """F6: prompt tokens and text features (synthetic text-tower weights, seed 0)."""
+    mc = ref.model_mod
+    prompts_w = [sys.modules["models.clip.utils"].format_count(b[0] if b[0] == b[1] else b, "word") for b in BINS]
+    prompts_n = [sys.modules["models.clip.utils"].format_count(b[0] if b[0] == b[1] else b, "number") for b in BINS]
+    m = build_ref_model(ref, layers=1, prompt_type="word")
+    mn = build_ref_model(ref, layers=1, prompt_type="number")
+    return dict(prompts_word=np.asarray(prompts_w), prompts_number=np.asarray(prompts_n),
+                tokens_word=ref.tokenize(prompts_w).numpy(), tokens_number=ref.tokenize(prompts_n).numpy(),
+                text_features_word=m.text_features.numpy(), text_features_number=mn.text_features.numpy())
+
+
+def main():
+    torch.set_num_threads(8)
+    ref = load_reference()
+    save("f6_text.npz", **text_case(ref))
+    save("f1_loss_224.npz", **loss_case(ref, 224, [0, 1, 3, 10, 47, 200, 1000, 25], seed=101))
+    save("f1_loss_448.npz", **loss_case(ref, 448, [5, 0, 150, 2000], seed=202))
+    save("f2_head.npz", **head_case(ref))
+    save("f5_sliding.npz", **sliding_case(ref))
+    save("f4_e2e_l2.npz", **e2e_case(ref, layers=2))
+    save("f3_e2e_l12.npz", **e2e_case(ref, layers=12))
+
+
+if __name__ == "__main__":
+    main()

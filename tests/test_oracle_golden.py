@@ -1,0 +1,120 @@
+"""Pin the CPU oracle (oracle/) against the golden fixtures produced by running the reference.
+
+These run on CPU (`-m "not gpu"`).  Tolerances: the reference and the oracle are both fp32 with
+different summation orders; the C Sinkhorn accumulates in double.  Forward outputs agree to
+~1e-6 relative; gradients are compared in relative L2 norm because the BatchNorm backward of the
+decoder cancels a near-constant count-loss gradient (fp32 vs fp64 of the reference itself differs by
+~2e-3 max-relative there, see DESIGN.md "Parity tolerances").
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import ANCHORS_NWPU, BINS, golden, rel_l2, rel_max, split_points
+from oracle import ref
+from ebc_amd import synthetic as syn
+
+
+@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"])
+def test_sinkhorn_oracle_matches_reference(fixture):
+    d = golden(fixture)
+    size = int(d["size"])
+    offs = d["offsets"]
+    u_ref = d["u_flat"]
+    for b, p in enumerate(split_points(d)):
+        if len(p) == 0:
+            continue
+        r = ref.ot_crop(p, d["pred_density"][b, 0], size)
+        assert rel_max(r["beta"], d["beta"][b]) < 2e-6
+        assert rel_max(r["v"], d["v"][b]) < 2e-5
+        assert rel_max(r["ot_grad"], d["ot_grad"][b]) < 2e-6
+        assert rel_max(r["u"], u_ref[offs[b]:offs[b + 1]]) < 2e-5
+        ne = len(r["err"])
+        np.testing.assert_allclose(r["err"], d["err"][b][:ne], rtol=1e-4)
+        assert abs(r["wd"] - d["wd"][b]) <= 1e-5 * abs(d["wd"][b]) + 1e-6
+        assert r["iters"] == 100 and not r["rolled_back"]   # never converges at these shapes
+
+
+def test_sinkhorn_oracle_plan_small():
+    """P = u K v for crops with n <= 200 (bregman_pytorch.py:140)."""
+    d = golden("f1_loss_224.npz")
+    lib_pts = split_points(d)
+    for b, p in enumerate(lib_pts):
+        key = f"P_{b}"
+        if key not in d.files or len(p) == 0:
+            continue
+        r = ref.ot_crop(p, d["pred_density"][b, 0], 224)
+        g = 28
+        cood = np.arange(0, 224, 8, dtype=np.float32) + 4
+        x = p[:, :1]; y = p[:, 1:]
+        xd = -2 * (x * cood) + x * x + cood * cood
+        yd = -2 * (y * cood) + y * y + cood * cood
+        K = np.exp((yd[:, :, None] + xd[:, None, :]).reshape(len(p), -1) / -10.0)
+        P = r["u"][:, None] * K * r["v"][None, :]
+        assert rel_l2(P, d[key]) < 1e-5
+
+
+@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"])
+def test_dace_loss_oracle_matches_reference(fixture):
+    d = golden(fixture)
+    size = int(d["size"])
+    pts = split_points(d)
+    dens = np.stack([syn.point_map(p, size, size)[None] for p in pts])
+    pc = torch.tensor(d["pred_class"], requires_grad=True)
+    pd = torch.tensor(d["pred_density"], requires_grad=True)
+    loss, info = ref.dace_loss(pc, pd, torch.from_numpy(dens), pts, BINS, input_size=size)
+    loss.backward()
+    for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
+        assert abs(float(info[k]) - float(d["info_" + k])) <= 1e-5 * abs(float(d["info_" + k])) + 1e-4, k
+    assert abs(float(info["ot_loss"])) < 1e-3 and abs(float(d["info_ot_loss"])) < 1e-3   # ~0 by construction
+    assert rel_max(pc.grad.numpy(), d["grad_pred_class"]) < 1e-5
+    assert rel_max(pd.grad.numpy(), d["grad_pred_density"]) < 1e-5
+
+
+def test_head_oracle_matches_reference():
+    d = golden("f2_head.npz")
+    g = np.random.Generator(np.random.PCG64(int(d["seed"])))
+    X = np.maximum(g.standard_normal((2, 768, 28, 28)), 0).astype(np.float32)
+    R1 = g.standard_normal((2, 5, 28, 28)).astype(np.float32)
+    R2 = g.standard_normal((2, 1, 28, 28)).astype(np.float32)
+    p = ref.params_from_state(syn.trainable_state(0, layers=1))
+    xt = torch.tensor(X, requires_grad=True)
+    logits, exp = ref.head(p, xt, torch.from_numpy(d["text_features"]), ANCHORS_NWPU)
+    ((logits * torch.from_numpy(R1)).sum() + (exp * torch.from_numpy(R2)).sum()).backward()
+    assert rel_max(logits.detach().numpy(), d["logits"]) < 1e-5
+    assert rel_max(exp.detach().numpy(), d["exp"]) < 1e-5
+    assert rel_l2(xt.grad.numpy()[:, ::7, ::3, ::3], d["grad_x_sub"]) < 1e-5
+    assert rel_l2(p["projection.weight"].grad.numpy()[::3, ::3], d["grad_proj_w_sub"]) < 1e-5
+    assert rel_l2(p["projection.bias"].grad.numpy(), d["grad_proj_b"]) < 1e-5
+    assert abs(float(p["logit_scale"].grad) - float(d["grad_logit_scale"])) < 1e-4 * abs(float(d["grad_logit_scale"]))
+
+
+@pytest.mark.parametrize("fixture", ["f4_e2e_l2.npz", "f3_e2e_l12.npz"])
+def test_e2e_oracle_matches_reference(fixture):
+    d = golden(fixture)
+    L = int(d["layers"])
+    txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
+    p = ref.params_from_state(syn.full_state(0, layers=L, include_text=False))
+    img, pts, dens = syn.synthetic_crops(2, 224, seed=int(d["seed"]), counts=list(d["counts"]))
+    logits, exp, feats = ref.forward(p, torch.from_numpy(img), txt, ANCHORS_NWPU, L)
+    loss, info = ref.dace_loss(logits, exp, torch.from_numpy(dens), pts, BINS)
+    loss.backward()
+    assert rel_max(logits.detach().numpy(), d["logits"]) < 1e-5
+    assert rel_max(exp.detach().numpy(), d["exp"]) < 1e-5
+    enc = feats.detach().permute(0, 2, 3, 1).reshape(2, 196, 768).numpy()[:, ::3, ::2]
+    assert rel_max(enc, d["enc_out_sub"]) < 1e-5
+    for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
+        assert abs(float(info[k]) - float(d["info_" + k])) <= 1e-5 * abs(float(d["info_" + k])), k
+    gv = np.stack([p[f"vpt_{i}"].grad.numpy() for i in range(L)])
+    assert rel_l2(gv[:, :, ::4], d["grad_vpt_sub"]) < 5e-4   # reference fp32 vs fp64: 2e-4
+    assert rel_l2(p["projection.weight"].grad.numpy()[::3, ::3], d["grad_proj_w_sub"]) < 1e-4
+    assert rel_l2(p["image_decoder.0.conv1.weight"].grad.numpy()[::5, ::5], d["grad_dec_conv1_sub"]) < 5e-3
+    assert abs(float(p["logit_scale"].grad) - float(d["grad_logit_scale"])) < 1e-4 * abs(float(d["grad_logit_scale"]))
+
+
+def test_sliding_window_fixture_shapes():
+    """F5 fixture sanity (the assembler itself is tested in test_eval.py)."""
+    d = golden("f5_sliding.npz")
+    for i in range(4):
+        H, W, win, stride = d[f"cfg_{i}"]
+        assert d[f"pred_{i}"].shape == (1, 1, H // 8, W // 8)
