@@ -1,0 +1,75 @@
+"""ctypes binding of libebc_hip.so (the C-ABI declared in include/ebc_hip.h).
+
+The product path has no fallback: if the library or a HIP device is missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libebc_hip.so")
+
+EBC_F32, EBC_F16, EBC_BF16 = 0, 1, 2
+EBC_COUNT_DMCOUNT, EBC_COUNT_MAE, EBC_COUNT_MSE = 0, 1, 2
+_ERR = {-1: "EBC_E_ARG", -2: "EBC_E_LAUNCH", -3: "EBC_E_UNSUPPORTED"}
+
+_lib: Optional[ctypes.CDLL] = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_Z = ctypes.c_size_t
+
+# name -> (restype, argtypes); must mirror include/ebc_hip.h
+SIGNATURES = {
+    "ebc_version": (_I, []),
+    "ebc_dace_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "ebc_dace_loss": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _I, _F, _I,
+                           _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
+}
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the library (host-side symbols only; no device work)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise RuntimeError(f"libebc_hip.so not built at {path}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def lib() -> ctypes.CDLL:
+    """The library, for a compute call: requires a HIP device."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("ebc_amd: no HIP device visible; the MI355X path has no CPU fallback")
+    return load()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {_ERR.get(rc, rc)}")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous(), "ebc_amd kernels take contiguous device tensors"
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    return {torch.float32: EBC_F32, torch.float16: EBC_F16, torch.bfloat16: EBC_BF16}[dt]

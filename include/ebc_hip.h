@@ -1,0 +1,71 @@
+/*
+ * libebc_hip.so — C-ABI of the MI355X-native CLIP-EBC hot path (gfx950 / CDNA4).
+ *
+ * The reference (Yiming-M/CLIP-EBC) is pure Python on PyTorch; it has no FFI.  Its boundary
+ * is the Python API.  These entry points are what that API binds to through
+ * ctypes (clip-ebc_amd/ebc_amd/_lib.py); each cites the reference interface it replaces.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is caller-owned DEVICE memory (torch-allocated), except where noted;
+ *   - no allocation, no host<->device synchronisation, no device sync inside a call; work is
+ *     enqueued on `stream` (a hipStream_t passed as void*), so calls are graph-capturable;
+ *   - return 0 (EBC_OK) or a negative EBC_E_* code; numerical roll-backs are reported per
+ *     crop through `status`, never as an error;
+ *   - `dtype` selects the GEMM/attention input type: EBC_F32 (parity mode, exact-f32 MFMA),
+ *     EBC_F16 (the reference's AMP dtype) or EBC_BF16.
+ */
+#ifndef EBC_HIP_H
+#define EBC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* ebc_stream_t;
+
+enum { EBC_F32 = 0, EBC_F16 = 1, EBC_BF16 = 2 };
+enum { EBC_OK = 0, EBC_E_ARG = -1, EBC_E_LAUNCH = -2, EBC_E_UNSUPPORTED = -3 };
+enum { EBC_COUNT_DMCOUNT = 0, EBC_COUNT_MAE = 1, EBC_COUNT_MSE = 2 };
+
+/* Library version / self-description (host-only, no device work). */
+int ebc_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * DACE loss with DMCount, fused, one workgroup per crop, all Sinkhorn iterations on device.
+ *
+ * Replaces DACELoss.forward (losses/dace_loss.py:49-70) with its DMLoss
+ * (losses/dm_loss.py:99-124), OTLoss (losses/dm_loss.py:38-79) and
+ * sinkhorn (losses/bregman_pytorch.py:11-144), forward AND backward:
+ *   pred_class     [B, N, g, g] f32 logits      (g = size / reduction)
+ *   pred_density   [B, 1, g, g] f32
+ *   target_density [B, 1, size, size] f32 dot map (or already [B,1,g,g] if target_is_reduced)
+ *   points         [sum(n_b), 2] f32 (x, y) pixels, packed;  offsets [B+1] int32 (device)
+ *   bins_lo/hi     [N] f32 (device), inclusive bins; hi may be +inf
+ *   order          [B] int32 (device) crop processing order (heaviest first), or NULL
+ * Outputs:
+ *   grad_class   [B, N, g, g]  d loss / d pred_class  (for upstream grad 1)
+ *   grad_density [B, 1, g, g]  d loss / d pred_density
+ *   losses       [5] f32: loss, ot_loss, tv_loss, count_loss, ce_loss (loss_info keys)
+ *   crop_stats   [B, 8] f32: ce_b, tv_b*n_b, count_b, ot_b, wd_b, iters, rolled_back, err_last
+ *   beta_out     [B, g*g] f32 or NULL;  status [B] int32 or NULL (iterations, negative = rollback)
+ * count_mode: EBC_COUNT_DMCOUNT / _MAE / _MSE (DACELoss count_loss="dmcount"/"mae"/"mse").
+ * norm_cood: OTLoss norm_cood (dm_loss.py:31-34,51): coordinates mapped to [-1, 1].
+ * workspace: ebc_dace_workspace_bytes(...) bytes of device memory.
+ */
+size_t ebc_dace_workspace_bytes(int B, int total_points, int size, int reduction);
+int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,
+                  int target_is_reduced, const float* points, const int* offsets, const int* order,
+                  const float* bins_lo, const float* bins_hi, int B, int N, int size, int reduction,
+                  int count_mode, int norm_cood, float weight_count_loss, float weight_ot, float weight_tv,
+                  float reg, int max_iter, float stop_thr, int eval_freq,
+                  float* grad_class, float* grad_density, float* losses, float* crop_stats,
+                  float* beta_out, int* status, void* workspace, size_t workspace_bytes,
+                  ebc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EBC_HIP_H */

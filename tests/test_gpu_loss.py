@@ -1,0 +1,109 @@
+"""GPU parity: fused DACE/DMCount kernel vs the golden fixtures and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import BINS, golden, rel_l2, rel_max, split_points
+from oracle import ref
+from ebc_amd import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pred_class, pred_density, target_density, points, size, count_loss="dmcount", reduced=False):
+    from ebc_amd.losses import DACELoss
+    dev = torch.device("cuda:0")
+    fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss=count_loss, input_size=size)
+    pc = torch.tensor(pred_class, device=dev, requires_grad=True)
+    pd = torch.tensor(pred_density, device=dev, requires_grad=True)
+    td = torch.from_numpy(target_density).to(dev)
+    if reduced:
+        td = ref.reshape_density(td, 8)
+    loss, info = fn(pc, pd, td, [torch.from_numpy(p).to(dev) for p in points])
+    loss.backward()
+    torch.cuda.synchronize()
+    return float(loss), {k: float(v) for k, v in info.items()}, pc.grad.cpu().numpy(), pd.grad.cpu().numpy()
+
+
+@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"])
+def test_dace_kernel_matches_reference_fixture(fixture):
+    d = golden(fixture)
+    size = int(d["size"])
+    pts = split_points(d)
+    dens = np.stack([syn.point_map(p, size, size)[None] for p in pts])
+    loss, info, gc, gd = _run(d["pred_class"], d["pred_density"], dens, pts, size)
+    for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
+        assert abs(info[k] - float(d["info_" + k])) <= 2e-5 * abs(float(d["info_" + k])) + 1e-4, (k, info[k])
+    assert abs(info["ot_loss"]) < 1e-3
+    assert rel_max(gc, d["grad_pred_class"]) < 1e-5
+    # OT gradient through the separable kernel: K rounding differs from exp(C/-reg) by ~ulp(C)/reg
+    assert rel_max(gd, d["grad_pred_density"]) < 1e-4
+    assert rel_l2(gd, d["grad_pred_density"]) < 2e-5
+
+
+def _random_batch(B, size, seed, counts=None):
+    g = np.random.Generator(np.random.PCG64(seed))
+    h = size // 8
+    if counts is None:
+        counts = np.clip(np.floor(g.lognormal(np.log(20.0), 1.2, B)), 0, 2048).astype(int).tolist()
+    pts = [(g.random((n, 2)) * size).astype(np.float32) for n in counts]
+    dens = np.stack([syn.point_map(p, size, size)[None] for p in pts])
+    pcl = g.standard_normal((B, 5, h, h)).astype(np.float32)
+    pde = (g.random((B, 1, h, h)) * 2.0).astype(np.float32)
+    return pcl, pde, dens, pts
+
+
+def _oracle(pcl, pde, dens, pts, size, count_loss="dmcount"):
+    pc = torch.tensor(pcl, requires_grad=True)
+    pd = torch.tensor(pde, requires_grad=True)
+    if count_loss == "dmcount":
+        loss, info = ref.dace_loss(pc, pd, torch.from_numpy(dens), pts, BINS, input_size=size)
+    else:
+        td = ref.reshape_density(torch.from_numpy(dens), 8)
+        ce = torch.nn.functional.cross_entropy(pc, ref.bin_count(td, BINS), reduction="none").sum(dim=(-1, -2)).mean()
+        diff = pd - td
+        cnt = (diff.abs() if count_loss == "mae" else diff * diff).sum(dim=(-1, -2, -3)).mean()
+        loss = ce + cnt
+        info = {"loss": loss, "ce_loss": ce, f"{count_loss}_loss": cnt}
+    loss.backward()
+    return float(loss), {k: float(v) for k, v in info.items()}, pc.grad.numpy(), pd.grad.numpy()
+
+
+@pytest.mark.parametrize("size,counts", [
+    (224, None),                                  # lognormal ragged batch, 16 crops
+    (224, [0, 0, 0, 0]),                          # empty crops: OT skipped (dm_loss.py:49)
+    (224, [600, 1, 2048, 473, 474, 475, 3]),      # around / above the LDS capacity (global factors)
+    (448, [0, 130, 127, 129, 900, 2]),            # g = 56
+])
+def test_dace_kernel_matches_oracle(size, counts):
+    B = 16 if counts is None else len(counts)
+    pcl, pde, dens, pts = _random_batch(B, size, seed=3 + size, counts=counts)
+    loss, info, gc, gd = _run(pcl, pde, dens, pts, size)
+    oloss, oinfo, ogc, ogd = _oracle(pcl, pde, dens, pts, size)
+    for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
+        assert abs(info[k] - oinfo[k]) <= 2e-5 * abs(oinfo[k]) + 1e-4, (k, info[k], oinfo[k])
+    assert rel_max(gc, ogc) < 1e-5
+    assert rel_l2(gd, ogd) < 2e-5
+
+
+@pytest.mark.parametrize("mode", ["mae", "mse"])
+def test_dace_kernel_count_modes(mode):
+    pcl, pde, dens, pts = _random_batch(6, 224, seed=9)
+    loss, info, gc, gd = _run(pcl, pde, dens, pts, 224, count_loss=mode)
+    oloss, oinfo, ogc, ogd = _oracle(pcl, pde, dens, pts, 224, count_loss=mode)
+    assert abs(loss - oloss) <= 1e-5 * abs(oloss)
+    assert abs(info[f"{mode}_loss"] - oinfo[f"{mode}_loss"]) <= 1e-5 * abs(oinfo[f"{mode}_loss"])
+    assert rel_max(gc, ogc) < 1e-5 and rel_max(gd, ogd) < 1e-5
+
+
+def test_dace_kernel_reduced_target_and_dmloss():
+    from ebc_amd.losses import DMLoss
+    pcl, pde, dens, pts = _random_batch(5, 224, seed=12)
+    a = _run(pcl, pde, dens, pts, 224)
+    b = _run(pcl, pde, dens, pts, 224, reduced=True)
+    assert a[0] == pytest.approx(b[0], rel=1e-6)
+    np.testing.assert_allclose(a[3], b[3], rtol=1e-6, atol=1e-9)
+    dev = torch.device("cuda:0")
+    pd = torch.tensor(pde, device=dev, requires_grad=True)
+    loss, info = DMLoss(224, 8)(pd, torch.from_numpy(dens).to(dev), [torch.from_numpy(p).to(dev) for p in pts])
+    assert float(loss) == pytest.approx(a[1]["loss"] - a[1]["ce_loss"], rel=1e-5)
