@@ -30,6 +30,7 @@ SIGNATURES = {
     "ebc_dace_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "ebc_dace_loss": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _I, _F, _I,
                            _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
+    "ebc_gemm": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
 }
 
 

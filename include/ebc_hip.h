@@ -65,6 +65,20 @@ int ebc_dace_loss(const float* pred_class, const float* pred_density, const floa
                   float* beta_out, int* status, void* workspace, size_t workspace_bytes,
                   ebc_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * GEMM  C[M,N] = A[M,K] . B[N,K]^T (+bias[N]) with a fused epilogue.  A, B of `dtype`; K % 64 == 0
+ * (K % 32 for f32), N % 64 == 0.  Replaces the nn.Linear / nn.MultiheadAttention projections of
+ * ResidualAttentionBlock (models/clip/_clip/blocks.py:22-42), the patch-embed conv1
+ * (image_encoder.py:141, as im2col-GEMM) and the 1x1 projection (models/clip/model.py:91-95).
+ *   epilogue 0 STORE:    C = acc + bias                      (C of dtype, or f32 if out_f32)
+ *   epilogue 1 GELU:     aux = acc + bias; C = QuickGELU(aux) (blocks.py:17-19)
+ *   epilogue 2 RESID:    C(f32) = resid(f32) + acc + bias     (residual stream, may be in place)
+ *   epilogue 3 GELU_BWD: C = acc * QuickGELU'(aux)           (MLP backward, dX only)
+ */
+enum { EBC_EPI_STORE = 0, EBC_EPI_GELU = 1, EBC_EPI_RESID = 2, EBC_EPI_GELU_BWD = 3 };
+int ebc_gemm(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
+             const float* bias, const float* resid, void* aux, int M, int N, int K, ebc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

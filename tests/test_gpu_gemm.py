@@ -1,0 +1,90 @@
+"""GPU numerics of the MFMA GEMM (all epilogues, f32/f16/bf16) against a torch fp64 reference."""
+import pytest
+import torch
+
+from ebc_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}
+TOL = {"f32": 2e-6, "f16": 2e-3, "bf16": 1.6e-2}
+
+
+def _gemm(dt, epi, out_f32, A, B, bias=None, resid=None, aux=None, C=None):
+    M, K = A.shape
+    N = B.shape[0]
+    if C is None:
+        od = torch.float32 if (out_f32 or dt == torch.float32 or epi == 2) else dt
+        C = torch.empty(M, N, device=A.device, dtype=od)
+    rc = _lib.lib().ebc_gemm(_lib.dtype_code(dt), epi, int(out_f32), _lib.ptr(A), _lib.ptr(B), _lib.ptr(C),
+                             _lib.ptr(bias), _lib.ptr(resid), _lib.ptr(aux), M, N, K, _lib.stream())
+    _lib.check(rc, "ebc_gemm")
+    return C
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm())
+
+
+@pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(3664, 2304, 768), (458, 768, 3072), (37, 128, 64), (1000, 512, 768), (3664, 768, 768)])
+def test_gemm_store_bias(dname, M, N, K):
+    if dname == "f32" and K % 32:
+        pytest.skip()
+    dt = DT[dname]
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda", generator=g).to(dt)
+    B = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(dt)
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref = A.double() @ B.double().t() + bias.double()
+    C = _gemm(dt, 0, 1, A, B, bias=bias)
+    assert _rel(C, ref) < TOL[dname]
+    if dt != torch.float32:
+        C16 = _gemm(dt, 0, 0, A, B, bias=bias)
+        assert C16.dtype == dt and _rel(C16, ref) < 2 * TOL[dname] + 4e-3
+
+
+@pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
+def test_gemm_gelu_and_backward(dname):
+    dt = DT[dname]
+    M, N, K = 777, 3072, 768
+    g = torch.Generator(device="cuda").manual_seed(7)
+    A = torch.randn(M, K, device="cuda", generator=g).to(dt)
+    B = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(dt)
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    aux = torch.empty(M, N, device="cuda", dtype=dt)
+    C = _gemm(dt, 1, 0, A, B, bias=bias, aux=aux)
+    pre = A.double() @ B.double().t() + bias.double()
+    ref = pre * torch.sigmoid(1.702 * pre)
+    assert _rel(aux, pre) < TOL[dname] + (4e-3 if dt != torch.float32 else 0)
+    assert _rel(C, ref) < TOL[dname] + (4e-3 if dt != torch.float32 else 0)
+    # backward: dA = (dG . W2) * gelu'(pre)
+    W2t = (torch.randn(N, 768, device="cuda", generator=g) / 768 ** 0.5).to(dt)   # [N_out=3072, K=768]
+    dG = torch.randn(M, 768, device="cuda", generator=g).to(dt)
+    D = _gemm(dt, 3, 0, dG, W2t, aux=aux)
+    a = aux.double()
+    s = torch.sigmoid(1.702 * a)
+    ref_d = (dG.double() @ W2t.double().t()) * (s + 1.702 * a * s * (1 - s))
+    assert _rel(D, ref_d) < TOL[dname] + (4e-3 if dt != torch.float32 else 0)
+
+
+@pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
+def test_gemm_residual_inplace(dname):
+    dt = DT[dname]
+    M, N, K = 3664, 768, 3072
+    g = torch.Generator(device="cuda").manual_seed(11)
+    A = torch.randn(M, K, device="cuda", generator=g).to(dt)
+    B = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(dt)
+    bias = torch.randn(N, device="cuda", generator=g)
+    X = torch.randn(M, N, device="cuda", generator=g)
+    ref = X.double() + A.double() @ B.double().t() + bias.double()
+    _gemm(dt, 2, 1, A, B, bias=bias, resid=X, C=X)
+    assert _rel(X, ref) < TOL[dname]
+
+
+def test_gemm_rejects_bad_shapes():
+    A = torch.zeros(16, 48, device="cuda", dtype=torch.float16)
+    B = torch.zeros(64, 48, device="cuda", dtype=torch.float16)
+    C = torch.zeros(16, 64, device="cuda", dtype=torch.float16)
+    rc = _lib.lib().ebc_gemm(1, 0, 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), None, None, None, 16, 64, 48, _lib.stream())
+    assert rc == -1
