@@ -1,0 +1,358 @@
+// Multi-head self-attention for the CLIP ViT-B/16 + VPT encoder on gfx950: forward, and the
+// FA2-style backward split into a dQ kernel and a dK/dV kernel (no atomics).
+//
+// Reference: nn.MultiheadAttention(d_model=768, n_head=12) called as attn(x, x, x,
+// need_weights=False) in ResidualAttentionBlock.attention (models/clip/_clip/blocks.py:35-37),
+// i.e. softmax(Q K^T / sqrt(64)) V per head with the packed in-projection layout
+// qkv[row] = [q(768) | k(768) | v(768)], head h at columns h*64 .. h*64+63.
+//
+// The sequence is short (1 CLS + 32 VPT + 196 patches = 229 tokens), so a workgroup keeps the
+// whole K and V (or Q and dO) of one (crop, head) in LDS, padded to LP = 256 rows with a
+// 144-byte row pitch (conflict-free for both ds_read_b128 row reads and ds_read_b64_tr_b16
+// column reads); scores for 16 query rows x 256 keys live in registers, so no online softmax.
+// Operand orientation ("swapped" S^T = K Q^T) puts each query on one lane, so the probability
+// accumulators are directly the A operand of P.V with no LDS round trip (mfma.h).
+//   grid: B * H * ceil(L/64) workgroups of 4 waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
+#include "ebc_common.h"
+#include "mfma.h"
+
+using namespace ebc;
+
+namespace {
+
+constexpr int HD = 64;          // head dim
+constexpr int LP = 256;         // padded sequence (>= L)
+constexpr int NKT = LP / 16;    // 16-row tiles
+
+template <class E> struct AttnCfg {
+    using T = typename E::T;
+    static constexpr int EB = E::BYTES;
+    static constexpr int LDR = HD + 16 / EB;                 // row pitch in elements (144 B / 272 B)
+    static constexpr int CPR = HD * EB / 16;                 // 16-B chunks per row
+    static constexpr size_t TILE_BYTES = (size_t)LP * LDR * EB;
+};
+
+template <class E>
+__device__ __forceinline__ void load_rows(typename E::T* dst, const typename E::T* src, int ld, int L)
+{
+    // dst[s][0..63] = src[s*ld + 0..63] for s < L, zero for L <= s < LP
+    using C = AttnCfg<E>;
+    for (int e = threadIdx.x; e < LP * C::CPR; e += blockDim.x) {
+        const int s = e / C::CPR, c = e % C::CPR;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (s < L) v = *reinterpret_cast<const uint4*>(src + (size_t)s * ld + c * (16 / C::EB));
+        *reinterpret_cast<uint4*>(dst + s * C::LDR + c * (16 / C::EB)) = v;
+    }
+}
+
+// 8 contiguous elements of a global row (zeros when !valid)
+template <class E>
+__device__ __forceinline__ typename E::Frag gload8(const typename E::T* p, bool valid) {
+    if (valid) return load8<E>(p);
+    typename E::Frag z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = E::from(0.f);
+    return z;
+}
+
+template <class E>
+__device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* base, int row, int col) {
+    return load8<E>(base + row * AttnCfg<E>::LDR + col);
+}
+
+// ------------------------------------------------------------------------------ forward
+template <class E>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const typename E::T* __restrict__ qkv, typename E::T* __restrict__ out,
+                                                       float* __restrict__ lse, int B, int L, int H, float scale)
+{
+    using T = typename E::T;
+    using C = AttnCfg<E>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Ks = reinterpret_cast<T*>(smem);
+    T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    const int nqb = (L + 63) / 64;
+    const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+    const int b = bh / H, h = bh % H;
+    const int D3 = 3 * H * HD, D = H * HD;
+    const T* base = qkv + (size_t)b * L * D3 + h * HD;
+    load_rows<E>(Ks, base + D, D3, L);
+    load_rows<E>(Vs, base + 2 * D, D3, L);
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+    const int q0 = qb * 64 + w * 16;
+    const int qme = q0 + fr;                                   // this lane's query (column of S^T)
+    typename E::Frag qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qme < L);
+    __syncthreads();
+
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+        s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) s[kt] = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], s[kt]);
+    }
+    // s[kt][i] = S[q = qme][key = 16 kt + 4 fg + i]
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int key = 16 * kt + 4 * fg + i;
+            s[kt][i] = key < L ? s[kt][i] * scale : -INFINITY;
+            mx = fmaxf(mx, s[kt][i]);
+        }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { s[kt][i] = expf(s[kt][i] - mx); sum += s[kt][i]; }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+
+    f32x4 o[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < NKT / 2; ++st) {
+        const float pv[8] = {s[2 * st][0], s[2 * st][1], s[2 * st][2], s[2 * st][3],
+                             s[2 * st + 1][0], s[2 * st + 1][1], s[2 * st + 1][2], s[2 * st + 1][3]};
+        const typename E::Frag pf = pack8<E>(pv);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) o[dt] = mma(pf, load_colfrag<E>(Vs, C::LDR, 32 * st, 16 * dt), o[dt]);
+    }
+    // o[dt][i] = O[q = q0 + 4 fg + i][d = 16 dt + fr]; divide by the row sum held on lane (q - q0)
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ql = 4 * fg + i;
+        const float iv = __shfl(inv, ql, 64);
+        const int q = q0 + ql;
+        if (q < L) {
+            T* orow = out + ((size_t)b * L + q) * D + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) orow[16 * dt + fr] = E::from(o[dt][i] * iv);
+        }
+    }
+    if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx + logf(sum);
+}
+
+// ------------------------------------------------------------------------------ backward dQ
+template <class E>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                                          typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
+{
+    using T = typename E::T;
+    using C = AttnCfg<E>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Ks = reinterpret_cast<T*>(smem);
+    T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    const int nqb = (L + 63) / 64;
+    const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+    const int b = bh / H, h = bh % H;
+    const int D3 = 3 * H * HD, D = H * HD;
+    const T* base = qkv + (size_t)b * L * D3 + h * HD;
+    load_rows<E>(Ks, base + D, D3, L);
+    load_rows<E>(Vs, base + 2 * D, D3, L);
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+    const int q0 = qb * 64 + w * 16;
+    const int qme = q0 + fr;
+    const bool qv = qme < L;
+    typename E::Frag qf[2], df[2];
+    const T* drow = dout + ((size_t)b * L + qme) * D + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qv);
+        df[ks] = gload8<E>(drow + 32 * ks + 8 * fg, qv);
+    }
+    const float lq = qv ? lse[((size_t)b * H + h) * L + qme] : INFINITY;
+    const float dq = qv ? delta[((size_t)b * H + h) * L + qme] : 0.f;
+    __syncthreads();
+
+    f32x4 dq_acc[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < NKT / 2; ++st) {
+        float ds[8];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int kt = 2 * st + hf;
+            f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                sv = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], sv);
+                pv = mma(lds_rowfrag<E>(Vs, 16 * kt + fr, 32 * ks + 8 * fg), df[ks], pv);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int key = 16 * kt + 4 * fg + i;
+                const float p = key < L ? expf(sv[i] * scale - lq) : 0.f;
+                ds[4 * hf + i] = p * (pv[i] - dq);
+            }
+        }
+        const typename E::Frag dsf = pack8<E>(ds);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, load_colfrag<E>(Ks, C::LDR, 32 * st, 16 * dt), dq_acc[dt]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = q0 + 4 * fg + i;
+        if (q < L) {
+            T* row = dqkv + ((size_t)b * L + q) * D3 + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) row[16 * dt + fr] = E::from(dq_acc[dt][i] * scale);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ backward dK, dV
+template <class E>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                           const float* __restrict__ lse, const float* __restrict__ delta,
+                                                           typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
+{
+    using T = typename E::T;
+    using C = AttnCfg<E>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Qs = reinterpret_cast<T*>(smem);
+    T* Ds = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    float* ls = reinterpret_cast<float*>(smem + 2 * C::TILE_BYTES);
+    float* dl = ls + LP;
+    const int nkb = (L + 63) / 64;
+    const int bh = blockIdx.x / nkb, kb = blockIdx.x % nkb;
+    const int b = bh / H, h = bh % H;
+    const int D3 = 3 * H * HD, D = H * HD;
+    const T* base = qkv + (size_t)b * L * D3 + h * HD;
+    load_rows<E>(Qs, base, D3, L);
+    load_rows<E>(Ds, dout + (size_t)b * L * D + h * HD, D, L);
+    for (int q = threadIdx.x; q < LP; q += blockDim.x) {
+        ls[q] = q < L ? lse[((size_t)b * H + h) * L + q] : INFINITY;
+        dl[q] = q < L ? delta[((size_t)b * H + h) * L + q] : 0.f;
+    }
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+    const int k0 = kb * 64 + w * 16;
+    const int kme = k0 + fr;
+    const bool kv = kme < L;
+    typename E::Frag kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        kf[ks] = gload8<E>(base + (size_t)kme * D3 + D + 32 * ks + 8 * fg, kv);
+        vf[ks] = gload8<E>(base + (size_t)kme * D3 + 2 * D + 32 * ks + 8 * fg, kv);
+    }
+    __syncthreads();
+
+    f32x4 dk[HD / 16], dv[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll 2
+    for (int st = 0; st < NKT / 2; ++st) {
+        float pp[8], ds[8];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int qt = 2 * st + hf;
+            f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                sv = mma(lds_rowfrag<E>(Qs, 16 * qt + fr, 32 * ks + 8 * fg), kf[ks], sv);   // S^T[q][key]
+                pv = mma(lds_rowfrag<E>(Ds, 16 * qt + fr, 32 * ks + 8 * fg), vf[ks], pv);   // dP^T[q][key]
+            }
+            const float4 l4 = *reinterpret_cast<const float4*>(ls + 16 * qt + 4 * fg);
+            const float4 d4 = *reinterpret_cast<const float4*>(dl + 16 * qt + 4 * fg);
+            const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float p = expf(sv[i] * scale - lq[i]);     // lse = +inf for padded queries -> 0
+                pp[4 * hf + i] = p;
+                ds[4 * hf + i] = p * (pv[i] - dq[i]);
+            }
+        }
+        const typename E::Frag pf = pack8<E>(pp), dsf = pack8<E>(ds);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+            dv[dt] = mma(pf, load_colfrag<E>(Ds, C::LDR, 32 * st, 16 * dt), dv[dt]);
+            dk[dt] = mma(dsf, load_colfrag<E>(Qs, C::LDR, 32 * st, 16 * dt), dk[dt]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int key = k0 + 4 * fg + i;
+        if (key < L) {
+            T* row = dqkv + ((size_t)b * L + key) * D3 + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) {
+                row[D + 16 * dt + fr] = E::from(dk[dt][i] * scale);
+                row[2 * D + 16 * dt + fr] = E::from(dv[dt][i]);
+            }
+        }
+    }
+}
+
+template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+{
+    using C = AttnCfg<E>;
+    const size_t lds = 2 * C::TILE_BYTES;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)attn_fwd_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
+        attr = true;
+    }
+    const int grid = B * H * ((L + 63) / 64);
+    hipLaunchKernelGGL(attn_fwd_kernel<E>, dim3(grid), dim3(256), lds, st, (const typename E::T*)qkv,
+                       (typename E::T*)out, lse, B, L, H, 0.125f);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+template <class E> int attn_bwd_t(const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
+                                  int B, int L, int H, hipStream_t st)
+{
+    using C = AttnCfg<E>;
+    const size_t lds_dq = 2 * C::TILE_BYTES, lds_kv = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dq) != hipSuccess) return EBC_E_LAUNCH;
+        if (hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv) != hipSuccess) return EBC_E_LAUNCH;
+        attr = true;
+    }
+    const int grid = B * H * ((L + 63) / 64);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<E>, dim3(grid), dim3(256), lds_dq, st, (const typename E::T*)qkv,
+                       (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
+    EBC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<E>, dim3(grid), dim3(256), lds_kv, st, (const typename E::T*)qkv,
+                       (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+}  // namespace
+
+namespace ebc {
+int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+{
+    if (L <= 0 || L > LP || B <= 0 || H <= 0) return EBC_E_UNSUPPORTED;
+    switch (dtype) {
+        case EBC_F32: return attn_fwd_t<EF32>(qkv, out, lse, B, L, H, st);
+        case EBC_F16: return attn_fwd_t<EF16>(qkv, out, lse, B, L, H, st);
+        case EBC_BF16: return attn_fwd_t<EBF16>(qkv, out, lse, B, L, H, st);
+    }
+    return EBC_E_ARG;
+}
+int attention_bwd(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
+                  int B, int L, int H, hipStream_t st)
+{
+    if (L <= 0 || L > LP || B <= 0 || H <= 0) return EBC_E_UNSUPPORTED;
+    switch (dtype) {
+        case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, lse, delta, dqkv, B, L, H, st);
+        case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, lse, delta, dqkv, B, L, H, st);
+        case EBC_BF16: return attn_bwd_t<EBF16>(qkv, dout, lse, delta, dqkv, B, L, H, st);
+    }
+    return EBC_E_ARG;
+}
+}  // namespace ebc

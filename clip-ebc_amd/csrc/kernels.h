@@ -1,0 +1,36 @@
+// Internal launchers shared by the C-ABI entry points and the ViT orchestrator.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace ebc {
+int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
+            const float* resid, void* aux, int M, int N, int K, hipStream_t st);
+int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,
+                  void* out, float* outf, float* mean, float* rstd, int M, int D, hipStream_t st);
+int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg, int gstride, int goff,
+                  const float* mean, const float* rstd, const float* gamma, const float* dx_in, float* dx_out,
+                  void* dx_out_t, int M, int D, hipStream_t st);
+int im2col(int dtype, const float* x, void* out, int B, int H, int W, int P, hipStream_t st);
+int embed_tokens(const float* patch, const float* cls, const float* pos, const float* gamma, const float* beta,
+                 const float* vpt, long vpt_bstride, float* X, int B, int L, int G, int NVPT, int D, hipStream_t st);
+int insert_vpt(float* X, const float* vpt, long vpt_bstride, int B, int L, int NVPT, int D, hipStream_t st);
+int vpt_grad(int dtype, float* dX, void* dXt, float* dvpt, int B, int L, int NVPT, int D, int per_batch, int accumulate,
+             hipStream_t st);
+int head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+             float* logits, float* expo, int P, int HW, int NB, hipStream_t st);
+int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+             const float* dlogits, const float* dexp, const float* gscale, void* dZ, float* dbias, float* dscale,
+             int P, int HW, int NB, hipStream_t st);
+int attn_delta(int dtype, const void* dO, const void* O, float* delta, int B, int L, int H, hipStream_t st);
+int cast_f32(int dtype, const float* in, void* out, size_t n, hipStream_t st);
+int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st);
+int attention_bwd(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
+                  int B, int L, int H, hipStream_t st);
+}  // namespace ebc
+
+#define EBC_TRY(x)                  \
+    do {                            \
+        int _rc = (x);              \
+        if (_rc != 0) return _rc;   \
+    } while (0)

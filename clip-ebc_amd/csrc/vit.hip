@@ -1,0 +1,241 @@
+// Host-side orchestration of the CLIP ViT-B/16 + deep-VPT encoder (forward, and dX-only backward
+// with the per-layer VPT gradients), plus the C-ABI wrappers of the individual kernels.
+//
+// Reference: CLIP_EBC._forward_vpt   models/clip/model.py:142-189
+//            ResidualAttentionBlock  models/clip/_clip/blocks.py:22-42
+//
+// Layout in HBM (M = B * L rows, L = 1 + NV + G tokens, row-major [B][L][768]):
+//   X_l   f32 [M,768]  residual stream entering block l (rows 1..NV hold vpt_l)   l = 0..layers
+//   X1_l  f32 [M,768]  after the attention half of block l
+//   QKV_l T   [M,2304] packed in-projection output,  O_l T [M,768] attention output
+//   A_l   T   [M,3072] MLP pre-activation (for QuickGELU')
+//   mean/rstd of ln_1, ln_2 per row; lse_l [B,H,L] softmax log-normalisers
+// The persistent [B, L, 768] buffer replaces the reference's 24 torch.cat per step: VPT rows are
+// overwritten in place before each block (and their gradient rows reduced + zeroed in backward).
+#include <vector>
+
+#include "ebc_common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int WIDTH = 768, HEADS = 12, MLP = 3072, QKVW = 3 * WIDTH;
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Carver {
+    char* base; size_t off = 0; bool dry;
+    Carver(void* b, bool d) : base((char*)b), dry(d) {}
+    template <class P> P* take(size_t bytes) {
+        P* p = dry ? nullptr : reinterpret_cast<P*>(base + off);
+        off += align_up(bytes);
+        return p;
+    }
+};
+
+struct LayerSave {
+    float *X1, *m1, *r1, *m2, *r2, *lse;
+    void *QKV, *O, *A;
+};
+
+struct Layout {
+    std::vector<float*> X;          // layers + 1
+    std::vector<LayerSave> s;       // layers
+    void *H, *G, *patch_t;          // transient
+    float *patch_f, *mpost, *rpost;
+    // backward transients
+    float *dXa, *dXb, *delta;
+    void *dXt, *dH, *dA, *dO, *dQKV;
+    size_t bytes;
+};
+
+Layout carve(void* ws, int B, int L, int G, int layers, int dtype, int training)
+{
+    const size_t M = (size_t)B * L;
+    const size_t es = dtype == EBC_F32 ? 4 : 2;
+    Carver c(ws, ws == nullptr);
+    Layout lay;
+    const int nsave = training ? layers : 1;
+    lay.X.resize(layers + 1);
+    for (int l = 0; l <= layers; ++l)
+        lay.X[l] = (training || l < 2) ? c.take<float>(M * WIDTH * 4) : lay.X[l & 1];
+    if (!training) for (int l = 2; l <= layers; ++l) lay.X[l] = lay.X[l & 1];
+    lay.s.resize(layers);
+    for (int l = 0; l < layers; ++l) {
+        LayerSave& s = lay.s[l];
+        if (l < nsave) {
+            s.X1 = c.take<float>(M * WIDTH * 4);
+            s.m1 = c.take<float>(M * 4); s.r1 = c.take<float>(M * 4);
+            s.m2 = c.take<float>(M * 4); s.r2 = c.take<float>(M * 4);
+            s.lse = c.take<float>((size_t)B * HEADS * L * 4);
+            s.QKV = c.take<void>(M * QKVW * es);
+            s.O = c.take<void>(M * WIDTH * es);
+            s.A = c.take<void>(M * MLP * es);
+        } else {
+            s = lay.s[0];
+        }
+    }
+    lay.H = c.take<void>(M * WIDTH * es);
+    lay.G = c.take<void>(M * MLP * es);
+    lay.patch_t = c.take<void>((size_t)B * G * WIDTH * es);
+    lay.patch_f = c.take<float>((size_t)B * G * WIDTH * 4);
+    lay.mpost = c.take<float>((size_t)B * G * 4);
+    lay.rpost = c.take<float>((size_t)B * G * 4);
+    if (training) {
+        lay.dXa = c.take<float>(M * WIDTH * 4);
+        lay.dXb = c.take<float>(M * WIDTH * 4);
+        lay.delta = c.take<float>((size_t)B * HEADS * L * 4);
+        lay.dXt = c.take<void>(M * WIDTH * es);
+        lay.dH = c.take<void>(M * WIDTH * es);
+        lay.dA = c.take<void>(M * MLP * es);
+        lay.dO = c.take<void>(M * WIDTH * es);
+        lay.dQKV = c.take<void>(M * QKVW * es);
+    } else {
+        lay.dXa = lay.dXb = lay.delta = nullptr;
+        lay.dXt = lay.dH = lay.dA = lay.dO = lay.dQKV = nullptr;
+    }
+    lay.bytes = c.off;
+    return lay;
+}
+
+bool check_weights(const EbcVitWeights* w) {
+    return w && w->layers > 0 && w->layer && w->width == WIDTH && w->heads == HEADS && w->patch == 16 && w->num_vpt >= 0;
+}
+
+}  // namespace
+
+extern "C" size_t ebc_vit_workspace_bytes(int B, int H, int W, int layers, int num_vpt, int dtype, int training)
+{
+    const int G = (H / 16) * (W / 16), L = 1 + num_vpt + G;
+    return carve(nullptr, B, L, G, layers, dtype, training).bytes;
+}
+
+extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B, int H, int W,
+                               const float* const* vpt, long vpt_bstride, int dtype, int training,
+                               void* ws, size_t ws_bytes, float* feat, ebc_stream_t stream)
+{
+    if (!check_weights(w) || !image || !ws || !feat || B <= 0 || H % 16 || W % 16) return EBC_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int NV = w->num_vpt, G = (H / 16) * (W / 16), L = 1 + NV + G, layers = w->layers;
+    if (L > 256) return EBC_E_UNSUPPORTED;
+    const int M = B * L;
+    Layout lay = carve(ws, B, L, G, layers, dtype, training);
+    if (lay.bytes > ws_bytes) return EBC_E_ARG;
+    if (NV > 0 && (!vpt || !vpt[0])) return EBC_E_ARG;
+
+    // patch embedding: im2col + GEMM with conv1 weight [768, 3*16*16] (image_encoder.py:141)
+    EBC_TRY(ebc::im2col(dtype, image, lay.patch_t, B, H, W, 16, st));
+    EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 1, lay.patch_t, w->w_patch, lay.patch_f, nullptr, nullptr, nullptr,
+                         B * G, WIDTH, WIDTH, st));
+    // CLS + pos + ln_pre, VPT_0 rows (model.py:150-168)
+    EBC_TRY(ebc::embed_tokens(lay.patch_f, w->cls, w->pos, w->ln_pre_g, w->ln_pre_b, NV ? vpt[0] : nullptr,
+                              vpt_bstride, lay.X[0], B, L, G, NV, WIDTH, st));
+    for (int l = 0; l < layers; ++l) {
+        const EbcVitLayer& p = w->layer[l];
+        LayerSave& s = lay.s[training ? l : 0];
+        float* X = lay.X[l];
+        float* Xn = lay.X[l + 1];
+        if (l > 0 && NV > 0 && vpt[l])                                 // deep VPT: replace prompt rows
+            EBC_TRY(ebc::insert_vpt(X, vpt[l], vpt_bstride, B, L, NV, WIDTH, st));
+        // x = x + out_proj(attn(ln_1(x)))
+        EBC_TRY(ebc::layernorm_fwd(dtype, X, 0, 0, 0, p.ln1_g, p.ln1_b, lay.H, nullptr, s.m1, s.r1, M, WIDTH, st));
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.H, p.w_qkv, s.QKV, p.b_qkv, nullptr, nullptr, M, QKVW, WIDTH, st));
+        EBC_TRY(ebc::attention_fwd(dtype, s.QKV, s.O, s.lse, B, L, HEADS, st));
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_RESID, 1, s.O, p.w_out, s.X1, p.b_out, X, nullptr, M, WIDTH, WIDTH, st));
+        // x = x + c_proj(QuickGELU(c_fc(ln_2(x))))
+        EBC_TRY(ebc::layernorm_fwd(dtype, s.X1, 0, 0, 0, p.ln2_g, p.ln2_b, lay.H, nullptr, s.m2, s.r2, M, WIDTH, st));
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_GELU, 0, lay.H, p.w_fc, lay.G, p.b_fc, nullptr, training ? s.A : nullptr,
+                             M, MLP, WIDTH, st));
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_RESID, 1, lay.G, p.w_proj, Xn, p.b_proj, s.X1, nullptr, M, WIDTH, MLP, st));
+    }
+    // ln_post on the patch rows only (CLS and prompt rows are dropped, model.py:185-188)
+    EBC_TRY(ebc::layernorm_fwd(EBC_F32, lay.X[layers], G, L, 1 + NV, w->ln_post_g, w->ln_post_b, feat, nullptr,
+                               lay.mpost, lay.rpost, B * G, WIDTH, st));
+    return EBC_OK;
+}
+
+extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int dtype, void* ws, size_t ws_bytes,
+                                const float* dfeat, float* const* dvpt, long vpt_bstride, ebc_stream_t stream)
+{
+    if (!check_weights(w) || !ws || !dfeat) return EBC_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int NV = w->num_vpt, G = (H / 16) * (W / 16), L = 1 + NV + G, layers = w->layers;
+    const int M = B * L;
+    Layout lay = carve(ws, B, L, G, layers, dtype, 1);
+    if (lay.bytes > ws_bytes) return EBC_E_ARG;
+    const int per_batch = vpt_bstride != 0;
+    const size_t es = dtype == EBC_F32 ? 4 : 2;
+
+    // ln_post backward into the patch rows of dX_L; CLS / prompt rows get zero gradient
+    float* dX = lay.dXa;
+    float* dXo = lay.dXb;
+    if (hipMemsetAsync(dX, 0, (size_t)M * WIDTH * 4, st) != hipSuccess) return EBC_E_LAUNCH;
+    if (hipMemsetAsync(lay.dXt, 0, (size_t)M * WIDTH * es, st) != hipSuccess) return EBC_E_LAUNCH;
+    EBC_TRY(ebc::layernorm_bwd(dtype, 1, dfeat, lay.X[layers], G, L, 1 + NV, lay.mpost, lay.rpost, w->ln_post_g,
+                               nullptr, dX, lay.dXt, B * G, WIDTH, st));
+    for (int l = layers - 1; l >= 0; --l) {
+        const EbcVitLayer& p = w->layer[l];
+        LayerSave& s = lay.s[l];
+        // MLP half: dA = (dX . W_proj) * QuickGELU'(A);  dH2 = dA . W_fc;  dX1 = dX + LN2'(dH2)
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_GELU_BWD, 0, lay.dXt, p.wt_proj, lay.dA, nullptr, nullptr, s.A, M, MLP, WIDTH, st));
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dA, p.wt_fc, lay.dH, nullptr, nullptr, nullptr, M, WIDTH, MLP, st));
+        EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, s.X1, 0, 0, 0, s.m2, s.r2, p.ln2_g, dX, dXo, lay.dXt, M, WIDTH, st));
+        { float* t = dX; dX = dXo; dXo = t; }
+        // attention half: dO = dX1 . W_out;  dQKV = attn'(...);  dH = dQKV . W_qkv;  dX = dX1 + LN1'(dH)
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dXt, p.wt_out, lay.dO, nullptr, nullptr, nullptr, M, WIDTH, WIDTH, st));
+        EBC_TRY(ebc::attn_delta(dtype, lay.dO, s.O, lay.delta, B, L, HEADS, st));
+        EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st));
+        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dQKV, p.wt_qkv, lay.dH, nullptr, nullptr, nullptr, M, WIDTH, QKVW, st));
+        EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, lay.X[l], 0, 0, 0, s.m1, s.r1, p.ln1_g, dX, dXo, lay.dXt, M, WIDTH, st));
+        { float* t = dX; dX = dXo; dXo = t; }
+        // prompt rows: dvpt_l = sum_b dX[b, 1..NV]; they were replaced at this block's input, so the
+        // previous block's output gets zero gradient there (deep VPT).  Shallow VPT: only layer 0.
+        if (NV > 0 && dvpt && dvpt[l]) {
+            EBC_TRY(ebc::vpt_grad(dtype, dX, lay.dXt, dvpt[l], B, L, NV, WIDTH, per_batch, 0, st));
+        }
+    }
+    return EBC_OK;
+}
+
+// ---------------------------------------------------------------------------- kernel C-ABI
+extern "C" int ebc_layernorm_fwd(int dtype, const float* x, int rows_per_group, int group_stride, int group_offset,
+                                 const float* gamma, const float* beta, void* out, float* out_f32, float* mean,
+                                 float* rstd, int M, int D, ebc_stream_t stream)
+{
+    return ebc::layernorm_fwd(dtype, x, rows_per_group, group_stride, group_offset, gamma, beta, out, out_f32, mean,
+                              rstd, M, D, (hipStream_t)stream);
+}
+extern "C" int ebc_layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rows_per_group,
+                                 int group_stride, int group_offset, const float* mean, const float* rstd,
+                                 const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, int D,
+                                 ebc_stream_t stream)
+{
+    return ebc::layernorm_bwd(dtype, dy_f32, dy, x, rows_per_group, group_stride, group_offset, mean, rstd, gamma,
+                              dx_in, dx_out, dx_out_t, M, D, (hipStream_t)stream);
+}
+extern "C" int ebc_attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, ebc_stream_t stream)
+{
+    return ebc::attention_fwd(dtype, qkv, out, lse, B, L, H, (hipStream_t)stream);
+}
+extern "C" int ebc_attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse,
+                                 float* delta_ws, void* dqkv, int B, int L, int H, ebc_stream_t stream)
+{
+    EBC_TRY(ebc::attn_delta(dtype, dout, out, delta_ws, B, L, H, (hipStream_t)stream));
+    return ebc::attention_bwd(dtype, qkv, dout, lse, delta_ws, dqkv, B, L, H, (hipStream_t)stream);
+}
+extern "C" int ebc_head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+                            float* logits, float* expo, int P, int HW, int NB, ebc_stream_t stream)
+{
+    return ebc::head_fwd(dtype_z, Z, text, logit_scale, anchors, logits, expo, P, HW, NB, (hipStream_t)stream);
+}
+extern "C" int ebc_head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
+                            const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
+                            float* dbias, float* dscale, int P, int HW, int NB, ebc_stream_t stream)
+{
+    return ebc::head_bwd(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW,
+                         NB, (hipStream_t)stream);
+}
+extern "C" int ebc_cast_f32(int dtype, const float* in, void* out, size_t n, ebc_stream_t stream)
+{
+    return ebc::cast_f32(dtype, in, out, n, (hipStream_t)stream);
+}

@@ -1,0 +1,567 @@
+// Memory-bound pieces of the CLIP-EBC ViT path on gfx950: LayerNorm fwd/bwd, patch im2col,
+// token embedding (+CLS, +pos, ln_pre, VPT rows), VPT insert / gradient, the blockwise
+// image-text similarity head fwd/bwd, and the attention-backward row statistic.
+//
+// Reference: LayerNorm (fp32 math)        models/clip/_clip/blocks.py:8-14
+//            token prologue               models/clip/model.py:147-158, image_encoder.py:141-148
+//            VPT assemble / disassemble   models/clip/model.py:131-140, 161-183
+//            ln_post + drop CLS           models/clip/model.py:185-188
+//            similarity head              models/clip/model.py:198-217
+// Every kernel is one wave per row (D = 256*NV), 16-B vector accesses, fp32 statistics.
+#include "ebc_common.h"
+#include "mfma.h"
+
+using namespace ebc;
+
+namespace {
+
+constexpr float LN_EPS = 1e-5f;
+
+template <class T> __device__ __forceinline__ void st4(T* p, float4 v);
+template <> __device__ __forceinline__ void st4<float>(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+template <> __device__ __forceinline__ void st4<_Float16>(_Float16* p, float4 v) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<h4*>(p) = h4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+}
+template <> __device__ __forceinline__ void st4<__bf16>(__bf16* p, float4 v) {
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<b4*>(p) = b4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+}
+template <class T> __device__ __forceinline__ float4 ld4(const T* p) {
+    return make_float4((float)p[0], (float)p[1], (float)p[2], (float)p[3]);
+}
+template <> __device__ __forceinline__ float4 ld4<float>(const float* p) { return *reinterpret_cast<const float4*>(p); }
+template <> __device__ __forceinline__ float4 ld4<_Float16>(const _Float16* p) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4 v = *reinterpret_cast<const h4*>(p);
+    return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+template <> __device__ __forceinline__ float4 ld4<__bf16>(const __bf16* p) {
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    const b4 v = *reinterpret_cast<const b4*>(p);
+    return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+
+struct RowMap {            // out row r -> source row (r / rpg) * gstride + goff + r % rpg
+    int rpg, gstride, goff;
+    __device__ __forceinline__ size_t operator()(int r) const {
+        return (size_t)(r / rpg) * gstride + goff + (r % rpg);
+    }
+};
+
+// Normalise NV float4 per lane of one row held in registers.
+template <int NV>
+__device__ __forceinline__ void ln_row(float4 (&v)[NV], const float* gamma, const float* beta, float& mean, float& rstd) {
+    constexpr float inv = 1.0f / (256.0f * NV);
+    const int lane = threadIdx.x & 63;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    mean = wave_sum(s) * inv;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+        q += (a * a + b * b) + (c * c + d * d);
+    }
+    rstd = 1.0f / sqrtf(wave_sum(q) * inv + LN_EPS);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = 4 * lane + 256 * i;
+        const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+        const float4 b = *reinterpret_cast<const float4*>(beta + c);
+        v[i] = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
+                           (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
+    }
+}
+
+template <class T, int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, RowMap map, const float* gamma,
+                                                     const float* beta, T* out, float* outf, float* mean_out,
+                                                     float* rstd_out, int M)
+{
+    constexpr int D = 256 * NV;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= M) return;
+    const float* xr = x + map(r) * D;
+    float4 v[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const float4*>(xr + 4 * lane + 256 * i);
+    float mean, rstd;
+    ln_row<NV>(v, gamma, beta, mean, rstd);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const size_t o = (size_t)r * D + 4 * lane + 256 * i;
+        if (out) st4<T>(out + o, v[i]);
+        if (outf) st4<float>(outf + o, v[i]);
+    }
+    if (lane == 0 && mean_out) { mean_out[r] = mean; rstd_out[r] = rstd; }
+}
+
+// dx_out = dx_in + LN'(dy):  rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
+template <class T, class DY, int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, const float* __restrict__ x, RowMap map,
+                                                     const float* mean_in, const float* rstd_in, const float* gamma,
+                                                     const float* dx_in, float* dx_out, T* dx_out_t, int M)
+{
+    constexpr int D = 256 * NV;
+    constexpr float inv = 1.0f / (float)D;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= M) return;
+    const size_t xr = map(r) * D;
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float4 g[NV], xh[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = 4 * lane + 256 * i;
+        const float4 d = ld4<DY>(dy + (size_t)r * D + c);
+        const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
+        const float4 xv = *reinterpret_cast<const float4*>(x + xr + c);
+        g[i] = make_float4(d.x * gm.x, d.y * gm.y, d.z * gm.z, d.w * gm.w);
+        xh[i] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
+        s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
+        s2 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
+    }
+    s1 = wave_sum(s1) * inv;
+    s2 = wave_sum(s2) * inv;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = 4 * lane + 256 * i;
+        float4 o = make_float4(rstd * (g[i].x - s1 - xh[i].x * s2), rstd * (g[i].y - s1 - xh[i].y * s2),
+                               rstd * (g[i].z - s1 - xh[i].z * s2), rstd * (g[i].w - s1 - xh[i].w * s2));
+        if (dx_in) {
+            const float4 a = *reinterpret_cast<const float4*>(dx_in + xr + c);
+            o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+        }
+        *reinterpret_cast<float4*>(dx_out + xr + c) = o;
+        if (dx_out_t) st4<T>(dx_out_t + xr + c, o);
+    }
+}
+
+// x [B,3,H,W] f32 -> patches [B*gh*gw, 3*P*P] (k = c*P*P + kh*P + kw, conv1 weight order)
+template <class T>
+__global__ void im2col_kernel(const float* __restrict__ x, T* __restrict__ out, int B, int H, int W, int P)
+{
+    const int gh = H / P, gw = W / P, KD = 3 * P * P, K4 = KD / 4;
+    const size_t total = (size_t)B * gh * gw * K4;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int k4 = (int)(e % K4);
+        const size_t row = e / K4;
+        const int px = (int)(row % gw), py = (int)((row / gw) % gh), b = (int)(row / ((size_t)gw * gh));
+        const int k = 4 * k4, c = k / (P * P), kh = (k / P) % P, kw = k % P;
+        const float4 v = *reinterpret_cast<const float4*>(x + (((size_t)b * 3 + c) * H + (py * P + kh)) * W + px * P + kw);
+        st4<T>(out + row * KD + k, v);
+    }
+}
+
+// X[b, s] for the first block (models/clip/model.py:147-168):
+//   s = 0: ln_pre(cls + pos[0]);  1 <= s <= NVPT: vpt_0;  s > NVPT: ln_pre(patch[b, s-1-NVPT] + pos[s-NVPT])
+template <int NV>
+__global__ __launch_bounds__(256) void embed_kernel(const float* __restrict__ patch, const float* cls, const float* pos,
+                                                    const float* gamma, const float* beta, const float* vpt,
+                                                    long vpt_bstride, float* X, int B, int L, int G, int NVPT)
+{
+    constexpr int D = 256 * NV;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= B * L) return;
+    const int b = r / L, s = r % L;
+    float* xo = X + (size_t)r * D;
+    if (s >= 1 && s <= NVPT) {
+        const float* vp = vpt + b * vpt_bstride + (size_t)(s - 1) * D;
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            *reinterpret_cast<float4*>(xo + 4 * lane + 256 * i) = *reinterpret_cast<const float4*>(vp + 4 * lane + 256 * i);
+        return;
+    }
+    const int p = s == 0 ? -1 : s - 1 - NVPT;
+    float4 v[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = 4 * lane + 256 * i;
+        const float4 e = p < 0 ? *reinterpret_cast<const float4*>(cls + c)
+                               : *reinterpret_cast<const float4*>(patch + ((size_t)b * G + p) * D + c);
+        const float4 q = *reinterpret_cast<const float4*>(pos + (size_t)(p + 1) * D + c);
+        v[i] = make_float4(e.x + q.x, e.y + q.y, e.z + q.z, e.w + q.w);
+    }
+    float mean, rstd;
+    ln_row<NV>(v, gamma, beta, mean, rstd);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) *reinterpret_cast<float4*>(xo + 4 * lane + 256 * i) = v[i];
+}
+
+__global__ void insert_vpt_kernel(float* X, const float* vpt, long vpt_bstride, int B, int L, int NVPT, int D)
+{
+    const size_t total = (size_t)B * NVPT * D / 4;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(e % (D / 4));
+        const int r = (int)((e / (D / 4)) % NVPT), b = (int)(e / ((size_t)(D / 4) * NVPT));
+        reinterpret_cast<float4*>(X + ((size_t)b * L + 1 + r) * D)[c4] =
+            reinterpret_cast<const float4*>(vpt + b * vpt_bstride + (size_t)r * D)[c4];
+    }
+}
+
+// dvpt[r, c] (+)= sum_b dX[b, 1+r, c]  (or per batch when per_batch), then zero those rows of dX / dXt.
+template <class T>
+__global__ void vpt_grad_kernel(float* dX, T* dXt, float* dvpt, int B, int L, int NVPT, int D, int per_batch, int accumulate)
+{
+    const int total = NVPT * D;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int r = e / D, c = e % D;
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) {
+            const size_t o = ((size_t)b * L + 1 + r) * D + c;
+            if (per_batch) {
+                float* dst = dvpt + (size_t)b * total + e;
+                *dst = accumulate ? *dst + dX[o] : dX[o];
+            } else {
+                s += dX[o];
+            }
+            dX[o] = 0.f;
+            if (dXt) dXt[o] = (T)0.f;
+        }
+        if (!per_batch) dvpt[e] = accumulate ? dvpt[e] + s : s;
+    }
+}
+
+// ----------------------------------------------------------------------------- similarity head
+// One wave per pixel, CH = 512 channels (8 per lane), NB <= 16 bins.  Text features normalised in LDS.
+constexpr int CH = 512;
+constexpr int PIX_PER_BLOCK = 16;
+
+template <class TZ>
+__device__ __forceinline__ void load_pix(const TZ* z, float (&v)[8]) {
+    const int lane = threadIdx.x & 63;
+    const float4 a = ld4<TZ>(z + 4 * lane), b = ld4<TZ>(z + 256 + 4 * lane);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+__device__ void load_text(const float* text, int NB, float* tn, float* scratch) {
+    // tn[k][c] = text[k][c] / max(||text[k]||, 1e-12)   (F.normalize, model.py:204)
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    for (int k = w; k < NB; k += blockDim.x / 64) {
+        float s = 0.f;
+        for (int c = lane; c < CH; c += 64) { const float x = text[k * CH + c]; s += x * x; }
+        s = wave_sum(s);
+        const float inv = 1.0f / fmaxf(sqrtf(s), 1e-12f);
+        for (int c = lane; c < CH; c += 64) tn[k * CH + c] = text[k * CH + c] * inv;
+    }
+    __syncthreads();
+}
+
+template <class TZ>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z, const float* text, const float* logit_scale,
+                                                       const float* anchors, float* logits, float* expo, int P, int HW, int NB)
+{
+    extern __shared__ __attribute__((aligned(16))) float tn[];
+    load_text(text, NB, tn, nullptr);
+    const float s = expf(*logit_scale);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int pi = w; pi < PIX_PER_BLOCK; pi += 4) {
+        const int p = blockIdx.x * PIX_PER_BLOCK + pi;
+        if (p >= P) break;
+        float v[8];
+        load_pix<TZ>(Z + (size_t)p * CH, v);
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+        const float inv = 1.0f / fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
+        float lg[16];
+        float mx = -INFINITY;
+        for (int k = 0; k < NB; ++k) {
+            const float* t = tn + k * CH;
+            const float4 a = *reinterpret_cast<const float4*>(t + 4 * lane), b = *reinterpret_cast<const float4*>(t + 256 + 4 * lane);
+            float d = (s * (v[0] * inv)) * a.x + (s * (v[1] * inv)) * a.y + (s * (v[2] * inv)) * a.z + (s * (v[3] * inv)) * a.w;
+            d += (s * (v[4] * inv)) * b.x + (s * (v[5] * inv)) * b.y + (s * (v[6] * inv)) * b.z + (s * (v[7] * inv)) * b.w;
+            lg[k] = wave_sum(d);
+            mx = fmaxf(mx, lg[k]);
+        }
+        float se = 0.f;
+        for (int k = 0; k < NB; ++k) se += expf(lg[k] - mx);
+        float e = 0.f;
+        for (int k = 0; k < NB; ++k) e += (expf(lg[k] - mx) / se) * anchors[k];
+        if (lane == 0) {
+            const int b = p / HW, hw = p % HW;
+            for (int k = 0; k < NB; ++k) logits[((size_t)b * NB + k) * HW + hw] = lg[k];
+            expo[(size_t)b * HW + hw] = e;
+        }
+    }
+}
+
+// dZ = d/dZ of (logits, exp) given upstream dlogits [B,NB,HW], dexp [B,1,HW] (x *gscale if given);
+// also d bias (column sums of dZ) and d logit_scale, accumulated with atomics (zeroed by the launcher).
+template <class TZ, class TD>
+__global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z, const float* text, const float* logit_scale,
+                                                       const float* anchors, const float* dlogits, const float* dexp,
+                                                       const float* gscale, TD* dZ, float* dbias, float* dscale,
+                                                       int P, int HW, int NB)
+{
+    extern __shared__ __attribute__((aligned(16))) float tn[];
+    float* dbias_l = tn + NB * CH;       // [4 waves][CH]
+    float* dsc_l = dbias_l + 4 * CH;     // [4]
+    load_text(text, NB, tn, nullptr);
+    const float ls = *logit_scale, s = expf(ls);
+    const float gs = gscale ? *gscale : 1.0f;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float dsc = 0.f;
+    for (int pi = w; pi < PIX_PER_BLOCK; pi += 4) {
+        const int p = blockIdx.x * PIX_PER_BLOCK + pi;
+        if (p >= P) break;
+        float v[8];
+        load_pix<TZ>(Z + (size_t)p * CH, v);
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+        const float nrm = sqrtf(wave_sum(ss));
+        const float den = fmaxf(nrm, 1e-12f), inv = 1.0f / den;
+        float zn[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) zn[j] = v[j] * inv;
+        float lg[16], pr[16];
+        float mx = -INFINITY;
+        for (int k = 0; k < NB; ++k) {
+            const float* t = tn + k * CH;
+            const float4 a = *reinterpret_cast<const float4*>(t + 4 * lane), b = *reinterpret_cast<const float4*>(t + 256 + 4 * lane);
+            float d = (s * zn[0]) * a.x + (s * zn[1]) * a.y + (s * zn[2]) * a.z + (s * zn[3]) * a.w;
+            d += (s * zn[4]) * b.x + (s * zn[5]) * b.y + (s * zn[6]) * b.z + (s * zn[7]) * b.w;
+            lg[k] = wave_sum(d);
+            mx = fmaxf(mx, lg[k]);
+        }
+        float se = 0.f;
+        for (int k = 0; k < NB; ++k) { pr[k] = expf(lg[k] - mx); se += pr[k]; }
+        float e = 0.f;
+        for (int k = 0; k < NB; ++k) { pr[k] /= se; e += pr[k] * anchors[k]; }
+        const int b = p / HW, hw = p % HW;
+        const float de = dexp[(size_t)b * HW + hw] * gs;
+        float dzn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < NB; ++k) {
+            // d logit_k = dlogits_k + dexp * p_k (anchor_k - e)   (softmax + expectation backward)
+            const float dl = dlogits[((size_t)b * NB + k) * HW + hw] * gs + de * pr[k] * (anchors[k] - e);
+            dsc += dl * lg[k];                             // logits = exp(ls) * cos  ->  d ls = dl * logits
+            const float* t = tn + k * CH;
+            const float4 a = *reinterpret_cast<const float4*>(t + 4 * lane), bq = *reinterpret_cast<const float4*>(t + 256 + 4 * lane);
+            const float c = dl * s;
+            dzn[0] += c * a.x; dzn[1] += c * a.y; dzn[2] += c * a.z; dzn[3] += c * a.w;
+            dzn[4] += c * bq.x; dzn[5] += c * bq.y; dzn[6] += c * bq.z; dzn[7] += c * bq.w;
+        }
+        // F.normalize backward: dz = (dzn - zn * <zn, dzn>) / ||z||   (or dzn / eps when clamped)
+        float dot = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += zn[j] * dzn[j];
+        dot = (nrm > 1e-12f) ? wave_sum(dot) : 0.f;
+        float dz[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { dz[j] = (dzn[j] - zn[j] * dot) * inv; db[j] += dz[j]; }
+        st4<TD>(dZ + (size_t)p * CH + 4 * lane, make_float4(dz[0], dz[1], dz[2], dz[3]));
+        st4<TD>(dZ + (size_t)p * CH + 256 + 4 * lane, make_float4(dz[4], dz[5], dz[6], dz[7]));
+    }
+    // lane 0's dsc is the wave's per-pixel sum (wave_sum results are lane-uniform)
+    for (int j = 0; j < 4; ++j) { dbias_l[w * CH + 4 * lane + j] = db[j]; dbias_l[w * CH + 256 + 4 * lane + j] = db[4 + j]; }
+    if (lane == 0) dsc_l[w] = dsc;
+    __syncthreads();
+    for (int c = threadIdx.x; c < CH; c += blockDim.x) {
+        const float t = dbias_l[c] + dbias_l[CH + c] + dbias_l[2 * CH + c] + dbias_l[3 * CH + c];
+        if (dbias) atomicAdd(dbias + c, t);
+    }
+    if (threadIdx.x == 0 && dscale) atomicAdd(dscale, dsc_l[0] + dsc_l[1] + dsc_l[2] + dsc_l[3]);
+}
+
+// delta[b, h, q] = sum_d dO[b*L+q, h*64+d] * O[b*L+q, h*64+d]   (FA-style backward row statistic)
+template <class T>
+__global__ void attn_delta_kernel(const T* dO, const T* O, float* delta, int B, int L, int H)
+{
+    const int total = B * L * H;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int h = e % H, row = e / H;
+        const int b = row / L, q = row % L;
+        const T* a = dO + (size_t)row * H * 64 + h * 64;
+        const T* o = O + (size_t)row * H * 64 + h * 64;
+        float s = 0.f;
+#pragma unroll
+        for (int d = 0; d < 64; d += 4) {
+            const float4 x = ld4<T>(a + d), y = ld4<T>(o + d);
+            s += (x.x * y.x + x.y * y.y) + (x.z * y.z + x.w * y.w);
+        }
+        delta[((size_t)b * H + h) * L + q] = s;
+    }
+}
+
+template <class T>
+__global__ void cast_kernel(const float* in, T* out, size_t n4)
+{
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n4; e += (size_t)gridDim.x * blockDim.x)
+        st4<T>(out + 4 * e, reinterpret_cast<const float4*>(in)[e]);
+}
+
+inline int grid_for(size_t n, int block = 256) {
+    const size_t g = (n + block - 1) / block;
+    return (int)(g < 8192 ? (g ? g : 1) : 8192);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------- launchers
+namespace ebc {
+
+int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,
+                  void* out, float* outf, float* mean, float* rstd, int M, int D, hipStream_t st)
+{
+    if (D != 768 || M <= 0) return EBC_E_UNSUPPORTED;
+    const RowMap map{rpg > 0 ? rpg : M, gstride, goff};
+    const dim3 grid((M + 3) / 4);
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL((ln_fwd_kernel<float, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (float*)out, outf, mean, rstd, M); break;
+        case EBC_F16: hipLaunchKernelGGL((ln_fwd_kernel<_Float16, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (_Float16*)out, outf, mean, rstd, M); break;
+        case EBC_BF16: hipLaunchKernelGGL((ln_fwd_kernel<__bf16, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (__bf16*)out, outf, mean, rstd, M); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+template <class T>
+static int ln_bwd_t(int dy_f32, const void* dy, const float* x, RowMap map, const float* mean, const float* rstd,
+                    const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, hipStream_t st)
+{
+    const dim3 grid((M + 3) / 4);
+    if (dy_f32)
+        hipLaunchKernelGGL((ln_bwd_kernel<T, float, 3>), grid, dim3(256), 0, st, (const float*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M);
+    else
+        hipLaunchKernelGGL((ln_bwd_kernel<T, T, 3>), grid, dim3(256), 0, st, (const T*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg, int gstride, int goff,
+                  const float* mean, const float* rstd, const float* gamma, const float* dx_in, float* dx_out,
+                  void* dx_out_t, int M, int D, hipStream_t st)
+{
+    if (D != 768 || M <= 0) return EBC_E_UNSUPPORTED;
+    const RowMap map{rpg > 0 ? rpg : M, gstride, goff};
+    switch (dtype) {
+        case EBC_F32: return ln_bwd_t<float>(1, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, st);
+        case EBC_F16: return ln_bwd_t<_Float16>(dy_f32, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, st);
+        case EBC_BF16: return ln_bwd_t<__bf16>(dy_f32, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, st);
+    }
+    return EBC_E_ARG;
+}
+
+int im2col(int dtype, const float* x, void* out, int B, int H, int W, int P, hipStream_t st)
+{
+    if (H % P || W % P || (P * P * 3) % 4 || P % 4) return EBC_E_ARG;
+    const size_t n = (size_t)B * (H / P) * (W / P) * 3 * P * P / 4;
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, x, (float*)out, B, H, W, P); break;
+        case EBC_F16: hipLaunchKernelGGL(im2col_kernel<_Float16>, dim3(grid_for(n)), dim3(256), 0, st, x, (_Float16*)out, B, H, W, P); break;
+        case EBC_BF16: hipLaunchKernelGGL(im2col_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, st, x, (__bf16*)out, B, H, W, P); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int embed_tokens(const float* patch, const float* cls, const float* pos, const float* gamma, const float* beta,
+                 const float* vpt, long vpt_bstride, float* X, int B, int L, int G, int NVPT, int D, hipStream_t st)
+{
+    if (D != 768 || L != 1 + NVPT + G) return EBC_E_ARG;
+    hipLaunchKernelGGL(embed_kernel<3>, dim3((B * L + 3) / 4), dim3(256), 0, st, patch, cls, pos, gamma, beta, vpt,
+                       vpt_bstride, X, B, L, G, NVPT);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int insert_vpt(float* X, const float* vpt, long vpt_bstride, int B, int L, int NVPT, int D, hipStream_t st)
+{
+    const size_t n = (size_t)B * NVPT * D / 4;
+    hipLaunchKernelGGL(insert_vpt_kernel, dim3(grid_for(n)), dim3(256), 0, st, X, vpt, vpt_bstride, B, L, NVPT, D);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int vpt_grad(int dtype, float* dX, void* dXt, float* dvpt, int B, int L, int NVPT, int D, int per_batch, int accumulate, hipStream_t st)
+{
+    const int n = NVPT * D;
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL(vpt_grad_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, dX, (float*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
+        case EBC_F16: hipLaunchKernelGGL(vpt_grad_kernel<_Float16>, dim3(grid_for(n)), dim3(256), 0, st, dX, (_Float16*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
+        case EBC_BF16: hipLaunchKernelGGL(vpt_grad_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, st, dX, (__bf16*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+             float* logits, float* expo, int P, int HW, int NB, hipStream_t st)
+{
+    if (NB <= 0 || NB > 16) return EBC_E_UNSUPPORTED;
+    const dim3 grid((P + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
+    const size_t lds = (size_t)NB * CH * 4;
+    switch (dtype_z) {
+        case EBC_F32: hipLaunchKernelGGL(head_fwd_kernel<float>, grid, dim3(256), lds, st, (const float*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
+        case EBC_F16: hipLaunchKernelGGL(head_fwd_kernel<_Float16>, grid, dim3(256), lds, st, (const _Float16*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
+        case EBC_BF16: hipLaunchKernelGGL(head_fwd_kernel<__bf16>, grid, dim3(256), lds, st, (const __bf16*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+             const float* dlogits, const float* dexp, const float* gscale, void* dZ, float* dbias, float* dscale,
+             int P, int HW, int NB, hipStream_t st)
+{
+    if (NB <= 0 || NB > 16) return EBC_E_UNSUPPORTED;
+    if (dbias && hipMemsetAsync(dbias, 0, CH * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
+    if (dscale && hipMemsetAsync(dscale, 0, sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
+    const dim3 grid((P + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
+    const size_t lds = ((size_t)NB * CH + 4 * CH + 4) * 4;
+#define HB(TZ, TD) hipLaunchKernelGGL((head_bwd_kernel<TZ, TD>), grid, dim3(256), lds, st, (const TZ*)Z, text, logit_scale, anchors, dlogits, dexp, gscale, (TD*)dZ, dbias, dscale, P, HW, NB)
+    // the dZ element type is the caller's buffer type (dtype_dz), independent of Z's
+#define HBZ(TZ)                                                   \
+    switch (dtype_dz) {                                           \
+        case EBC_F32: HB(TZ, float); break;                       \
+        case EBC_F16: HB(TZ, _Float16); break;                    \
+        case EBC_BF16: HB(TZ, __bf16); break;                     \
+        default: return EBC_E_ARG;                                \
+    }
+    switch (dtype_z) {
+        case EBC_F32: HBZ(float); break;
+        case EBC_F16: HBZ(_Float16); break;
+        case EBC_BF16: HBZ(__bf16); break;
+        default: return EBC_E_ARG;
+    }
+#undef HBZ
+#undef HB
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int attn_delta(int dtype, const void* dO, const void* O, float* delta, int B, int L, int H, hipStream_t st)
+{
+    const int n = B * L * H;
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float*)dO, (const float*)O, delta, B, L, H); break;
+        case EBC_F16: hipLaunchKernelGGL(attn_delta_kernel<_Float16>, dim3(grid_for(n)), dim3(256), 0, st, (const _Float16*)dO, (const _Float16*)O, delta, B, L, H); break;
+        case EBC_BF16: hipLaunchKernelGGL(attn_delta_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const __bf16*)dO, (const __bf16*)O, delta, B, L, H); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int cast_f32(int dtype, const float* in, void* out, size_t n, hipStream_t st)
+{
+    if (n % 4) return EBC_E_ARG;
+    switch (dtype) {
+        case EBC_F16: hipLaunchKernelGGL(cast_kernel<_Float16>, dim3(grid_for(n / 4)), dim3(256), 0, st, in, (_Float16*)out, n / 4); break;
+        case EBC_BF16: hipLaunchKernelGGL(cast_kernel<__bf16>, dim3(grid_for(n / 4)), dim3(256), 0, st, in, (__bf16*)out, n / 4); break;
+        case EBC_F32: hipLaunchKernelGGL(cast_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st, in, (float*)out, n / 4); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+}  // namespace ebc

@@ -31,6 +31,16 @@ SIGNATURES = {
     "ebc_dace_loss": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _I, _F, _I,
                            _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "ebc_gemm": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "ebc_vit_workspace_bytes": (_Z, [_I, _I, _I, _I, _I, _I, _I]),
+    "ebc_vit_forward": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_long, _I, _I, _P, _Z, _P, _P]),
+    "ebc_vit_backward": (_I, [_P, _I, _I, _I, _I, _P, _Z, _P, _P, ctypes.c_long, _P]),
+    "ebc_layernorm_fwd": (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "ebc_layernorm_bwd": (_I, [_I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "ebc_attention_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _P]),
+    "ebc_attention_bwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "ebc_head_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "ebc_head_bwd": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "ebc_cast_f32": (_I, [_I, _P, _P, _Z, _P]),
 }
 
 

@@ -1,0 +1,413 @@
+"""Drop-in CLIP-EBC model (ViT-B/16 + deep VPT) whose hot path runs in libebc_hip.so.
+
+Reference surface kept:
+  * `get_model(backbone, input_size, reduction, bins, anchor_points, **kw)`  (models/__init__.py:10-44)
+  * `CLIP_EBC.forward(x) -> (logits [B,N,H/r,W/r], exp [B,1,H/r,W/r])` in train mode, `exp` in eval
+    (models/clip/model.py:191-217); attributes `.bins`, `.anchor_points`, `.reduction`,
+    `.encoder_reduction`, `.num_vpt`, `.deep_vpt`; identical `state_dict()` keys
+    (`image_encoder.*`, `vpt_{l}`, `image_decoder.0.*`, `projection.*`, `text_encoder.*`, `logit_scale`).
+  * mixed precision follows the caller's `torch.autocast` (the reference trains under
+    `torch.cuda.amp.autocast`, train.py:36-40): fp16/bf16 GEMM inputs, fp32 residual stream and
+    statistics; without autocast the whole path is exact-f32 (parity mode).
+
+Execution: the 12-block encoder forward/backward is ONE C-ABI call each (`ebc_vit_forward/backward`);
+the projection + similarity head is an MFMA GEMM + a fused head kernel.  The BasicBlock decoder
+(models/utils.py:254-303) stays on PyTorch-ROCm (MIOpen) in this round.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from collections import OrderedDict
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+from . import _lib
+from . import synthetic
+from .text import CLIPTextEncoder, format_count, prompt_tokens
+
+WIDTH, HEADS, PATCH, EMBED = 768, 12, 16, 512
+
+
+# ----------------------------------------------------------------------------- parameter containers
+class _Block(nn.Module):
+    """Parameter layout of ResidualAttentionBlock (models/clip/_clip/blocks.py:22-42)."""
+
+    def __init__(self, width: int = WIDTH, heads: int = HEADS):
+        super().__init__()
+        self.attn = nn.MultiheadAttention(width, heads)
+        self.ln_1 = nn.LayerNorm(width)
+        self.mlp = nn.Sequential(OrderedDict([("c_fc", nn.Linear(width, 4 * width)), ("gelu", nn.Identity()),
+                                              ("c_proj", nn.Linear(4 * width, width))]))
+        self.ln_2 = nn.LayerNorm(width)
+
+
+class _Transformer(nn.Module):
+    def __init__(self, width, layers, heads):
+        super().__init__()
+        self.width, self.layers = width, layers
+        self.resblocks = nn.Sequential(*[_Block(width, heads) for _ in range(layers)])
+
+
+class VisionTransformer(nn.Module):
+    """Parameter layout + geometry of the CLIP visual tower, features_only (image_encoder.py:118-198)."""
+
+    def __init__(self, input_resolution: int = 224, patch_size: int = PATCH, output_dim: int = EMBED,
+                 width: int = WIDTH, layers: int = 12, heads: int = HEADS):
+        super().__init__()
+        self.input_resolution = (input_resolution, input_resolution)
+        self.patch_size = (patch_size, patch_size)
+        self.conv1 = nn.Conv2d(3, width, kernel_size=patch_size, stride=patch_size, bias=False)
+        self.num_patches_h = self.num_patches_w = input_resolution // patch_size
+        self.class_embedding = nn.Parameter(torch.zeros(width))
+        self.positional_embedding = nn.Parameter(torch.zeros(self.num_patches_h * self.num_patches_w + 1, width))
+        self.ln_pre = nn.LayerNorm(width)
+        self.transformer = _Transformer(width, layers, heads)
+        self.ln_post = nn.LayerNorm(width)
+        self.channels, self.reduction, self.clip_embed_dim = width, patch_size, output_dim
+
+    def _interpolate_pos_embed(self, h: int, w: int) -> Tensor:
+        """image_encoder.py:183-198 (bicubic resize of the patch grid; identity at the native size)."""
+        if h == self.num_patches_h and w == self.num_patches_w:
+            return self.positional_embedding
+        pe = self.positional_embedding[1:].reshape(self.num_patches_h, self.num_patches_w, -1).permute(2, 0, 1)[None]
+        pe = F.interpolate(pe, size=(h, w), mode="bicubic")[0].permute(1, 2, 0).reshape(h * w, -1)
+        return torch.cat([self.positional_embedding[:1], pe], dim=0)
+
+
+class BasicBlock(nn.Module):
+    """models/utils.py:254-303 (the ViT decoder block, in_channels == out_channels)."""
+    expansion = 1
+
+    def __init__(self, in_channels: int, out_channels: int, **kw: Any) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_channels, out_channels, 3, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(out_channels)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(out_channels, out_channels, 3, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(out_channels)
+        self.downsample = nn.Identity()
+        if in_channels != out_channels:
+            self.downsample = nn.Sequential(nn.Conv2d(in_channels, out_channels, 1, bias=False), nn.BatchNorm2d(out_channels))
+
+    def forward(self, x: Tensor) -> Tensor:
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        out = out + self.downsample(x)
+        return self.relu(out)
+
+
+# ----------------------------------------------------------------------------- C structs
+_VP = ctypes.c_void_p
+
+
+class EbcVitLayer(ctypes.Structure):
+    _fields_ = [(n, _VP) for n in ("w_qkv", "b_qkv", "w_out", "b_out", "w_fc", "b_fc", "w_proj", "b_proj",
+                                   "ln1_g", "ln1_b", "ln2_g", "ln2_b", "wt_qkv", "wt_out", "wt_fc", "wt_proj")]
+
+
+class EbcVitWeights(ctypes.Structure):
+    _fields_ = [("layers", ctypes.c_int), ("width", ctypes.c_int), ("heads", ctypes.c_int), ("patch", ctypes.c_int),
+                ("num_vpt", ctypes.c_int)] + [(n, _VP) for n in ("w_patch", "cls", "pos", "ln_pre_g", "ln_pre_b",
+                                                                 "ln_post_g", "ln_post_b")] + [("layer", ctypes.POINTER(EbcVitLayer))]
+
+
+def _p(t: Tensor) -> int:
+    return t.data_ptr()
+
+
+class _EncoderCache:
+    """Frozen encoder weights in the compute dtype (+ transposes for the dX backward), kept resident."""
+
+    def __init__(self, enc: VisionTransformer, num_vpt: int, dtype: torch.dtype, device: torch.device):
+        self.dtype, self.device = dtype, device
+        keep: List[Tensor] = []
+
+        def cvt(t: Tensor, dt=dtype) -> Tensor:
+            r = t.detach().to(device=device, dtype=dt).contiguous()
+            keep.append(r)
+            return r
+
+        layers = len(enc.transformer.resblocks)
+        self.layer_arr = (EbcVitLayer * layers)()
+        for i, blk in enumerate(enc.transformer.resblocks):
+            L = self.layer_arr[i]
+            mats = {"qkv": blk.attn.in_proj_weight, "out": blk.attn.out_proj.weight,
+                    "fc": blk.mlp.c_fc.weight, "proj": blk.mlp.c_proj.weight}
+            for k, w in mats.items():
+                setattr(L, "w_" + k, _p(cvt(w)))
+                setattr(L, "wt_" + k, _p(cvt(w.detach().t())))
+            L.b_qkv = _p(cvt(blk.attn.in_proj_bias, torch.float32))
+            L.b_out = _p(cvt(blk.attn.out_proj.bias, torch.float32))
+            L.b_fc = _p(cvt(blk.mlp.c_fc.bias, torch.float32))
+            L.b_proj = _p(cvt(blk.mlp.c_proj.bias, torch.float32))
+            L.ln1_g, L.ln1_b = _p(cvt(blk.ln_1.weight, torch.float32)), _p(cvt(blk.ln_1.bias, torch.float32))
+            L.ln2_g, L.ln2_b = _p(cvt(blk.ln_2.weight, torch.float32)), _p(cvt(blk.ln_2.bias, torch.float32))
+        self.w_patch = cvt(enc.conv1.weight.reshape(WIDTH, -1))
+        self.cls = cvt(enc.class_embedding, torch.float32)
+        self.ln = [cvt(t, torch.float32) for t in (enc.ln_pre.weight, enc.ln_pre.bias, enc.ln_post.weight, enc.ln_post.bias)]
+        self.enc, self.num_vpt, self.layers = enc, num_vpt, layers
+        self.keep = keep
+        self.structs: Dict[Tuple[int, int], Tuple[EbcVitWeights, Tensor]] = {}
+
+    def weights(self, gh: int, gw: int) -> EbcVitWeights:
+        if (gh, gw) not in self.structs:
+            with torch.no_grad():
+                pos = self.enc._interpolate_pos_embed(gh, gw).detach().to(self.device, torch.float32).contiguous()
+            w = EbcVitWeights()
+            w.layers, w.width, w.heads, w.patch, w.num_vpt = self.layers, WIDTH, HEADS, PATCH, self.num_vpt
+            w.w_patch, w.cls, w.pos = _p(self.w_patch), _p(self.cls), _p(pos)
+            w.ln_pre_g, w.ln_pre_b, w.ln_post_g, w.ln_post_b = (_p(t) for t in self.ln)
+            w.layer = ctypes.cast(self.layer_arr, ctypes.POINTER(EbcVitLayer))
+            self.structs[(gh, gw)] = (w, pos)
+        return self.structs[(gh, gw)][0]
+
+
+class _VitFn(torch.autograd.Function):
+    """ebc_vit_forward / ebc_vit_backward: image -> ln_post(patch tokens) [B, G, 768] f32."""
+
+    @staticmethod
+    def forward(ctx, cache, image, vpt_bstride, training, *vpts):
+        L = _lib.lib()
+        B, _, H, W = image.shape
+        gh, gw = H // PATCH, W // PATCH
+        dt = _lib.dtype_code(cache.dtype)
+        dev = image.device
+        image = image.detach().float().contiguous()
+        nbytes = L.ebc_vit_workspace_bytes(B, H, W, cache.layers, cache.num_vpt, dt, int(training))
+        ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        feat = torch.empty(B, gh * gw, WIDTH, device=dev, dtype=torch.float32)
+        vp = [v.detach().float().contiguous() for v in vpts]
+        arr = (_VP * cache.layers)(*([_p(v) for v in vp] + [None] * (cache.layers - len(vp))))
+        w = cache.weights(gh, gw)
+        rc = L.ebc_vit_forward(ctypes.byref(w), _lib.ptr(image), B, H, W, arr, vpt_bstride, dt, int(training),
+                               _lib.ptr(ws), nbytes, _lib.ptr(feat), _lib.stream())
+        _lib.check(rc, "ebc_vit_forward")
+        ctx.cache, ctx.ws, ctx.shape, ctx.bstride = cache, ws, (B, H, W), vpt_bstride
+        ctx.vpt_shapes = [v.shape for v in vpts]
+        ctx.vp_keep = vp
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        L = _lib.lib()
+        cache = ctx.cache
+        B, H, W = ctx.shape
+        dvpt = [torch.empty(s, device=dfeat.device, dtype=torch.float32) for s in ctx.vpt_shapes]
+        arr = (_VP * cache.layers)(*([_p(v) for v in dvpt] + [None] * (cache.layers - len(dvpt))))
+        w = cache.weights(H // PATCH, W // PATCH)
+        rc = L.ebc_vit_backward(ctypes.byref(w), B, H, W, _lib.dtype_code(cache.dtype), _lib.ptr(ctx.ws), ctx.ws.numel(),
+                                _lib.ptr(dfeat.float().contiguous()), arr, ctx.bstride, _lib.stream())
+        _lib.check(rc, "ebc_vit_backward")
+        ctx.ws = None
+        return (None, None, None, None) + tuple(dvpt)
+
+
+class _HeadFn(torch.autograd.Function):
+    """Projection (1x1 conv as MFMA GEMM) + similarity head (models/clip/model.py:198-217)."""
+
+    @staticmethod
+    def forward(ctx, y, weight, bias, logit_scale, text, anchors, cdtype):
+        L = _lib.lib()
+        B, C, Hh, Ww = y.shape
+        P, HW, NB = B * Hh * Ww, Hh * Ww, text.shape[0]
+        dt = _lib.dtype_code(cdtype)
+        Y = y.detach().permute(0, 2, 3, 1).to(cdtype).reshape(P, C).contiguous()
+        Wc = weight.detach().reshape(EMBED, C).to(cdtype).contiguous()
+        bf = bias.detach().float().contiguous()
+        Z = torch.empty(P, EMBED, device=y.device, dtype=torch.float32)
+        _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(Y), _lib.ptr(Wc), _lib.ptr(Z), _lib.ptr(bf), None, None,
+                              P, EMBED, C, _lib.stream()), "ebc_gemm(projection)")
+        ls = logit_scale.detach().float().reshape(1).contiguous()
+        logits = torch.empty(B, NB, Hh, Ww, device=y.device, dtype=torch.float32)
+        expo = torch.empty(B, 1, Hh, Ww, device=y.device, dtype=torch.float32)
+        _lib.check(L.ebc_head_fwd(_lib.EBC_F32, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
+                                  _lib.ptr(logits), _lib.ptr(expo), P, HW, NB, _lib.stream()), "ebc_head_fwd")
+        ctx.save_for_backward(Y, Wc, Z, ls, text, anchors)
+        ctx.meta = (B, C, Hh, Ww, cdtype, y.dtype, weight.shape)
+        return logits, expo
+
+    @staticmethod
+    def backward(ctx, dlogits, dexp):
+        L = _lib.lib()
+        Y, Wc, Z, ls, text, anchors = ctx.saved_tensors
+        B, C, Hh, Ww, cdtype, ydt, wshape = ctx.meta
+        P, HW, NB = B * Hh * Ww, Hh * Ww, text.shape[0]
+        dev = Z.device
+        dl = torch.zeros(B, NB, Hh, Ww, device=dev) if dlogits is None else dlogits.float().contiguous()
+        de = torch.zeros(B, 1, Hh, Ww, device=dev) if dexp is None else dexp.float().contiguous()
+        dt = _lib.dtype_code(cdtype)
+        dZ = torch.empty(P, EMBED, device=dev, dtype=cdtype)
+        dbias = torch.empty(EMBED, device=dev, dtype=torch.float32)
+        dscale = torch.empty(1, device=dev, dtype=torch.float32)
+        _lib.check(L.ebc_head_bwd(_lib.EBC_F32, dt, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
+                                  _lib.ptr(dl), _lib.ptr(de), None, _lib.ptr(dZ), _lib.ptr(dbias), _lib.ptr(dscale),
+                                  P, HW, NB, _lib.stream()), "ebc_head_bwd")
+        Wt = Wc.t().contiguous()                                   # [C, 512]
+        dY = torch.empty(P, C, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dZ), _lib.ptr(Wt), _lib.ptr(dY), None, None, None,
+                              P, C, EMBED, _lib.stream()), "ebc_gemm(projection dX)")
+        dW = torch.mm(dZ.t(), Y).float().reshape(wshape)         # dW = dZ^T Y (library GEMM, K = B*H*W)
+        dy = dY.view(B, Hh, Ww, C).permute(0, 3, 1, 2).to(ydt)
+        return dy, dW, dbias, dscale.reshape(()), None, None, None
+
+
+# ----------------------------------------------------------------------------- model
+resnet_backbones = ["resnet50", "resnet101", "resnet50x4", "resnet50x16", "resnet50x64"]
+vit_backbones = ["vit_b_16"]
+
+
+class CLIP_EBC(nn.Module):
+    """models/clip/model.py:30-217 for the vit_b_16 backbone."""
+
+    def __init__(self, backbone: str, bins: List[Tuple[float, float]], anchor_points: List[float],
+                 reduction: Optional[int] = None, freeze_text_encoder: bool = True, prompt_type: str = "number",
+                 input_size: Optional[int] = None, num_vpt: Optional[int] = None, deep_vpt: Optional[bool] = None,
+                 vpt_drop: Optional[float] = None, decoder_cfg: Optional[List[int]] = None, vit_layers: int = 12,
+                 text_layers: int = 12, text_features: Optional[Tensor] = None, weights_seed: Optional[int] = 0,
+                 **kwargs: Any) -> None:
+        super().__init__()
+        if backbone not in vit_backbones:
+            raise NotImplementedError(f"backbone {backbone!r}: only vit_b_16 is on the MI355X path (SURVEY.md §8)")
+        assert input_size is not None, "Expected input_size to be an integer, got None."
+        assert num_vpt is not None, "Expected num_vpt to be an integer, got None."
+        assert deep_vpt is not None, "Expected deep_vpt to be a boolean, got None."
+        assert vpt_drop is not None, "Expected vpt_drop to be a float, got None."
+        self.backbone = backbone
+        self.image_encoder = VisionTransformer(input_size, PATCH, EMBED, WIDTH, vit_layers, HEADS)
+        self.image_encoder_depth = vit_layers
+        for p in self.image_encoder.parameters():
+            p.requires_grad = False
+        self.num_vpt, self.deep_vpt, self.vpt_drop = num_vpt, deep_vpt, vpt_drop
+        val = math.sqrt(6.0 / float(3 * PATCH + WIDTH))
+        for idx in range(vit_layers if deep_vpt else 1):
+            setattr(self, f"vpt_{idx}", nn.Parameter(torch.empty(num_vpt, WIDTH).uniform_(-val, val)))
+        self.encoder_reduction = PATCH
+        self.reduction = self.encoder_reduction if reduction is None else reduction
+        self.channels, self.clip_embed_dim = WIDTH, EMBED
+        decoder_cfg = decoder_cfg or [WIDTH]
+        layers, cin = [], WIDTH
+        for v in decoder_cfg:
+            layers.append(BasicBlock(cin, v))
+            cin = v
+        self.image_decoder = nn.Sequential(*layers)
+        self.channels = decoder_cfg[-1]
+        self.projection = nn.Conv2d(self.channels, EMBED, kernel_size=1)
+        self.prompt_type = prompt_type
+        self.text_encoder = CLIPTextEncoder(EMBED, 77, 49408, 512, 8, text_layers)
+        self.freeze_text_encoder = freeze_text_encoder
+        for p in self.text_encoder.parameters():
+            p.requires_grad = False
+        self.bins = bins
+        self.anchor_points = torch.tensor(anchor_points, dtype=torch.float32, requires_grad=False).view(1, -1, 1, 1)
+        self.logit_scale = nn.Parameter(torch.ones([]) * np.log(1 / 0.07), requires_grad=True)
+        pb = [b[0] if b[0] == b[1] else b for b in self.bins]
+        self.text_prompts = [format_count(b, self.prompt_type) for b in pb]
+        if weights_seed is not None:
+            self._load_synthetic(weights_seed, vit_layers, text_layers, input_size)
+        self._given_text = text_features
+        self.register_buffer("text_features", torch.zeros(len(bins), EMBED), persistent=False)
+        self.register_buffer("_anchors", self.anchor_points.reshape(-1).clone(), persistent=False)
+        self._refresh_text()
+        self._cache: Optional[_EncoderCache] = None
+        self._cache_key = None
+
+    # -- weights ---------------------------------------------------------------------------
+    def _load_synthetic(self, seed, vit_layers, text_layers, input_size):
+        sd = synthetic.full_state(seed, layers=vit_layers, text_layers=text_layers, input_size=input_size)
+        own = self.state_dict()
+        sd = {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items() if k in own}
+        self.load_state_dict(sd, strict=False)
+
+    def _refresh_text(self):
+        if getattr(self, "_given_text", None) is not None:
+            tf = torch.as_tensor(self._given_text, dtype=torch.float32)
+        else:
+            tf = self.text_encoder(prompt_tokens(self.text_prompts).to(self.text_encoder.positional_embedding.device)).float()
+        with torch.no_grad():
+            self.text_features.copy_(tf.to(self.text_features.device))
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        res = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        if hasattr(self, "text_features"):
+            self._refresh_text()
+        self._cache = None
+        return res
+
+    def _apply(self, fn, recurse=True):
+        self._cache = None
+        return super()._apply(fn, recurse)
+
+    def _encoder_cache(self, dtype: torch.dtype, device: torch.device) -> _EncoderCache:
+        ver = sum(p._version for p in self.image_encoder.parameters())
+        key = (dtype, device, ver)
+        if self._cache is None or self._cache_key != key:
+            self._cache = _EncoderCache(self.image_encoder, self.num_vpt, dtype, device)
+            self._cache_key = key
+        return self._cache
+
+    # -- forward ---------------------------------------------------------------------------
+    def _compute_dtype(self, x: Tensor) -> torch.dtype:
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            return torch.get_autocast_dtype("cuda")
+        return torch.float32
+
+    def _prepare_vpts(self, B: int) -> Tuple[List[Tensor], int]:
+        n = self.image_encoder_depth if self.deep_vpt else 1
+        vpts = [getattr(self, f"vpt_{i}") for i in range(n)]
+        if self.training and self.vpt_drop and self.vpt_drop > 0:          # model.py:131-140 (per-crop dropout)
+            vpts = [F.dropout(v.unsqueeze(0).expand(B, -1, -1), self.vpt_drop, True).contiguous() for v in vpts]
+            return vpts, self.num_vpt * WIDTH
+        return vpts, 0
+
+    def _forward_vpt(self, x: Tensor) -> Tensor:
+        """[B,3,H,W] -> [B,768,H/16,W/16] (channels_last memory), models/clip/model.py:142-189."""
+        B, _, H, W = x.shape
+        cache = self._encoder_cache(self._compute_dtype(x), x.device)
+        vpts, bstride = self._prepare_vpts(B)
+        training = torch.is_grad_enabled() and any(v.requires_grad for v in vpts)
+        with torch.autocast("cuda", enabled=False):
+            feat = _VitFn.apply(cache, x, bstride, training, *vpts)
+        return feat.view(B, H // PATCH, W // PATCH, WIDTH).permute(0, 3, 1, 2)
+
+    def forward(self, x: Tensor) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+        if not x.is_cuda:
+            raise RuntimeError("ebc_amd.CLIP_EBC runs on the MI355X HIP path only (input is on the CPU)")
+        cdt = self._compute_dtype(x)
+        x = self._forward_vpt(x)
+        if self.reduction != self.encoder_reduction:
+            x = F.interpolate(x, scale_factor=self.encoder_reduction / self.reduction, mode="bilinear")
+        x = self.image_decoder(x)
+        with torch.autocast("cuda", enabled=False):
+            logits, exp = _HeadFn.apply(x, self.projection.weight, self.projection.bias, self.logit_scale,
+                                        self.text_features, self._anchors, cdt)
+        return (logits, exp) if self.training else exp
+
+
+def _clip_ebc(backbone: str, bins, anchor_points, reduction=None, freeze_text_encoder=True, prompt_type="number",
+              input_size=None, num_vpt=None, deep_vpt=None, vpt_drop=None, decoder_block=None, decoder_cfg=None,
+              **kw) -> CLIP_EBC:
+    """models/clip/model.py:220-270 (vit_b_16: BasicBlock decoder [768])."""
+    return CLIP_EBC(backbone, bins, anchor_points, reduction=reduction, freeze_text_encoder=freeze_text_encoder,
+                    prompt_type=prompt_type, input_size=input_size, num_vpt=num_vpt, deep_vpt=deep_vpt,
+                    vpt_drop=vpt_drop, decoder_cfg=decoder_cfg, **kw)
+
+
+def get_model(backbone: str, input_size: int, reduction: int, bins: Optional[List[Tuple[float, float]]] = None,
+              anchor_points: Optional[List[float]] = None, **kwargs: Any) -> CLIP_EBC:
+    """models/__init__.py:10-44.  Only the CLIP ViT-B/16 family is on the MI355X path."""
+    backbone = backbone.lower()
+    if "clip" not in backbone:
+        raise NotImplementedError(f"{backbone}: only clip_vit_b_16 is built for MI355X (SURVEY.md §8)")
+    backbone = backbone[5:]
+    assert bins is not None and anchor_points is not None, "CLIP-EBC needs bins and anchor_points"
+    kwargs.setdefault("prompt_type", "number")
+    kwargs.setdefault("num_vpt", 32)
+    kwargs.setdefault("vpt_drop", 0.0)
+    kwargs.setdefault("deep_vpt", True)
+    return _clip_ebc(backbone=backbone, input_size=input_size, reduction=reduction, bins=bins,
+                     anchor_points=anchor_points, **kwargs)

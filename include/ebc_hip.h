@@ -79,6 +79,71 @@ enum { EBC_EPI_STORE = 0, EBC_EPI_GELU = 1, EBC_EPI_RESID = 2, EBC_EPI_GELU_BWD 
 int ebc_gemm(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
              const float* bias, const float* resid, void* aux, int M, int N, int K, ebc_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * CLIP ViT-B/16 + deep VPT encoder: CLIP_EBC._forward_vpt (models/clip/model.py:142-189), whole
+ * forward and dX-only backward (frozen encoder: gradients reach the VPT tokens only), one call each.
+ * Weight pointers are device memory of `dtype` (matrices, nn.Linear [out, in] layout) or f32
+ * (biases, LayerNorm, embeddings); wt_* are the transposed matrices [in, out] used by backward.
+ * The EbcVitWeights / EbcVitLayer structs themselves live in HOST memory.
+ */
+typedef struct {
+    const void* w_qkv;  const float* b_qkv;    /* attn.in_proj_weight [2304,768], in_proj_bias */
+    const void* w_out;  const float* b_out;    /* attn.out_proj [768,768] */
+    const void* w_fc;   const float* b_fc;     /* mlp.c_fc [3072,768] */
+    const void* w_proj; const float* b_proj;   /* mlp.c_proj [768,3072] */
+    const float* ln1_g; const float* ln1_b; const float* ln2_g; const float* ln2_b;
+    const void* wt_qkv; const void* wt_out; const void* wt_fc; const void* wt_proj;   /* transposes */
+} EbcVitLayer;
+
+typedef struct {
+    int layers, width, heads, patch, num_vpt;
+    const void* w_patch;                        /* conv1.weight as [768, 3*16*16] */
+    const float* cls;                           /* class_embedding [768] */
+    const float* pos;                           /* positional_embedding [G+1, 768] for this input size */
+    const float* ln_pre_g; const float* ln_pre_b; const float* ln_post_g; const float* ln_post_b;
+    const EbcVitLayer* layer;                   /* host array [layers] */
+} EbcVitWeights;
+
+/* Workspace (device bytes) holding the saved activations (training) or the ping-pong buffers. */
+size_t ebc_vit_workspace_bytes(int B, int H, int W, int layers, int num_vpt, int dtype, int training);
+/* image [B,3,H,W] f32 -> feat [B, (H/16)*(W/16), 768] f32 (= ln_post of the patch tokens, NHWC).
+ * vpt: host array [layers] of device pointers ([num_vpt,768] f32, or [B,num_vpt,768] with
+ * vpt_bstride = num_vpt*768 elements for per-crop prompts); vpt[l] == NULL for l > 0 keeps the
+ * previous block's prompt outputs (shallow VPT, model.py:177-178). */
+int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B, int H, int W,
+                    const float* const* vpt, long vpt_bstride, int dtype, int training,
+                    void* workspace, size_t workspace_bytes, float* feat, ebc_stream_t stream);
+/* dfeat [B, G, 768] f32 -> dvpt[l] ([num_vpt,768] f32, summed over crops; per crop if vpt_bstride). */
+int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int dtype, void* workspace,
+                     size_t workspace_bytes, const float* dfeat, float* const* dvpt, long vpt_bstride,
+                     ebc_stream_t stream);
+
+/* LayerNorm over 768 channels (models/clip/_clip/blocks.py:8-14, fp32 math, eps 1e-5).
+ * Row r of the output reads input row (r / rows_per_group) * group_stride + group_offset +
+ * r % rows_per_group (rows_per_group = 0: identity), e.g. ln_post on the patch rows only. */
+int ebc_layernorm_fwd(int dtype, const float* x, int rows_per_group, int group_stride, int group_offset,
+                      const float* gamma, const float* beta, void* out, float* out_f32, float* mean,
+                      float* rstd, int M, int D, ebc_stream_t stream);
+int ebc_layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rows_per_group,
+                      int group_stride, int group_offset, const float* mean, const float* rstd,
+                      const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, int D,
+                      ebc_stream_t stream);
+/* Multi-head attention on the packed qkv [B*L, 3*H*64] (nn.MultiheadAttention, need_weights=False,
+ * blocks.py:35-37): out [B*L, H*64], lse [B,H,L]; backward writes dqkv [B*L, 3*H*64]. */
+int ebc_attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, ebc_stream_t stream);
+int ebc_attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse,
+                      float* delta_ws, void* dqkv, int B, int L, int H, ebc_stream_t stream);
+/* Blockwise image-text similarity head (models/clip/model.py:200-217):
+ * Z [P=B*HW, 512] projected features (NHWC rows) -> logits [B,NB,HW], exp [B,1,HW].
+ * Backward: dZ (element type dtype_dz), d projection bias (column sums), d logit_scale; gscale (device scalar) scales the
+ * upstream gradients (NULL = 1). */
+int ebc_head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+                 float* logits, float* expo, int P, int HW, int NB, ebc_stream_t stream);
+int ebc_head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
+                 const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
+                 float* dbias, float* dscale, int P, int HW, int NB, ebc_stream_t stream);
+int ebc_cast_f32(int dtype, const float* in, void* out, size_t n, ebc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

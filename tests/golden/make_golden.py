@@ -250,9 +250,32 @@ def text_case(ref):
                 text_features_word=m.text_features.numpy(), text_features_number=mn.text_features.numpy())
 
 
+def prompt_table(ref):
+    """CLIP BPE ids of the standard count prompts (data asset for ebc_amd/text.py; the product
+    has no tokenizer of its own: clip-ebc_amd/ebc_amd/data/prompt_tokens.json)."""
+    import json
+    fc = sys.modules["models.clip.utils"].format_count
+    prompts = set()
+    for t in ("word", "number"):
+        for n in range(0, 101):
+            prompts.add(fc(n, t))
+            prompts.add(fc((n, float("inf")), t))
+    prompts = sorted(prompts)
+    toks = ref.tokenize(prompts)
+    table = {p: [int(x) for x in toks[i].tolist() if x != 0] for i, p in enumerate(prompts)}
+    path = os.path.join(REPO, "clip-ebc_amd", "ebc_amd", "data", "prompt_tokens.json")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(table, f, separators=(",", ":"), sort_keys=True)
+    print("wrote", path, len(table), "prompts")
+
+
 def main():
     torch.set_num_threads(8)
     ref = load_reference()
+    prompt_table(ref)
+    if "--tokens-only" in sys.argv:
+        return
     save("f6_text.npz", **text_case(ref))
     save("f1_loss_224.npz", **loss_case(ref, 224, [0, 1, 3, 10, 47, 200, 1000, 25], seed=101))
     save("f1_loss_448.npz", **loss_case(ref, 448, [5, 0, 150, 2000], seed=202))
