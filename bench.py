@@ -1,0 +1,209 @@
+"""Benchmark: train crops/s for clip_vit_b_16 + deep VPT(32) + DMCount at 224x224 on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--crops-per-gpu B] [--dtype fp16|bf16|fp32]
+
+One step = forward (autocast, like the reference train.py:36-40) + DACE/DMCount loss (on-device
+Sinkhorn) + backward + GradScaler/Adam step over the 11.3 M trainable parameters, on synthetic
+crops pre-staged in HBM (BASELINE.md "Synthetic inputs").  N > 1: one process per GPU under
+torch.distributed.run, DDP over RCCL with SyncBatchNorm as trainer.py:147; weak scaling (fixed
+crops per GPU).  Rank 0 prints ONE JSON line (see README / DESIGN.md §Measurement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "clip-ebc_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BINS = [(0.0, 0.0), (1.0, 1.0), (2.0, 2.0), (3.0, 3.0), (4.0, float("inf"))]
+ANCHORS_NWPU = [0.0, 1.0, 2.0, 3.0, 4.21931]     # configs/reduction_8.json ["4"]["nwpu"]["average"]
+FLOP_PER_CROP = 135.63e9                          # 58.33 fwd + 77.30 bwd GFLOP
+MFMA_PEAK_TF = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.3}   # MI355X dense (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--crops-per-gpu", type=int, default=16)
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
+    ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled through")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-crops", type=int, default=8, help="crops per CPU-baseline step")
+    ap.add_argument("--cpu-steps", type=int, default=12)
+    return ap.parse_args()
+
+
+def make_batch(B, rank, step, device):
+    """BASELINE.md synthetic crops: seed 1000 + rank*100003 + step, lognormal(ln 20, 1.2) points."""
+    from ebc_amd import synthetic as syn
+    img, pts, dens = syn.synthetic_crops(B, 224, seed=1000 + rank * 100003 + step)
+    return (torch.from_numpy(img).to(device), [torch.from_numpy(p).to(device) for p in pts],
+            torch.from_numpy(dens).to(device), [len(p) for p in pts])
+
+
+def cpu_baseline(args, crops, steps):
+    """The oracle (oracle/ref.py: torch-fp32 CPU restatement of the reference step) on host cores."""
+    from oracle import ref
+    from ebc_amd import synthetic as syn
+    nthreads = torch.get_num_threads()
+    sd = syn.full_state(0, layers=12, include_text=False)
+    p = ref.params_from_state(sd)
+    train = [v for k, v in p.items() if v.requires_grad]
+    opt = torch.optim.Adam(train, lr=1e-4, weight_decay=1e-4)
+    txt = torch.randn(5, 512, generator=torch.Generator().manual_seed(0))
+
+    def step(s):
+        img, pts, dens = syn.synthetic_crops(crops, 224, seed=5000 + s)
+        logits, exp, _ = ref.forward(p, torch.from_numpy(img), txt, ANCHORS_NWPU, 12)
+        loss, _ = ref.dace_loss(logits, exp, torch.from_numpy(dens), pts, BINS)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step(0)                                                  # warm-up
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step(s + 1)
+    dt = time.perf_counter() - t0
+    return {"value": round(crops * steps / dt, 4), "unit": "crops/s", "cores": nthreads, "kind": "port",
+            "sample": f"{steps} steps x {crops} crops (fwd+DACE/DMCount+bwd+Adam, fp32, 12 layers) of the oracle "
+                      f"oracle/ref.py on {nthreads} host threads; {dt:.1f}s"}
+
+
+def probe_kernels(dtype, device, reps=50):
+    """Time the dominant encoder GEMM (MLP c_fc, M = 16*229) and the Sinkhorn loss kernel alone with
+    HIP events on the current stream; returns roofline entries."""
+    from ebc_amd import _lib
+    L = _lib.lib()
+    tdt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}[dtype]
+    M, N, K = 16 * 229, 3072, 768
+    A = torch.randn(M, K, device=device).to(tdt)
+    Bw = (torch.randn(N, K, device=device) / 28).to(tdt)
+    C = torch.empty(M, N, device=device, dtype=tdt)
+    aux = torch.empty(M, N, device=device, dtype=tdt)
+    bias = torch.zeros(N, device=device)
+    code = _lib.dtype_code(tdt)
+
+    def launch():
+        _lib.check(L.ebc_gemm(code, 1, 0, _lib.ptr(A), _lib.ptr(Bw), _lib.ptr(C), _lib.ptr(bias), None,
+                              _lib.ptr(aux), M, N, K, _lib.stream()), "probe gemm")
+    for _ in range(5):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    flops = 2.0 * M * N * K
+    return {"kernel": "gemm_nt_kernel<f16,GELU> (MLP c_fc 3664x3072x768, aux store)", "avg_us": t * 1e6,
+            "achieved": flops / t / 1e12, "flops_per_launch": flops}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    device = torch.device(f"cuda:{local}")
+    torch.manual_seed(42 + rank)
+
+    from ebc_amd.model import get_model
+    from ebc_amd.losses import DACELoss
+    model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
+                      vpt_drop=0.0, deep_vpt=True).to(device)
+    model.train()
+    if world > 1:
+        model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], output_device=local)
+    loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=224).to(device)
+    params = [p for p in model.parameters() if p.requires_grad]
+    try:
+        opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
+    except Exception:
+        opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4)
+    amp_dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.dtype]
+    scaler = torch.amp.GradScaler("cuda", enabled=args.dtype == "fp16")
+    B = args.crops_per_gpu
+    pool = [make_batch(B, rank, s, device) for s in range(args.pool)]
+    info_buf = torch.zeros(5, device=device)
+
+    def step(i):
+        img, pts, dens, _ = pool[i % len(pool)]
+        with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
+            logits, exp = model(img)
+            loss, info = loss_fn(logits, exp, dens, pts)
+        opt.zero_grad(set_to_none=True)
+        scaler.scale(loss).backward()
+        scaler.step(opt)
+        scaler.update()
+        # one packed all-reduce of the 5 loss_info scalars (reference: 5 separate + .item(), train.py:62)
+        torch.stack([info[k] for k in ("loss", "ot_loss", "tv_loss", "count_loss", "ce_loss")], out=info_buf)
+        if world > 1:
+            dist.all_reduce(info_buf)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    crops = B * world * args.steps
+    value = crops / elapsed
+    ms = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        probe = probe_kernels(args.dtype, device)
+        peak = MFMA_PEAK_TF[args.dtype]
+        out = {
+            "metric": "train crops/sec clip_vit_b_16 224px @1/2/4/8 MI355X; MAE parity",
+            "value": round(value, 3), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (BASELINE.md crops, pre-staged in HBM; synthetic random-init weights)",
+            "config": {"workload": f"clip_vit_b_16 224x224 deep-VPT(32) + DACE/DMCount train step, "
+                                   f"{B} crops/GPU, AMP {args.dtype} (BASELINE configs[2]" + (", DDP configs[3] shape" if world > 1 else "") + ")",
+                       "global_batch": B * world, "seq_len": 229, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(probe["achieved"], 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(probe["achieved"] / peak, 4), "traffic": None,
+                         "kernel": probe["kernel"], "avg_us": round(probe["avg_us"], 2)},
+            "step_roofline": {"flop_per_crop": FLOP_PER_CROP, "achieved_tflops": round(value / world * FLOP_PER_CROP / 1e12, 2),
+                              "frac": round(value / world * FLOP_PER_CROP / 1e12 / peak, 4)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, args.cpu_crops, args.cpu_steps)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
