@@ -41,6 +41,8 @@ SIGNATURES = {
     "ebc_head_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "ebc_head_bwd": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "ebc_cast_f32": (_I, [_I, _P, _P, _Z, _P]),
+    "ebc_tile_gather": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "ebc_tile_assemble": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
 }
 
 

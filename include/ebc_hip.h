@@ -144,6 +144,15 @@ int ebc_head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, co
                  float* dbias, float* dscale, int P, int HW, int NB, ebc_stream_t stream);
 int ebc_cast_f32(int dtype, const float* in, void* out, size_t n, ebc_stream_t stream);
 
+/* Sliding-window evaluation (utils/eval_utils.py:26-96).  Tiles t = i*cols + j, rows/cols =
+ * ceil((H-wh)/sh)+1, last row/column snapped to the border.
+ * gather:   tiles [tile_count, C, wh, ww] <- image [C, H, W], tiles tile_begin .. +tile_count
+ * assemble: out [Cp, H/r, W/r] = per-pixel mean of preds [rows*cols, Cp, wh/r, ww/r] */
+int ebc_tile_gather(const float* image, float* tiles, int C, int H, int W, int wh, int ww, int sh, int sw,
+                    int tile_begin, int tile_count, ebc_stream_t stream);
+int ebc_tile_assemble(const float* preds, float* out, int Cp, int H, int W, int wh, int ww, int sh, int sw,
+                      int reduction, ebc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,51 @@
+"""GPU: sliding-window tiling + overlap averaging (ebc_tile_gather / ebc_tile_assemble) against the
+reference's own outputs (F5 fixture: utils/eval_utils.py:26-96 run with a stub model), and the
+full-model sliding-window path."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import ANCHORS_NWPU, BINS, golden
+
+pytestmark = pytest.mark.gpu
+
+
+class Stub(torch.nn.Module):
+    reduction = 8
+
+    def forward(self, x):
+        return torch.nn.functional.avg_pool2d(x.mean(1, keepdim=True).abs(), 8)
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_sliding_window_matches_reference_fixture(case):
+    from ebc_amd.eval_utils import sliding_window_predict
+    d = golden("f5_sliding.npz")
+    H, W, win, stride = (int(v) for v in d[f"cfg_{case}"])
+    img = np.random.Generator(np.random.PCG64(11 + case)).standard_normal((1, 3, H, W)).astype(np.float32)
+    out = sliding_window_predict(Stub(), torch.from_numpy(img).cuda(), win, stride, max_tiles_per_batch=5)
+    assert out.shape == d[f"pred_{case}"].shape and out.device.type == "cpu"
+    np.testing.assert_allclose(out.numpy(), d[f"pred_{case}"], rtol=2e-6, atol=1e-7)
+
+
+def test_sliding_window_full_model_counts():
+    """2-layer model on a 500x700 image: the tiled eval equals averaging per-tile model outputs."""
+    from ebc_amd.eval_utils import sliding_window_predict, tile_grid
+    from ebc_amd.model import get_model
+    txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
+    m = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", vit_layers=2, text_features=txt).cuda().eval()
+    img = torch.randn(1, 3, 500, 700, device="cuda")
+    out = sliding_window_predict(m, img, 224, 224)
+    rows, cols = tile_grid(500, 700, (224, 224), (224, 224))
+    tiles, origins = [], []
+    for i in range(rows):
+        for j in range(cols):
+            y = min(i * 224, 500 - 224); x = min(j * 224, 700 - 224)
+            tiles.append(img[:, :, y:y + 224, x:x + 224]); origins.append((y, x))
+    with torch.no_grad():
+        preds = m(torch.cat(tiles)).cpu()
+    acc = torch.zeros(1, 500 // 8, 700 // 8); cnt = torch.zeros_like(acc)
+    for t, (y, x) in enumerate(origins):
+        acc[:, y // 8:(y + 224) // 8, x // 8:(x + 224) // 8] += preds[t]
+        cnt[:, y // 8:(y + 224) // 8, x // 8:(x + 224) // 8] += 1
+    np.testing.assert_allclose(out[0].numpy(), (acc / cnt).numpy(), rtol=1e-5, atol=1e-6)
