@@ -12,7 +12,7 @@
 // column reads); scores for 16 query rows x 256 keys live in registers, so no online softmax.
 // Operand orientation ("swapped" S^T = K Q^T) puts each query on one lane, so the probability
 // accumulators are directly the A operand of P.V with no LDS round trip (mfma.h).
-//   grid: B * H * ceil(L/64) workgroups of 4 waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
+//   grid: B * H * ceil(L/128) workgroups of 8 waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
 #include "ebc_common.h"
 #include "mfma.h"
 
@@ -23,6 +23,9 @@ namespace {
 constexpr int HD = 64;          // head dim
 constexpr int LP = 256;         // padded sequence (>= L)
 constexpr int NKT = LP / 16;    // 16-row tiles
+constexpr int NWV = 8;          // waves per workgroup (16 queries / keys each)
+constexpr int QB = 16 * NWV;    // queries (fwd, dQ) or keys (dKV) per workgroup
+constexpr float LOG2E = 1.4426950408889634f;
 
 template <class E> struct AttnCfg {
     using T = typename E::T;
@@ -37,11 +40,19 @@ __device__ __forceinline__ void load_rows(typename E::T* dst, const typename E::
 {
     // dst[s][0..63] = src[s*ld + 0..63] for s < L, zero for L <= s < LP
     using C = AttnCfg<E>;
-    for (int e = threadIdx.x; e < LP * C::CPR; e += blockDim.x) {
+    constexpr int PER = LP * C::CPR / (64 * NWV);          // 16-B chunks per thread (all loads first)
+    uint4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int e = threadIdx.x + k * 64 * NWV;
         const int s = e / C::CPR, c = e % C::CPR;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (s < L) v = *reinterpret_cast<const uint4*>(src + (size_t)s * ld + c * (16 / C::EB));
-        *reinterpret_cast<uint4*>(dst + s * C::LDR + c * (16 / C::EB)) = v;
+        v[k] = s < L ? *reinterpret_cast<const uint4*>(src + (size_t)s * ld + c * (16 / C::EB)) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int e = threadIdx.x + k * 64 * NWV;
+        const int s = e / C::CPR, c = e % C::CPR;
+        *reinterpret_cast<uint4*>(dst + s * C::LDR + c * (16 / C::EB)) = v[k];
     }
 }
 
@@ -62,7 +73,7 @@ __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* bas
 
 // ------------------------------------------------------------------------------ forward
 template <class E>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const typename E::T* __restrict__ qkv, typename E::T* __restrict__ out,
+__global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T* __restrict__ qkv, typename E::T* __restrict__ out,
                                                        float* __restrict__ lse, int B, int L, int H, float scale)
 {
     using T = typename E::T;
@@ -70,7 +81,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename E::T* __re
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
-    const int nqb = (L + 63) / 64;
+    const int nqb = (L + QB - 1) / QB;
     const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
@@ -79,7 +90,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename E::T* __re
     load_rows<E>(Vs, base + 2 * D, D3, L);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
-    const int q0 = qb * 64 + w * 16;
+    const int q0 = qb * QB + w * 16;
     const int qme = q0 + fr;                                   // this lane's query (column of S^T)
     typename E::Frag qf[2];
 #pragma unroll
@@ -109,7 +120,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename E::T* __re
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { s[kt][i] = expf(s[kt][i] - mx); sum += s[kt][i]; }
+        for (int i = 0; i < 4; ++i) { s[kt][i] = __builtin_amdgcn_exp2f((s[kt][i] - mx) * LOG2E); sum += s[kt][i]; }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
 
@@ -142,7 +153,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename E::T* __re
 
 // ------------------------------------------------------------------------------ backward dQ
 template <class E>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+__global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                                           typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
 {
@@ -151,7 +162,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const typename E::T* _
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
-    const int nqb = (L + 63) / 64;
+    const int nqb = (L + QB - 1) / QB;
     const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
@@ -160,7 +171,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const typename E::T* _
     load_rows<E>(Vs, base + 2 * D, D3, L);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
-    const int q0 = qb * 64 + w * 16;
+    const int q0 = qb * QB + w * 16;
     const int qme = q0 + fr;
     const bool qv = qme < L;
     typename E::Frag qf[2], df[2];
@@ -192,7 +203,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const typename E::T* _
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int key = 16 * kt + 4 * fg + i;
-                const float p = key < L ? expf(sv[i] * scale - lq) : 0.f;
+                const float p = key < L ? __builtin_amdgcn_exp2f((sv[i] * scale - lq) * LOG2E) : 0.f;
                 ds[4 * hf + i] = p * (pv[i] - dq);
             }
         }
@@ -213,7 +224,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const typename E::T* _
 
 // ------------------------------------------------------------------------------ backward dK, dV
 template <class E>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+__global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                            const float* __restrict__ lse, const float* __restrict__ delta,
                                                            typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
 {
@@ -224,7 +235,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const typename E::T* 
     T* Ds = reinterpret_cast<T*>(smem + C::TILE_BYTES);
     float* ls = reinterpret_cast<float*>(smem + 2 * C::TILE_BYTES);
     float* dl = ls + LP;
-    const int nkb = (L + 63) / 64;
+    const int nkb = (L + QB - 1) / QB;
     const int bh = blockIdx.x / nkb, kb = blockIdx.x % nkb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
@@ -237,7 +248,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const typename E::T* 
     }
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
-    const int k0 = kb * 64 + w * 16;
+    const int k0 = kb * QB + w * 16;
     const int kme = k0 + fr;
     const bool kv = kme < L;
     typename E::Frag kf[2], vf[2];
@@ -268,7 +279,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const typename E::T* 
             const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float p = expf(sv[i] * scale - lq[i]);     // lse = +inf for padded queries -> 0
+                const float p = __builtin_amdgcn_exp2f((sv[i] * scale - lq[i]) * LOG2E);   // lse = +inf (padding) -> 0
                 pp[4 * hf + i] = p;
                 ds[4 * hf + i] = p * (pv[i] - dq[i]);
             }
@@ -303,8 +314,8 @@ template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B,
         if (hipFuncSetAttribute((const void*)attn_fwd_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
         attr = true;
     }
-    const int grid = B * H * ((L + 63) / 64);
-    hipLaunchKernelGGL(attn_fwd_kernel<E>, dim3(grid), dim3(256), lds, st, (const typename E::T*)qkv,
+    const int grid = B * H * ((L + QB - 1) / QB);
+    hipLaunchKernelGGL(attn_fwd_kernel<E>, dim3(grid), dim3(64 * NWV), lds, st, (const typename E::T*)qkv,
                        (typename E::T*)out, lse, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
@@ -321,11 +332,11 @@ template <class E> int attn_bwd_t(const void* qkv, const void* dout, const float
         if (hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv) != hipSuccess) return EBC_E_LAUNCH;
         attr = true;
     }
-    const int grid = B * H * ((L + 63) / 64);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<E>, dim3(grid), dim3(256), lds_dq, st, (const typename E::T*)qkv,
+    const int grid = B * H * ((L + QB - 1) / QB);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<E>, dim3(grid), dim3(64 * NWV), lds_dq, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<E>, dim3(grid), dim3(256), lds_kv, st, (const typename E::T*)qkv,
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<E>, dim3(grid), dim3(64 * NWV), lds_kv, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
     return EBC_OK;

@@ -12,9 +12,9 @@
 //    (dm_loss.py:53-59), so K = exp(C/-reg) = Ey_i[iy] * Ex_i[jx] with Ey = exp(yd/-reg),
 //    Ex = exp(xd/-reg).  A crop's kernel matrix shrinks from n*g^2 to 2*n*g floats, which fits
 //    the 160 KiB LDS for n <= ~470 (g = 28) and streams from L2 above that.
-//  * K^T u (a [g x n][n x g] product) is register-tiled 4x4 per thread and split over point
-//    slices; K v is computed per point as sum_iy Ey[iy] * (sum_jx Ex[jx] v[iy][jx]) with the
-//    v rows of a row-group held in registers (wave-uniform broadcast LDS reads).
+//  * exp(C/-reg) underflows to exactly 0 beyond ~32 px (reg = 10), so each point's factors are
+//    nonzero on a <= 9-row x 9-column window: K^T u and K v run over those windows only
+//    (~10x fewer FMAs at g = 28, ~40x at g = 56), accumulated with LDS float atomics.
 //  * The reference's control flow is kept exactly: err every eval_freq iterations
 //    (bregman_pytorch.py:117-126), stop when err <= stopThr or it > maxIter, NaN/Inf rollback
 //    to the previous (u, v) and break (:111-115), the 1e-16 epsilons, denormals kept (the build
@@ -26,23 +26,16 @@ using namespace ebc;
 namespace {
 
 constexpr int NT = 512;                  // threads per workgroup (8 waves, 2 per SIMD)
-constexpr int NWAVE = NT / 64;
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
 
 template <int G> struct Cfg {
     static constexpr int GG = G * G;
-    static constexpr int NTILE = (G / 4) * (G / 4);      // 4x4 output tiles of K^T u
-    static constexpr int SL = NT / NTILE;                // point slices
-    static constexpr int R = (G <= 28) ? 4 : 2;          // rows per group in the K v pass
-    static constexpr int NG = G / R;                     // row groups
-    // fixed LDS (floats): pd, td, b, v0, v1, ktu, red[SL*GG], kvred[NWAVE*64], misc[64]
-    static constexpr int FIXED = 6 * GG + SL * GG + NWAVE * 64 + 64;
+    // fixed LDS (floats): pd, td, b, v0, v1, ktu, misc[64]
+    static constexpr int FIXED = 6 * GG + 64;
     static constexpr size_t FIXED_BYTES = (size_t)FIXED * 4;
-    static constexpr int PER_POINT = 2 * G + 2;          // Ey, Ex, u0, u1
-    static_assert(NTILE * SL <= NT && SL >= 1, "tiling");
-    static_assert(G % 4 == 0 && G % R == 0, "grid");
+    static constexpr int PER_POINT = 2 * G + 3;          // Ey, Ex, u0, u1, window
 };
 
 struct Params {
@@ -70,14 +63,31 @@ __device__ __forceinline__ float pcoord(float p, int size, int norm) {
     return norm ? p / (float)size * 2.0f - 1.0f : p;     // dm_loss.py:51
 }
 
-template <int G, typename FP>
+// Per point, K's separable factors are exactly zero outside a short window (exp(C/-reg)
+// underflows beyond ~32 px for reg = 10, i.e. <= 9 grid rows/columns): both products run over
+// [ylo, ylo+ylen) x [xlo, xlo+xlen) only.  Skipping exact zeros leaves every value unchanged up to
+// summation order; the windows are read off the computed factors, so any reg works.
+// Accumulation uses LDS float atomics (order-nondeterministic at the ~1e-7 relative level).
+__device__ __forceinline__ int block_max(int v, int* scratch) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    __syncthreads();
+    if (lane == 0) scratch[w] = v;
+    __syncthreads();
+    int r = 0;
+    for (int i = 0; i < nw; ++i) r = max(r, scratch[i]);
+    return r;
+}
+
+template <int G, typename FP, typename IP>
 __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
-                              const float* __restrict__ pts, FP Ey, FP Ex, FP u0, FP u1,
-                              const float* b, float* v0, float* v1, float* ktu, float* red,
-                              float* kvred, float* misc, int* iters_out, int* rolled_out, float* err_last_out)
+                              const float* __restrict__ pts, FP Ey, FP Ex, FP u0, FP u1, IP win,
+                              const float* b, float* v0, float* v1, float* ktu, float* misc,
+                              int* iters_out, int* rolled_out, float* err_last_out)
 {
-    using C = Cfg<G>;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    constexpr int GG = G * G;
+    const int t = threadIdx.x;
     const float a = 1.0f / (float)n;                         // target_prob = ones/n
     // factors: Ey[i][iy] = exp(yd/-reg), Ex[i][jx] = exp(xd/-reg)
     for (int e = t; e < n * G; e += NT) {
@@ -90,46 +100,39 @@ __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter
         Ex[e] = expf(xd / -reg);
     }
     for (int i = t; i < n; i += NT) u0[i] = 1.0f / (float)n;
-    for (int j = t; j < C::GG; j += NT) v0[j] = 1.0f / (float)C::GG;
+    for (int j = t; j < GG; j += NT) v0[j] = 1.0f / (float)GG;
     __syncthreads();
+    // nonzero windows (exp of a convex quadratic: the nonzeros are contiguous)
+    int wy_max = 0;
+    for (int i = t; i < n; i += NT) {
+        int ylo = G, yhi = -1, xlo = G, xhi = -1;
+        for (int k = 0; k < G; ++k) {
+            if (Ey[i * G + k] != 0.f) { ylo = min(ylo, k); yhi = k; }
+            if (Ex[i * G + k] != 0.f) { xlo = min(xlo, k); xhi = k; }
+        }
+        const int ylen = yhi >= ylo ? yhi - ylo + 1 : 0, xlen = xhi >= xlo ? xhi - xlo + 1 : 0;
+        win[i] = (ylen ? ylo : 0) | (ylen << 8) | ((xlen ? xlo : 0) << 16) | (xlen << 24);
+        wy_max = max(wy_max, ylen);
+    }
+    const int WY = block_max(wy_max, reinterpret_cast<int*>(misc));
+    const int items = n * WY;
 
     FP u = u0; FP un = u1;
     float* v = v0; float* vn = v1;
     int have_ktu = 0, it = 1, rolled = 0;
     float err = 1.0f, err_last = -1.0f;
 
-    // K^T u into ktu[GG] (or reuse)
+    // K^T u into ktu[GG]: one item = one (point, window row)
     auto ktu_pass = [&](FP uu) {
-        const int tile = t % C::NTILE, s = t / C::NTILE;
-        if (s < C::SL) {
-            const int ty = tile / (G / 4), tx = tile % (G / 4);
-            float acc[4][4];
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[p][q] = 0.f;
-            for (int i = s; i < n; i += C::SL) {
-                const float w = uu[i];
-                const float4 ey = *reinterpret_cast<const float4*>(&Ey[i * G + 4 * ty]);
-                const float4 ex = *reinterpret_cast<const float4*>(&Ex[i * G + 4 * tx]);
-                const float wy[4] = {w * ey.x, w * ey.y, w * ey.z, w * ey.w};
-                const float xx[4] = {ex.x, ex.y, ex.z, ex.w};
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[p][q] = fmaf(wy[p], xx[q], acc[p][q]);
-            }
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-                *reinterpret_cast<float4*>(&red[s * C::GG + (4 * ty + p) * G + 4 * tx]) =
-                    make_float4(acc[p][0], acc[p][1], acc[p][2], acc[p][3]);
-        }
+        for (int j = t; j < GG; j += NT) ktu[j] = 0.f;
         __syncthreads();
-        for (int j = t; j < C::GG; j += NT) {
-            float sacc = 0.f;
-#pragma unroll
-            for (int s2 = 0; s2 < C::SL; ++s2) sacc += red[s2 * C::GG + j];
-            ktu[j] = sacc;
+        for (int e = t; e < items; e += NT) {
+            const int i = e / WY, r = e - i * WY;
+            const int w = win[i];
+            if (r >= ((w >> 8) & 255)) continue;
+            const int iy = (w & 255) + r, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
+            const float wy = uu[i] * Ey[i * G + iy];
+            for (int c = 0; c < xlen; ++c) atomicAdd(&ktu[iy * G + xlo + c], wy * Ex[i * G + xlo + c]);
         }
         __syncthreads();
     };
@@ -137,54 +140,31 @@ __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter
     while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
         if (!have_ktu) ktu_pass(u);
         have_ktu = 0;
-        // v = b / (K^T u + eps)
+        // v = b / (K^T u + eps); zero the K v accumulators
         int bad = 0;
-        for (int j = t; j < C::GG; j += NT) {
+        for (int j = t; j < GG; j += NT) {
             const float val = b[j] / (ktu[j] + M_EPS);
             vn[j] = val;
             bad |= !isfinite(val);
         }
+        for (int i = t; i < n; i += NT) un[i] = 0.f;
         __syncthreads();
-        // u = a / (K v + eps): per point, sum_iy Ey[iy] * (sum_jx Ex[jx] * v[iy][jx])
-        for (int c0 = 0; c0 < n; c0 += 64) {
-            const int i = c0 + lane;
-            float kv = 0.f;
-            if (i < n) {
-                float ex[G];
-#pragma unroll
-                for (int q = 0; q < G; q += 4) {
-                    const float4 e4 = *reinterpret_cast<const float4*>(&Ex[i * G + q]);
-                    ex[q] = e4.x; ex[q + 1] = e4.y; ex[q + 2] = e4.z; ex[q + 3] = e4.w;
-                }
-                for (int grp = wv; grp < C::NG; grp += NWAVE) {
-#pragma unroll
-                    for (int r = 0; r < C::R; ++r) {
-                        const int iy = grp * C::R + r;
-                        const float* vr = &vn[iy * G];
-                        float tr = 0.f;
-#pragma unroll
-                        for (int q = 0; q < G; q += 4) {
-                            const float4 v4 = *reinterpret_cast<const float4*>(&vr[q]);
-                            tr = fmaf(ex[q], v4.x, tr);
-                            tr = fmaf(ex[q + 1], v4.y, tr);
-                            tr = fmaf(ex[q + 2], v4.z, tr);
-                            tr = fmaf(ex[q + 3], v4.w, tr);
-                        }
-                        kv = fmaf(Ey[i * G + iy], tr, kv);
-                    }
-                }
-            }
-            kvred[wv * 64 + lane] = kv;
-            __syncthreads();
-            if (t < 64 && c0 + t < n) {
-                float s = 0.f;
-#pragma unroll
-                for (int w2 = 0; w2 < NWAVE; ++w2) s += kvred[w2 * 64 + t];
-                const float val = a / (s + M_EPS);
-                un[c0 + t] = val;
-                bad |= !isfinite(val);
-            }
-            __syncthreads();
+        // K v: per (point, window row) Ey[iy] * sum_jx Ex[jx] v[iy][jx]
+        for (int e = t; e < items; e += NT) {
+            const int i = e / WY, r = e - i * WY;
+            const int w = win[i];
+            if (r >= ((w >> 8) & 255)) continue;
+            const int iy = (w & 255) + r, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
+            float sacc = 0.f;
+            for (int c = 0; c < xlen; ++c) sacc = fmaf(Ex[i * G + xlo + c], vn[iy * G + xlo + c], sacc);
+            atomicAdd(&un[i], Ey[i * G + iy] * sacc);
+        }
+        __syncthreads();
+        // u = a / (K v + eps)
+        for (int i = t; i < n; i += NT) {
+            const float val = a / (un[i] + M_EPS);
+            un[i] = val;
+            bad |= !isfinite(val);
         }
         bad = block_or(bad, reinterpret_cast<int*>(misc));
         if (bad) { rolled = 1; break; }                       // keep (u, v): rollback, :111-115
@@ -193,7 +173,7 @@ __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter
             ktu_pass(u);
             have_ktu = 1;
             float e = 0.f;
-            for (int j = t; j < C::GG; j += NT) {
+            for (int j = t; j < GG; j += NT) {
                 const float d = b[j] - ktu[j] * v[j];
                 e = fmaf(d, d, e);
             }
@@ -203,12 +183,41 @@ __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter
         ++it;
     }
     // leave the final v in v0 and u in u0
-    if (v != v0) { for (int j = t; j < C::GG; j += NT) v0[j] = v[j]; }
+    if (v != v0) { for (int j = t; j < GG; j += NT) v0[j] = v[j]; }
     if (u != u0) { for (int i = t; i < n; i += NT) u0[i] = u[i]; }
     __syncthreads();
     *iters_out = rolled ? it : it - 1;
     *rolled_out = rolled;
     *err_last_out = err_last;
+    misc[1] = __int_as_float(WY);                            // for the wd pass
+}
+
+// Wasserstein distance sum(C * P) over the windows (dm_loss.py:77; reported, unused by training)
+template <int G, typename FP, typename IP>
+__device__ float transport_cost(int n, int size, int norm, const float* pts, FP Ey, FP Ex, FP u, IP win,
+                                const float* v, int WY, float* misc)
+{
+    float w = 0.f;
+    for (int e = threadIdx.x; e < n * WY; e += NT) {
+        const int i = e / WY, r = e - i * WY;
+        const int wi = win[i];
+        if (r >= ((wi >> 8) & 255)) continue;
+        const int iy = (wi & 255) + r, xlo = (wi >> 16) & 255, xlen = (wi >> 24) & 255;
+        const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
+        const float c = cood(iy, size, norm);
+        const float yd = (-2.0f * (y * c) + y * y) + c * c;
+        float t1 = 0.f, t2 = 0.f;
+        for (int k = 0; k < xlen; ++k) {
+            const int jx = xlo + k;
+            const float cx = cood(jx, size, norm);
+            const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
+            const float kv = Ex[i * G + jx] * v[iy * G + jx];
+            t1 += kv;
+            t2 = fmaf(kv, xd, t2);
+        }
+        w += u[i] * Ey[i * G + iy] * (yd * t1 + t2);
+    }
+    return block_sum(w, misc);
 }
 
 template <int G>
@@ -223,9 +232,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     float* v0 = bb + GG;
     float* v1 = v0 + GG;
     float* ktu = v1 + GG;
-    float* red = ktu + GG;
-    float* kvred = red + C::SL * GG;
-    float* misc = kvred + NWAVE * 64;
+    float* misc = ktu + GG;
     float* fac = misc + 64;     // LDS factors (if they fit)
 
     const int p0 = P.offsets[b], n = P.offsets[b + 1] - p0;
@@ -301,16 +308,17 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         // 4. Sinkhorn OT (dm_loss.py:49-77)
         if (n > 0) {
             const float* pts = P.points + 2 * (size_t)p0;
-            if (n <= P.lds_cap) {
-                float* Ey = fac; float* Ex = Ey + n * G; float* u0 = Ex + n * G; float* u1 = u0 + n;
+            float* base = n <= P.lds_cap ? fac : P.ws_factors + (size_t)C::PER_POINT * p0;
+            float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
+            int* win = reinterpret_cast<int*>(u1 + n);
+            if (n <= P.lds_cap)
                 sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0, u1,
-                                 bb, v0, v1, ktu, red, kvred, misc, &iters, &rolled, &err_last);
-            } else {
-                float* base = P.ws_factors + (size_t)C::PER_POINT * p0;
-                float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
+                                 win, bb, v0, v1, ktu, misc, &iters, &rolled, &err_last);
+            else
                 sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0, u1,
-                                 bb, v0, v1, ktu, red, kvred, misc, &iters, &rolled, &err_last);
-            }
+                                 win, bb, v0, v1, ktu, misc, &iters, &rolled, &err_last);
+            const int WY = __float_as_int(misc[1]);
+            __syncthreads();
             // beta = reg * log(v + eps); gradient (dm_loss.py:65-74)
             float sb = 0.f;
             for (int j = t; j < GG; j += NT) {
@@ -329,31 +337,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                 v1[j] = og;
             }
             ot_b = block_sum(ol, misc);
-            // Wasserstein distance sum(C * P) (dm_loss.py:77; reported, unused by training)
-            const bool in_lds = n <= P.lds_cap;
-            const float* Ey = in_lds ? fac : P.ws_factors + (size_t)C::PER_POINT * p0;
-            const float* Ex = Ey + (size_t)n * G;
-            const float* uu = Ex + (size_t)n * G;
-            float w = 0.f;
-            for (int i = t; i < n; i += NT) {
-                const float x = pcoord(pts[2 * i], S, P.norm_cood), y = pcoord(pts[2 * i + 1], S, P.norm_cood);
-                float acc = 0.f;
-                for (int iy = 0; iy < G; ++iy) {
-                    const float c = cood(iy, S, P.norm_cood);
-                    const float yd = (-2.0f * (y * c) + y * y) + c * c;
-                    float t1 = 0.f, t2 = 0.f;
-                    for (int jx = 0; jx < G; ++jx) {
-                        const float cx = cood(jx, S, P.norm_cood);
-                        const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
-                        const float kv = Ex[(size_t)i * G + jx] * v0[iy * G + jx];
-                        t1 = fmaf(kv, 1.0f, t1);
-                        t2 = fmaf(kv, xd, t2);
-                    }
-                    acc += Ey[(size_t)i * G + iy] * (yd * t1 + t2);
-                }
-                w += uu[i] * acc;
-            }
-            wd_b = block_sum(w, misc);
+            wd_b = transport_cost<G>(n, S, P.norm_cood, pts, Ey, Ex, u0, win, v0, WY, misc);
         } else {
             for (int j = t; j < GG; j += NT) v1[j] = 0.f;
             __syncthreads();
@@ -429,7 +413,7 @@ template <int G> int launch(const Params& P0, hipStream_t st)
 extern "C" size_t ebc_dace_workspace_bytes(int B, int total_points, int size, int reduction)
 {
     const int g = size / reduction;
-    return sizeof(float) * ((size_t)(2 * g + 2) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
+    return sizeof(float) * ((size_t)(2 * g + 3) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
 }
 
 extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,

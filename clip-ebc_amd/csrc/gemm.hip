@@ -13,6 +13,8 @@
 // ds_read_b128 fragment reads are bank-conflict free; XCD-aware bijective tile remap.
 // The MFMA is issued "swapped" (weights as the A operand) so each lane ends with 4 consecutive
 // output columns of one row: vector epilogue loads/stores.
+#include <type_traits>
+
 #include "ebc_common.h"
 #include "mfma.h"
 
@@ -32,10 +34,23 @@ struct GemmArgs {
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-__device__ __forceinline__ float quick_gelu(float a) { return a / (1.0f + expf(-1.702f * a)); }
+// QuickGELU x*sigmoid(1.702x) (blocks.py:17-19) with the hardware exp2 / reciprocal (1-ulp each):
+// the IEEE expf + division forms cost ~25 VALU per element in the epilogue.
+__device__ __forceinline__ float sigmoid1702(float a) {
+    const float e = __builtin_amdgcn_exp2f(-1.702f * 1.4426950408889634f * a);
+    return __builtin_amdgcn_rcpf(1.0f + e);
+}
+__device__ __forceinline__ float quick_gelu(float a) { return a * sigmoid1702(a); }
 __device__ __forceinline__ float quick_gelu_grad(float a) {
-    const float s = 1.0f / (1.0f + expf(-1.702f * a));
+    const float s = sigmoid1702(a);
     return s + 1.702f * a * s * (1.0f - s);
+}
+
+template <int I, int N, class F> __device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
 }
 
 template <class TO> __device__ __forceinline__ void store4(TO* p, const float* v);
@@ -61,22 +76,71 @@ template <> __device__ __forceinline__ void load4<float>(const float* p, float* 
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
 }
 
-template <class E, class TO, int EPI, int BM, int BN>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs g)
+// 8 consecutive elements <-> float[8] (16 B for 16-bit types, 32 B for f32)
+template <class TO> __device__ __forceinline__ void store8(TO* p, const float* v) {
+    store4<TO>(p, v);
+    store4<TO>(p + 4, v + 4);
+}
+template <> __device__ __forceinline__ void store8<_Float16>(_Float16* p, const float* v) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    h8 r = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3],
+            (_Float16)v[4], (_Float16)v[5], (_Float16)v[6], (_Float16)v[7]};
+    *reinterpret_cast<h8*>(p) = r;
+}
+template <> __device__ __forceinline__ void store8<__bf16>(__bf16* p, const float* v) {
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    b8 r = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3], (__bf16)v[4], (__bf16)v[5], (__bf16)v[6], (__bf16)v[7]};
+    *reinterpret_cast<b8*>(p) = r;
+}
+template <class T> __device__ __forceinline__ void load8f(const T* p, float* v) {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const t8 x = *reinterpret_cast<const t8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)x[i];
+}
+template <> __device__ __forceinline__ void load8f<float>(const float* p, float* v) {
+    load4<float>(p, v);
+    load4<float>(p + 4, v + 4);
+}
+
+// The LDS-staged epilogue is used when the f32 output tile fits the LDS the kernel already owns
+// (or at most 160 KiB).
+template <int BM, int BN, int S> constexpr bool lds_epilogue() {
+    return (size_t)BM * (BN + 4) * 4 <= 160 * 1024;
+}
+template <int BM, int BN, int S> constexpr int gemm_lds_bytes() {
+    const int stage = S * (BM + BN) * 128;
+    const int ep = lds_epilogue<BM, BN, S>() ? BM * (BN + 4) * 4 : 0;
+    return stage > ep ? stage : ep;
+}
+
+// s_waitcnt vmcnt(n * PER) with an immediate: n is wave-uniform and in [0, MAXN]
+template <int PER, int MAXN>
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    if constexpr (MAXN >= 3) { if (n >= 3) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * PER) : "memory"); return; } }
+    if constexpr (MAXN >= 2) { if (n == 2) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER) : "memory"); return; } }
+    if constexpr (MAXN >= 1) { if (n == 1) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER) : "memory"); return; } }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
 {
+    static_assert(S >= 2 && S <= 5, "stages");
     using T = typename E::T;
+    constexpr int NW = WGM * WGN;                // waves per workgroup
     constexpr int EB = E::BYTES;
     constexpr int BK = 128 / EB;                 // elements per 128-B slab row
-    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
     constexpr int TM = WM / 16, TN = WN / 16;
     constexpr int ROWS = BM + BN;                // slab rows per stage (A rows then B rows)
     constexpr int STAGE = ROWS * 128;            // bytes
-    constexpr int NLD = ROWS / 32;               // glds wave-instructions per wave per stage
-    static_assert(ROWS % 32 == 0, "stage rows");
+    constexpr int NLD = ROWS / (8 * NW);         // glds wave-instructions per wave per stage
+    static_assert(ROWS % (8 * NW) == 0 && WM % 16 == 0 && WN % 16 == 0, "tiling");
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WGN, wn = wave % WGN;
     const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
     const int wg = xcd_remap(blockIdx.x, ntm * ntn);
     const int tm = wg / ntn, tn = wg % ntn;
@@ -119,52 +183,162 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs g)
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    stage(0, 0);
-    __syncthreads();
+    // S-deep LDS ring + register double-buffered fragments.  Tiles kt+1 .. kt+S-1 are in flight
+    // while tile kt is consumed; the wait is a counted vmcnt (LDS-DMA loads count on it) and the
+    // barrier a raw s_barrier, so no vmcnt(0) drain happens in the K loop (cdna_hip_programming.md
+    // §5 "Pipelining across barriers").  The next k32 step's ds_reads are issued before the current
+    // step's MFMAs; at a tile boundary the wait+barrier sit before the last step's MFMAs so the
+    // next tile's first fragments load underneath them.
+    constexpr int KS = BK / 32;                   // k32 steps per tile
+    static_assert(KS == 2 || S % 2 == 0, "register-set alternation");
     const int fr = lane & 15, fg = lane >> 4;
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
-        const char* sb = smem + (kt & 1) * STAGE;
+    // Fragment addressing is lane-constant: every fragment row is 16-aligned + fr, so the XOR
+    // swizzle term is (fr >> 1) & 7 for all of them.  Per lane one VGPR offset per (k32 step,
+    // 16-B half); the wave's row block, the sub-tile and the stage buffer are immediates.
+    const int xs = (fr >> 1) & 7;
+    int loff[KS][EB == 2 ? 1 : 2];
 #pragma unroll
-        for (int kk = 0; kk < BK / 32; ++kk) {
-            typename E::Frag af[TM], bf[TN];
-            // element offset of this lane's 8 elements within the 128-B row: kk*32 + 8*fg
-            const int e = kk * 32 + 8 * fg;
-            const int ch = (e * EB) >> 4;             // first 16-B chunk
+    for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-            for (int a = 0; a < TM; ++a) {
-                const int row = wm * WM + a * 16 + fr;
-                const char* rp = sb + row * 128;
-                if constexpr (EB == 2) {
-                    af[a] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + ((ch ^ swz(row)) << 4)));
-                } else {
-                    const float4 x0 = *reinterpret_cast<const float4*>(rp + ((ch ^ swz(row)) << 4));
-                    const float4 x1 = *reinterpret_cast<const float4*>(rp + (((ch + 1) ^ swz(row)) << 4));
-                    af[a] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                const int row = BM + wn * WN + b * 16 + fr;
-                const char* rp = sb + row * 128;
-                if constexpr (EB == 2) {
-                    bf[b] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + ((ch ^ swz(row)) << 4)));
-                } else {
-                    const float4 x0 = *reinterpret_cast<const float4*>(rp + ((ch ^ swz(row)) << 4));
-                    const float4 x1 = *reinterpret_cast<const float4*>(rp + (((ch + 1) ^ swz(row)) << 4));
-                    bf[b] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-                }
-            }
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b) acc[a][b] = mma(bf[b], af[a], acc[a][b]);   // swapped: C^T tile
+        for (int c = 0; c < (EB == 2 ? 1 : 2); ++c) {
+            const int ch = ((kk * 32 + 8 * fg) * EB >> 4) + c;
+            loff[kk][c] = fr * 128 + ((ch ^ xs) << 4);
         }
-        __syncthreads();
+    const char* abase = smem + wm * WM * 128;
+    const char* bbase = smem + (BM + wn * WN) * 128;
+    auto load_frags = [&](auto bufc, int kk, typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
+        constexpr int buf = decltype(bufc)::value;
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+            const char* rp = abase + buf * STAGE + a * 2048;
+            if constexpr (EB == 2) {
+                af[a] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
+            } else {
+                const float4 x0 = *reinterpret_cast<const float4*>(rp + loff[kk][0]);
+                const float4 x1 = *reinterpret_cast<const float4*>(rp + loff[kk][EB == 2 ? 0 : 1]);
+                af[a] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const char* rp = bbase + buf * STAGE + b * 2048;
+            if constexpr (EB == 2) {
+                bf[b] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
+            } else {
+                const float4 x0 = *reinterpret_cast<const float4*>(rp + loff[kk][0]);
+                const float4 x1 = *reinterpret_cast<const float4*>(rp + loff[kk][EB == 2 ? 0 : 1]);
+                bf[b] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            }
+        }
+    };
+    auto sync_tile = [&](int next_kt) {
+        // tile next_kt landed (count the later tiles still in flight), every wave done reading the
+        // buffer that the refill below overwrites
+        const int later = (nk - 1 - next_kt) < (S - 2) ? (nk - 1 - next_kt) : (S - 2);
+        wait_vmcnt<NLD, S - 2>(later);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nk) stage(s, s);
+    sync_tile(0);
+    if (S - 1 < nk) stage(S - 1, S - 1);
+    typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
+    load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
+    auto mma_all = [&](typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) acc[a][b] = mma(bf[b], af[a], acc[a][b]);   // swapped: C^T tile
+    };
+    // step body: prefetch the fragments of the step after (kt, kk) into (an, bn), then MMA (ac, bc);
+    // the K loop is unrolled by S so the stage buffer of every fragment load is a constant.
+    auto step = [&](auto bufc, int kt, int kk, typename E::Frag (&ac)[TM], typename E::Frag (&bc)[TN],
+                    typename E::Frag (&an)[TM], typename E::Frag (&bn)[TN]) {
+        constexpr int buf = decltype(bufc)::value;
+        if (kk + 1 < KS) {
+            load_frags(bufc, kk + 1, an, bn);
+        } else if (kt + 1 < nk) {
+            sync_tile(kt + 1);
+            if (kt + S < nk) stage(buf, kt + S);
+            load_frags(std::integral_constant<int, (buf + 1) % S>{}, 0, an, bn);
+        }
+        mma_all(ac, bc);
+    };
+    for (int kt0 = 0; kt0 < nk; kt0 += S) {
+        static_for<0, S>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const int kt = kt0 + s;
+            if (kt < nk) {
+                if constexpr (KS == 2) {
+                    step(sc, kt, 0, a0, b0, a1, b1);
+                    step(sc, kt, 1, a1, b1, a0, b0);
+                } else if constexpr ((s & 1) == 0) {
+                    step(sc, kt, 0, a0, b0, a1, b1);
+                } else {
+                    step(sc, kt, 0, a1, b1, a0, b0);
+                }
+            }
+        });
     }
 
     // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i]
     TO* C = reinterpret_cast<TO*>(g.C);
+    if constexpr (lds_epilogue<BM, BN, S>()) {
+        // Stage the f32 tile through LDS (row pitch BN+4 floats: conflict-free b128 writes), then
+        // every thread finishes 8 consecutive columns of a row: coalesced 16-B loads of resid/aux
+        // and 16-B (or 2x16-B) stores, 4-8x fewer store instructions than the fragment layout.
+        constexpr int EPL = BN + 4;
+        constexpr int NT = 64 * NW;
+        float* ep = reinterpret_cast<float*>(smem);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                *reinterpret_cast<float4*>(ep + (wm * WM + a * 16 + fr) * EPL + wn * WN + b * 16 + 4 * fg) =
+                    make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+        __syncthreads();
+        constexpr int C8 = BN / 8;
+#pragma unroll 2
+        for (int c = tid; c < BM * C8; c += NT) {
+            const int r = c / C8, col = (c % C8) * 8;
+            const int m = m0 + r;
+            if (m >= g.M) continue;
+            const int n = n0 + col;
+            const size_t off = (size_t)m * g.N + n;
+            const float4 x0 = *reinterpret_cast<const float4*>(ep + r * EPL + col);
+            const float4 x1 = *reinterpret_cast<const float4*>(ep + r * EPL + col + 4);
+            float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            if (g.bias) {
+                const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
+                const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
+                v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+                v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+            }
+            if constexpr (EPI == EPI_GELU) {
+                if (g.aux) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = quick_gelu(v[i]);
+            } else if constexpr (EPI == EPI_GELU_BWD) {
+                float pa[8];
+                load8f<T>(reinterpret_cast<const T*>(g.aux) + off, pa);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] *= quick_gelu_grad(pa[i]);
+            } else if constexpr (EPI == EPI_RESID) {
+                float rr[8];
+                load8f<float>(g.resid + off, rr);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] += rr[i];
+            }
+            store8<TO>(C + off, v);
+        }
+        return;
+    }
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
         const int m = m0 + wm * WM + a * 16 + fr;
@@ -198,30 +372,53 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs g)
     }
 }
 
-template <class E, class TO, int EPI, int BM, int BN>
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2>
 int launch_gemm(const GemmArgs& g, hipStream_t st)
 {
-    constexpr int LDS = 2 * (BM + BN) * 128;
+    constexpr int LDS = gemm_lds_bytes<BM, BN, S>();
+    static_assert(LDS <= 160 * 1024, "LDS");
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN>,
+        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
             return EBC_E_LAUNCH;
         attr = true;
     }
+    if (g.N % BN) return EBC_E_UNSUPPORTED;
     const int nwg = ((g.M + BM - 1) / BM) * (g.N / BN);
-    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN>), dim3(nwg), dim3(256), LDS, st, g);
+    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
+}
+
+// Tile configuration: 0 = heuristic; EBC_GEMM_CFG=<1..7> forces one (tuning runs).
+//   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   6: 256x128/8w
+//   7: 256x256/8w   (all 2-stage LDS-DMA rings; 128-B K slabs)
+int forced_cfg() {
+    static int cfg = -1;
+    if (cfg < 0) {
+        const char* e = getenv("EBC_GEMM_CFG");
+        cfg = e ? atoi(e) : 0;
+    }
+    return cfg;
 }
 
 template <class E, class TO, int EPI>
 int dispatch_tile(const GemmArgs& g, hipStream_t st)
 {
-    // enough workgroups to cover the 256 CUs: 128x128 when that gives >= 256 tiles, else 128x64
-    const int t128 = ((g.M + 127) / 128) * (g.N / 128);
-    if (g.N % 128 == 0 && t128 >= 256) return launch_gemm<E, TO, EPI, 128, 128>(g, st);
-    if (g.N % 64 == 0) return launch_gemm<E, TO, EPI, 128, 64>(g, st);
+    int cfg = forced_cfg();
+    const int bns[8] = {0, 128, 64, 192, 192, 96, 128, 256};
+    if (cfg > 0 && g.N % bns[cfg] != 0) cfg = 0;
+    if (cfg == 0) cfg = 2;
+    switch (cfg) {
+        case 1: return launch_gemm<E, TO, EPI, 128, 128, 2>(g, st);
+        case 2: return launch_gemm<E, TO, EPI, 128, 64, 2>(g, st);
+        case 3: return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2>(g, st);
+        case 4: return launch_gemm<E, TO, EPI, 192, 192, 2, 4, 2>(g, st);
+        case 5: return launch_gemm<E, TO, EPI, 128, 96, 2>(g, st);
+        case 6: return launch_gemm<E, TO, EPI, 256, 128, 2, 4, 2>(g, st);
+        case 7: return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2>(g, st);
+    }
     return EBC_E_UNSUPPORTED;
 }
 
