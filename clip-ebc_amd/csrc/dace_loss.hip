@@ -12,13 +12,17 @@
 //    (dm_loss.py:53-59), so K = exp(C/-reg) = Ey_i[iy] * Ex_i[jx] with Ey = exp(yd/-reg),
 //    Ex = exp(xd/-reg).  A crop's kernel matrix shrinks from n*g^2 to 2*n*g floats, which fits
 //    the 160 KiB LDS for n <= ~470 (g = 28) and streams from L2 above that.
+//  * K^T u = (u*Ey)^T Ex is a dense [G x n] x [n x G] product, run as 4x4 register blocks over
+//    b128 LDS reads with the points split across thread groups (partials summed by the v pass).
 //  * exp(C/-reg) underflows to exactly 0 beyond ~32 px (reg = 10), so each point's factors are
-//    nonzero on a <= 9-row x 9-column window: K^T u and K v run over those windows only
-//    (~10x fewer FMAs at g = 28, ~40x at g = 56), accumulated with LDS float atomics.
+//    nonzero on a <= 9-row x 9-column window: K v runs over those windows only, 8 lanes per point.
 //  * The reference's control flow is kept exactly: err every eval_freq iterations
 //    (bregman_pytorch.py:117-126), stop when err <= stopThr or it > maxIter, NaN/Inf rollback
 //    to the previous (u, v) and break (:111-115), the 1e-16 epsilons, denormals kept (the build
 //    never flushes f32 denormals).  The err pass's K^T u is reused by the next iteration.
+#include <cstdio>
+#include <cstdlib>
+
 #include "ebc_common.h"
 
 using namespace ebc;
@@ -32,10 +36,15 @@ constexpr float EPS = 1e-8f;             // dm_loss.py:7
 
 template <int G> struct Cfg {
     static constexpr int GG = G * G;
-    // fixed LDS (floats): pd, td, b, v0, v1, ktu, misc[64]
-    static constexpr int FIXED = 6 * GG + 64;
+    // K^T u: 4x4 cell blocks, the points split over KSPLIT thread groups whose partial sums live
+    // in LDS (KSPLIT x GG) and are summed by the consumer (no atomics: LDS float atomics run at
+    // ~3 cycles per lane).
+    static constexpr int NB = (G / 4) * (G / 4);
+    static constexpr int KSPLIT = NT / NB;
+    // fixed LDS (floats): pd, td, b, v0, v1, partial[KSPLIT][GG], misc[64]
+    static constexpr int FIXED = 5 * GG + KSPLIT * GG + 64;
     static constexpr size_t FIXED_BYTES = (size_t)FIXED * 4;
-    static constexpr int PER_POINT = 2 * G + 3;          // Ey, Ex, u0, u1, window
+    static constexpr int PER_POINT = 2 * G + 4;          // Ey, Ex (16-B aligned rows), u0, u1, window, pad
 };
 
 struct Params {
@@ -49,6 +58,7 @@ struct Params {
     float* grad_class; float* grad_density; float* crop_stats; float* beta_out; int* status;
     float* ws_factors;     // global factor storage for crops that do not fit LDS
     int lds_cap;           // max points kept in LDS
+    unsigned long long* prof;   // diagnostics (EBC_DACE_PROF=1): per crop 16 counters, else null
 };
 
 // ---------------------------------------------------------------------------------------
@@ -80,12 +90,26 @@ __device__ __forceinline__ int block_max(int v, int* scratch) {
     return r;
 }
 
+// sum over aligned groups of 8 lanes with DPP moves (no LDS round trip): quad xor-1, quad xor-2,
+// then half-row mirror pairs quad 0 with quad 1 of each 8-lane group
+__device__ __forceinline__ float sum8_dpp(float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x141, 0xF, 0xF, true));
+    return x;
+}
+
 template <int G, typename FP, typename IP>
 __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                               const float* __restrict__ pts, FP Ey, FP Ex, FP u0, FP u1, IP win,
-                              const float* b, float* v0, float* v1, float* ktu, float* misc,
-                              int* iters_out, int* rolled_out, float* err_last_out)
+                              const float* b, float* v0, float* v1, float* part, float* misc,
+                              int* iters_out, int* rolled_out, float* err_last_out, unsigned long long* pr)
 {
+    // diagnostics: pr[0..3] += shader cycles in K^T u / v / K v / err phases (thread 0's view)
+    unsigned long long tk = 0;
+    auto tick = [&](int k) {
+        if (pr && threadIdx.x == 0) { const unsigned long long c = clock64(); if (k >= 0) pr[k] += c - tk; tk = c; }
+    };
     constexpr int GG = G * G;
     const int t = threadIdx.x;
     const float a = 1.0f / (float)n;                         // target_prob = ones/n
@@ -115,70 +139,124 @@ __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter
         wy_max = max(wy_max, ylen);
     }
     const int WY = block_max(wy_max, reinterpret_cast<int*>(misc));
-    const int items = n * WY;
 
     FP u = u0; FP un = u1;
     float* v = v0; float* vn = v1;
     int have_ktu = 0, it = 1, rolled = 0;
     float err = 1.0f, err_last = -1.0f;
+    int* flag = reinterpret_cast<int*>(misc) + 16;            // NaN/Inf flags per iteration parity (misc[0..7]: block_sum scratch)
+    if (t < 2) flag[t] = 0;
+    __syncthreads();
 
-    // K^T u into ktu[GG]: one item = one (point, window row)
+    // K^T u partials: thread -> (4x4 block, point group); part[kg][GG] += (u_i Ey_i[iy]) Ex_i[jx]
+    using C = Cfg<G>;
+    constexpr int GB = G / 4;
+    const int kb = t % C::NB, kg = t / C::NB;
+    const int by = (kb / GB) * 4, bx = (kb % GB) * 4;
     auto ktu_pass = [&](FP uu) {
-        for (int j = t; j < GG; j += NT) ktu[j] = 0.f;
-        __syncthreads();
-        for (int e = t; e < items; e += NT) {
-            const int i = e / WY, r = e - i * WY;
-            const int w = win[i];
-            if (r >= ((w >> 8) & 255)) continue;
-            const int iy = (w & 255) + r, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
-            const float wy = uu[i] * Ey[i * G + iy];
-            for (int c = 0; c < xlen; ++c) atomicAdd(&ktu[iy * G + xlo + c], wy * Ex[i * G + xlo + c]);
+        if (kg < C::KSPLIT) {
+            float4 acc[4] = {};
+#pragma unroll 4
+            for (int i = kg; i < n; i += C::KSPLIT) {
+                const float ui = uu[i];
+                const float4 ey = *reinterpret_cast<const float4*>(&Ey[i * G + by]);
+                const float4 ex = *reinterpret_cast<const float4*>(&Ex[i * G + bx]);
+                const float wy[4] = {ui * ey.x, ui * ey.y, ui * ey.z, ui * ey.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    acc[r].x = fmaf(wy[r], ex.x, acc[r].x);
+                    acc[r].y = fmaf(wy[r], ex.y, acc[r].y);
+                    acc[r].z = fmaf(wy[r], ex.z, acc[r].z);
+                    acc[r].w = fmaf(wy[r], ex.w, acc[r].w);
+                }
+            }
+            float* pp = part + kg * GG + by * G + bx;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) *reinterpret_cast<float4*>(pp + r * G) = acc[r];
         }
         __syncthreads();
     };
+    auto ktu_at = [&](int j) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int k = 0; k < C::KSPLIT; ++k) sacc += part[k * GG + j];
+        return sacc;
+    };
+    // K v: 8 lanes per point, lane q takes window rows q, q+8, ...; the 8 row sums meet by shuffles
+    constexpr int WC = 10;
+    const int q = t & 7;
 
+    tick(-1);
     while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
         if (!have_ktu) ktu_pass(u);
         have_ktu = 0;
-        // v = b / (K^T u + eps); zero the K v accumulators
+        tick(0);
+        int* fl = flag + (it & 1);
+        // v = b / (K^T u + eps)
         int bad = 0;
         for (int j = t; j < GG; j += NT) {
-            const float val = b[j] / (ktu[j] + M_EPS);
+            const float val = b[j] / (ktu_at(j) + M_EPS);
             vn[j] = val;
             bad |= !isfinite(val);
         }
-        for (int i = t; i < n; i += NT) un[i] = 0.f;
+        if (bad) *fl = 1;
         __syncthreads();
-        // K v: per (point, window row) Ey[iy] * sum_jx Ex[jx] v[iy][jx]
-        for (int e = t; e < items; e += NT) {
-            const int i = e / WY, r = e - i * WY;
-            const int w = win[i];
-            if (r >= ((w >> 8) & 255)) continue;
-            const int iy = (w & 255) + r, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
-            float sacc = 0.f;
-            for (int c = 0; c < xlen; ++c) sacc = fmaf(Ex[i * G + xlo + c], vn[iy * G + xlo + c], sacc);
-            atomicAdd(&un[i], Ey[i * G + iy] * sacc);
+        if (t == 0) flag[(it + 1) & 1] = 0;                   // nobody reads it until after the next barrier
+        tick(1);
+        // u = a / (K v + eps); two points per 8-lane group per round so their LDS latencies overlap
+        for (int i0 = 0; i0 < n; i0 += NT / 4) {
+            float kv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = i0 + h * (NT / 8) + (t >> 3);
+                const bool live = i < n;
+                const int w = live ? win[i] : 0;
+                const int ylo = w & 255, ylen = (w >> 8) & 255, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
+                float acc = 0.f;
+                if (live) {
+                    const FP ex = Ex + i * G + xlo;
+                    for (int c0 = 0; c0 < xlen; c0 += WC) {
+                        float xv[WC];
+#pragma unroll
+                        for (int c = 0; c < WC; ++c) xv[c] = c0 + c < xlen ? ex[min(c0 + c, xlen - 1)] : 0.f;
+                        for (int r = q; r < ylen; r += 8) {
+                            const float* vr = vn + (ylo + r) * G + xlo;
+                            float sacc = 0.f;
+#pragma unroll
+                            for (int c = 0; c < WC; ++c) sacc = fmaf(xv[c], vr[min(c0 + c, xlen - 1)], sacc);
+                            acc = fmaf(Ey[i * G + ylo + r], sacc, acc);
+                        }
+                    }
+                }
+                kv[h] = acc;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) kv[h] = sum8_dpp(kv[h]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = i0 + h * (NT / 8) + (t >> 3);
+                if (i < n && q == 0) {
+                    const float val = a / (kv[h] + M_EPS);
+                    un[i] = val;
+                    if (!isfinite(val)) *fl = 1;
+                }
+            }
         }
         __syncthreads();
-        // u = a / (K v + eps)
-        for (int i = t; i < n; i += NT) {
-            const float val = a / (un[i] + M_EPS);
-            un[i] = val;
-            bad |= !isfinite(val);
-        }
-        bad = block_or(bad, reinterpret_cast<int*>(misc));
-        if (bad) { rolled = 1; break; }                       // keep (u, v): rollback, :111-115
+        tick(2);
+        if (*fl) { rolled = 1; break; }                       // keep (u, v): rollback, :111-115
         { FP tu = u; u = un; un = tu; float* tv = v; v = vn; vn = tv; }
         if (it % eval_freq == 0) {                            // :117-126
             ktu_pass(u);
             have_ktu = 1;
             float e = 0.f;
             for (int j = t; j < GG; j += NT) {
-                const float d = b[j] - ktu[j] * v[j];
+                const float d = b[j] - ktu_at(j) * v[j];
                 e = fmaf(d, d, e);
             }
             err = block_sum(e, misc);
             err_last = err;
+            tick(3);
         }
         ++it;
     }
@@ -231,11 +309,12 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     float* bb = td + GG;        // normed pred density (Sinkhorn b)
     float* v0 = bb + GG;
     float* v1 = v0 + GG;
-    float* ktu = v1 + GG;
-    float* misc = ktu + GG;
+    float* part = v1 + GG;      // K^T u partials [KSPLIT][GG]
+    float* misc = part + C::KSPLIT * GG;
     float* fac = misc + 64;     // LDS factors (if they fit)
 
     const int p0 = P.offsets[b], n = P.offsets[b + 1] - p0;
+    if (P.prof && t == 0) { for (int k = 0; k < 16; ++k) P.prof[b * 16 + k] = 0; P.prof[b * 16 + 6] = clock64(); P.prof[b * 16 + 5] = n; }
 
     // 1. pred density, target block sums (losses/utils.py:4-9)
     for (int j = t; j < GG; j += NT) { pd[j] = P.pred_density[(size_t)b * GG + j]; td[j] = 0.f; }
@@ -308,36 +387,38 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         // 4. Sinkhorn OT (dm_loss.py:49-77)
         if (n > 0) {
             const float* pts = P.points + 2 * (size_t)p0;
-            float* base = n <= P.lds_cap ? fac : P.ws_factors + (size_t)C::PER_POINT * p0;
-            float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
-            int* win = reinterpret_cast<int*>(u1 + n);
-            if (n <= P.lds_cap)
+            // Two inlined copies so each sees one address space for the factors: LDS-resident
+            // crops get ds_* accesses (a select between LDS and global would make them flat_*).
+            auto ot = [&](float* base) {
+                float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
+                int* win = reinterpret_cast<int*>(u1 + n);
                 sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0, u1,
-                                 win, bb, v0, v1, ktu, misc, &iters, &rolled, &err_last);
-            else
-                sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0, u1,
-                                 win, bb, v0, v1, ktu, misc, &iters, &rolled, &err_last);
-            const int WY = __float_as_int(misc[1]);
-            __syncthreads();
-            // beta = reg * log(v + eps); gradient (dm_loss.py:65-74)
-            float sb = 0.f;
-            for (int j = t; j < GG; j += NT) {
-                const float be = P.reg * logf(v0[j] + M_EPS);
-                v1[j] = be;
-                sb += pd[j] * be;
-                if (P.beta_out) P.beta_out[(size_t)b * GG + j] = be;
-            }
-            sb = block_sum(sb, misc);
-            const float den = pc * pc + EPS;
-            const float g1 = pc / den, g2 = sb / den;
-            float ol = 0.f;
-            for (int j = t; j < GG; j += NT) {
-                const float og = g1 * v1[j] - g2;
-                ol += pd[j] * og;
-                v1[j] = og;
-            }
-            ot_b = block_sum(ol, misc);
-            wd_b = transport_cost<G>(n, S, P.norm_cood, pts, Ey, Ex, u0, win, v0, WY, misc);
+                                 win, bb, v0, v1, part, misc, &iters, &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr);
+                if (P.prof && t == 0) P.prof[b * 16 + 8] = clock64();
+                const int WY = __float_as_int(misc[1]);
+                __syncthreads();
+                // beta = reg * log(v + eps); gradient (dm_loss.py:65-74)
+                float sb = 0.f;
+                for (int j = t; j < GG; j += NT) {
+                    const float be = P.reg * logf(v0[j] + M_EPS);
+                    v1[j] = be;
+                    sb += pd[j] * be;
+                    if (P.beta_out) P.beta_out[(size_t)b * GG + j] = be;
+                }
+                sb = block_sum(sb, misc);
+                const float den = pc * pc + EPS;
+                const float g1 = pc / den, g2 = sb / den;
+                float ol = 0.f;
+                for (int j = t; j < GG; j += NT) {
+                    const float og = g1 * v1[j] - g2;
+                    ol += pd[j] * og;
+                    v1[j] = og;
+                }
+                ot_b = block_sum(ol, misc);
+                wd_b = transport_cost<G>(n, S, P.norm_cood, pts, Ey, Ex, u0, win, v0, WY, misc);
+            };
+            if (n <= P.lds_cap) ot(fac);
+            else ot(P.ws_factors + (size_t)C::PER_POINT * p0);
         } else {
             for (int j = t; j < GG; j += NT) v1[j] = 0.f;
             __syncthreads();
@@ -350,6 +431,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
             P.grad_density[(size_t)b * GG + j] = P.w_count * (P.w_ot * v1[j] + P.w_tv * gtv + gcount);
         }
     }
+    if (P.prof && t == 0) { P.prof[b * 16 + 7] = clock64(); P.prof[b * 16 + 4] = iters; }
     if (t == 0) {
         float* st = P.crop_stats + (size_t)b * 8;
         st[0] = ce; st[1] = tv_b; st[2] = cnt_b; st[3] = ot_b; st[4] = wd_b;
@@ -403,8 +485,22 @@ template <int G> int launch(const Params& P0, hipStream_t st)
             return EBC_E_LAUNCH;
         attr = true;
     }
+    static unsigned long long* dprof = nullptr;
+    static const bool want_prof = getenv("EBC_DACE_PROF") != nullptr;
+    if (want_prof && !dprof && P.B <= 1024) (void)hipMalloc(&dprof, 1024 * 16 * sizeof(unsigned long long));
+    if (want_prof) P.prof = dprof;
     hipLaunchKernelGGL(dace_loss_kernel<G>, dim3(P.B), dim3(NT), LDS_MAX, st, P);
     EBC_CHECK_LAUNCH();
+    if (P.prof) {   // diagnostics only: synchronous read-back and a line per crop on stderr
+        unsigned long long h[1024 * 16];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpy(h, P.prof, (size_t)P.B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+        for (int b = 0; b < P.B; ++b) {
+            const unsigned long long* q = h + b * 16;
+            fprintf(stderr, "dace_prof crop %d n %llu iters %llu total %llu ktu %llu v %llu kv %llu err %llu sinkhorn_end %llu\n", b,
+                    q[5], q[4], q[7] - q[6], q[0], q[1], q[2], q[3], q[8] ? q[8] - q[6] : 0ull);
+        }
+    }
     return EBC_OK;
 }
 
@@ -413,7 +509,7 @@ template <int G> int launch(const Params& P0, hipStream_t st)
 extern "C" size_t ebc_dace_workspace_bytes(int B, int total_points, int size, int reduction)
 {
     const int g = size / reduction;
-    return sizeof(float) * ((size_t)(2 * g + 3) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
+    return sizeof(float) * ((size_t)(2 * g + 4) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
 }
 
 extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,

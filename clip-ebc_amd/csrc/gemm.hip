@@ -168,6 +168,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         src[i] = base + c * (16 / EB);
     }
     auto stage = [&](int buf, int kt) {
+#if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 2)
+        return;                                   // experiment build: no global->LDS traffic
+#endif
         char* dst = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
@@ -231,11 +234,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             }
         }
     };
-    auto sync_tile = [&](int next_kt) {
+    auto sync_tile = [&](int next_kt, auto tailc) {
         // tile next_kt landed (count the later tiles still in flight), every wave done reading the
-        // buffer that the refill below overwrites
-        const int later = (nk - 1 - next_kt) < (S - 2) ? (nk - 1 - next_kt) : (S - 2);
-        wait_vmcnt<NLD, S - 2>(later);
+        // buffer that the refill below overwrites.  Outside the tail S-2 later tiles are in flight.
+        if constexpr (decltype(tailc)::value) {
+            const int later = (nk - 1 - next_kt) < (S - 2) ? (nk - 1 - next_kt) : (S - 2);
+            wait_vmcnt<NLD, S - 2>(later);
+        } else {
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * NLD) : "memory");
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -244,11 +251,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
         if (s < nk) stage(s, s);
-    sync_tile(0);
+    sync_tile(0, std::true_type{});
     if (S - 1 < nk) stage(S - 1, S - 1);
     typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
     load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
     auto mma_all = [&](typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
+#if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 1)
+        return;                                   // experiment build: no MFMA (fragment reads die too)
+#endif
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -256,34 +266,52 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     };
     // step body: prefetch the fragments of the step after (kt, kk) into (an, bn), then MMA (ac, bc);
     // the K loop is unrolled by S so the stage buffer of every fragment load is a constant.
-    auto step = [&](auto bufc, int kt, int kk, typename E::Frag (&ac)[TM], typename E::Frag (&bc)[TN],
+    // The main loop runs whole groups of S tiles that are followed by at least S more, so it has no
+    // bounds tests (a branch-free body keeps the accumulators in place across the back edge);
+    // the last one or two groups run the same body with the tests.
+    auto step = [&](auto bufc, auto tailc, int kt, int kk, typename E::Frag (&ac)[TM], typename E::Frag (&bc)[TN],
                     typename E::Frag (&an)[TM], typename E::Frag (&bn)[TN]) {
         constexpr int buf = decltype(bufc)::value;
+        constexpr bool tail = decltype(tailc)::value;
         if (kk + 1 < KS) {
             load_frags(bufc, kk + 1, an, bn);
-        } else if (kt + 1 < nk) {
-            sync_tile(kt + 1);
-            if (kt + S < nk) stage(buf, kt + S);
+        } else if (!tail || kt + 1 < nk) {
+            sync_tile(kt + 1, tailc);
+            if (!tail || kt + S < nk) stage(buf, kt + S);
             load_frags(std::integral_constant<int, (buf + 1) % S>{}, 0, an, bn);
         }
         mma_all(ac, bc);
+        // keep the next step's fragment reads ahead of (interleaved with) this step's MFMAs and
+        // stop the scheduler from sinking them next to their first use
+        // (all of them within the first half of the MFMAs, two per MFMA)
+        constexpr int NRD = (TM + TN) * (EB == 2 ? 1 : 2), NG = (NRD + 1) / 2;
+        static_assert(NG <= TM * TN, "read/MFMA interleave");
+        static_for<0, NG>([&](auto) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);                 // DS reads
+        });
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - NG, 0);
+        __builtin_amdgcn_sched_barrier(0);
     };
-    for (int kt0 = 0; kt0 < nk; kt0 += S) {
+    auto group = [&](int kt0, auto tailc) {
         static_for<0, S>([&](auto sc) {
             constexpr int s = decltype(sc)::value;
             const int kt = kt0 + s;
-            if (kt < nk) {
+            if (!decltype(tailc)::value || kt < nk) {
                 if constexpr (KS == 2) {
-                    step(sc, kt, 0, a0, b0, a1, b1);
-                    step(sc, kt, 1, a1, b1, a0, b0);
+                    step(sc, tailc, kt, 0, a0, b0, a1, b1);
+                    step(sc, tailc, kt, 1, a1, b1, a0, b0);
                 } else if constexpr ((s & 1) == 0) {
-                    step(sc, kt, 0, a0, b0, a1, b1);
+                    step(sc, tailc, kt, 0, a0, b0, a1, b1);
                 } else {
-                    step(sc, kt, 0, a1, b1, a0, b0);
+                    step(sc, tailc, kt, 0, a1, b1, a0, b0);
                 }
             }
         });
-    }
+    };
+    int kt0 = 0;
+    for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
+    for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
 
     // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i]
     TO* C = reinterpret_cast<TO*>(g.C);
@@ -393,7 +421,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 
 // Tile configuration: 0 = heuristic; EBC_GEMM_CFG=<1..7> forces one (tuning runs).
 //   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   6: 256x128/8w
-//   7: 256x256/8w   (all 2-stage LDS-DMA rings; 128-B K slabs)
+//   7: 256x256/8w   (2-stage LDS-DMA rings; 128-B K slabs)
+//   8: 128x64 S3   9: 128x128 S3   10: 256x128/8w S3   11: 192x128/8w S3   12: 128x64 S4   13: 128x96 S3
 int forced_cfg() {
     static int cfg = -1;
     if (cfg < 0) {
@@ -407,9 +436,12 @@ template <class E, class TO, int EPI>
 int dispatch_tile(const GemmArgs& g, hipStream_t st)
 {
     int cfg = forced_cfg();
-    const int bns[8] = {0, 128, 64, 192, 192, 96, 128, 256};
-    if (cfg > 0 && g.N % bns[cfg] != 0) cfg = 0;
+    const int bns[14] = {0, 128, 64, 192, 192, 96, 128, 256, 64, 128, 128, 128, 64, 96};
+    if (cfg > 13 || (cfg > 0 && g.N % bns[cfg] != 0)) cfg = 0;
     if (cfg == 0) cfg = 2;
+    if constexpr (E::BYTES == 4) {                  // f32 (exact parity mode): one k32 step per
+        if (cfg >= 8) cfg = 2;                      // tile, register sets need an even ring
+    }
     switch (cfg) {
         case 1: return launch_gemm<E, TO, EPI, 128, 128, 2>(g, st);
         case 2: return launch_gemm<E, TO, EPI, 128, 64, 2>(g, st);
@@ -418,6 +450,16 @@ int dispatch_tile(const GemmArgs& g, hipStream_t st)
         case 5: return launch_gemm<E, TO, EPI, 128, 96, 2>(g, st);
         case 6: return launch_gemm<E, TO, EPI, 256, 128, 2, 4, 2>(g, st);
         case 7: return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2>(g, st);
+    }
+    if constexpr (E::BYTES == 2) {
+        switch (cfg) {
+            case 8: return launch_gemm<E, TO, EPI, 128, 64, 3>(g, st);
+            case 9: return launch_gemm<E, TO, EPI, 128, 128, 3>(g, st);
+            case 10: return launch_gemm<E, TO, EPI, 256, 128, 3, 4, 2>(g, st);
+            case 11: return launch_gemm<E, TO, EPI, 192, 128, 3, 4, 2>(g, st);
+            case 12: return launch_gemm<E, TO, EPI, 128, 64, 4>(g, st);
+            case 13: return launch_gemm<E, TO, EPI, 128, 96, 3>(g, st);
+        }
     }
     return EBC_E_UNSUPPORTED;
 }

@@ -11,7 +11,7 @@ from typing import Optional
 import torch
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libebc_hip.so")
+LIB_PATH = os.environ.get("EBC_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libebc_hip.so")   # override: tuning builds
 
 EBC_F32, EBC_F16, EBC_BF16 = 0, 1, 2
 EBC_COUNT_DMCOUNT, EBC_COUNT_MAE, EBC_COUNT_MSE = 0, 1, 2

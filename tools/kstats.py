@@ -1,0 +1,50 @@
+"""Summarise a rocprofv3 rocpd database (``--kernel-trace`` output) as per-kernel stats.
+
+usage: python tools/kstats.py <results.db> [--csv out.csv] [--top N] [--per STEPS]
+
+Prints calls / total / average / share per kernel name (templated names shortened), and with
+``--per`` the per-step time of each kernel (total / STEPS).
+"""
+import argparse
+import csv
+import re
+import sqlite3
+
+
+def short(name):
+    name = re.sub(r"\(anonymous namespace\)::", "", name)
+    name = re.sub(r"void ", "", name)
+    name = re.sub(r"\(.*\)$", "", name)          # drop the argument list
+    return name[:140]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--csv")
+    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--per", type=float, default=0.0)
+    a = ap.parse_args()
+    con = sqlite3.connect(a.db)
+    rows = con.execute("select name, count(*), sum(duration), avg(duration), min(duration), max(duration) "
+                       "from kernels group by name order by sum(duration) desc").fetchall()
+    total = sum(r[2] for r in rows)
+    out = []
+    for name, n, tot, avg, mn, mx in rows:
+        out.append({"kernel": short(name), "calls": n, "total_us": tot / 1e3, "avg_us": avg / 1e3,
+                    "min_us": mn / 1e3, "max_us": mx / 1e3, "pct": 100.0 * tot / total,
+                    "per_step_us": (tot / 1e3 / a.per) if a.per else ""})
+    print(f"{'pct':>6} {'calls':>6} {'avg_us':>9} {'per_step':>9}  kernel")
+    for r in out[:a.top]:
+        ps = f"{r['per_step_us']:9.1f}" if a.per else ""
+        print(f"{r['pct']:6.2f} {r['calls']:6d} {r['avg_us']:9.2f} {ps:>9}  {r['kernel']}")
+    print(f"total kernel time {total / 1e6:.3f} ms" + (f"  per step {total / 1e3 / a.per:.1f} us" if a.per else ""))
+    if a.csv:
+        with open(a.csv, "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(out[0].keys()))
+            w.writeheader()
+            w.writerows(out)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,11 @@
+"""One loss launch per point count with EBC_DACE_PROF=1 (per-phase shader cycles on stderr)."""
+import os
+import sys
+
+os.environ["EBC_DACE_PROF"] = "1"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+from loss_probe import run  # noqa: E402
+
+for n in (20, 300):
+    print(f"--- n={n}", file=sys.stderr, flush=True)
+    run([n] * 2, reps=1)
