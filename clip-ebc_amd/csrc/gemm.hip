@@ -30,9 +30,21 @@ struct GemmArgs {
     const float* resid;     // [M,N] f32 (EPI_RESID), may alias C
     void* aux;              // [M,N] element type: GELU pre-activation (written by EPI_GELU, read by EPI_GELU_BWD)
     int M, N, K;
+    // split-K: `splits` workgroups per output tile each take `kslice` of K; the last one to finish
+    // (per-tile arrival counter `cnt`, re-armed to 0 by it) adds the others' f32 partials (`part`)
+    int splits = 1, kslice = 0;
+    float* part = nullptr;
+    int* cnt = nullptr;
 };
 
-__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+// Slab rows are ROWB bytes (one BK-deep K slice): 128 (BK = 64 for 16-bit, 32 for f32) or 64
+// (BK = 32, 16-bit: deeper rings for the 256-wide tiles).  The 16-B chunks of a row are XOR
+// swizzled on the DMA source address so the ds_read_b128 fragment reads are conflict free
+// (brute-force checked against the MI355X_MICROARCH.md §LDS lane groups).
+template <int ROWB> __device__ __forceinline__ int swz_row(int row) {
+    if constexpr (ROWB == 128) return (row >> 1) & 7;
+    else return (0x1320 >> (((row >> 2) & 3) * 4)) & 3;      // [0,2,3,1][(row >> 2) & 3]
+}
 
 // QuickGELU x*sigmoid(1.702x) (blocks.py:17-19) with the hardware exp2 / reciprocal (1-ulp each):
 // the IEEE expf + division forms cost ~25 VALU per element in the epilogue.
@@ -103,15 +115,19 @@ template <> __device__ __forceinline__ void load8f<float>(const float* p, float*
     load4<float>(p + 4, v + 4);
 }
 
-// The LDS-staged epilogue is used when the f32 output tile fits the LDS the kernel already owns
-// (or at most 160 KiB).
-template <int BM, int BN, int S> constexpr bool lds_epilogue() {
-    return (size_t)BM * (BN + 4) * 4 <= 160 * 1024;
+// The epilogue stages the f32 tile through LDS in passes of EPR rows: all BM rows when they fit the
+// ring's bytes (or 64 KiB), else halves, quarters, ... (never below one wave's WM rows).
+template <int BM, int BN, int S, int ROWB, int WM> constexpr int ep_rows() {
+    const int ring = S * (BM + BN) * ROWB;
+    const int cap = ring > 64 * 1024 ? ring : 64 * 1024;
+    int r = BM;
+    while (r > WM && r * (BN + 4) * 4 > cap) r /= 2;
+    return r;
 }
-template <int BM, int BN, int S> constexpr int gemm_lds_bytes() {
-    const int stage = S * (BM + BN) * 128;
-    const int ep = lds_epilogue<BM, BN, S>() ? BM * (BN + 4) * 4 : 0;
-    return stage > ep ? stage : ep;
+template <int BM, int BN, int S, int ROWB, int WM> constexpr int gemm_lds_bytes() {
+    const int ring = S * (BM + BN) * ROWB;
+    const int ep = ep_rows<BM, BN, S, ROWB, WM>() * (BN + 4) * 4;
+    return ring > ep ? ring : ep;
 }
 
 // s_waitcnt vmcnt(n * PER) with an immediate: n is wave-uniform and in [0, MAXN]
@@ -123,40 +139,44 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN>
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
 {
     static_assert(S >= 2 && S <= 5, "stages");
     using T = typename E::T;
     constexpr int NW = WGM * WGN;                // waves per workgroup
     constexpr int EB = E::BYTES;
-    constexpr int BK = 128 / EB;                 // elements per 128-B slab row
+    constexpr int BK = ROWB / EB;                // K elements per slab row
     constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
     constexpr int TM = WM / 16, TN = WN / 16;
     constexpr int ROWS = BM + BN;                // slab rows per stage (A rows then B rows)
-    constexpr int STAGE = ROWS * 128;            // bytes
-    constexpr int NLD = ROWS / (8 * NW);         // glds wave-instructions per wave per stage
-    static_assert(ROWS % (8 * NW) == 0 && WM % 16 == 0 && WN % 16 == 0, "tiling");
+    constexpr int STAGE = ROWS * ROWB;           // bytes
+    constexpr int RPI = 1024 / ROWB;             // slab rows per LDS-DMA wave-instruction (1 KiB)
+    constexpr int CPR = ROWB / 16;               // 16-B chunks per row
+    constexpr int NLD = ROWS / (RPI * NW);       // glds wave-instructions per wave per stage
+    static_assert(ROWS % (RPI * NW) == 0 && WM % 16 == 0 && WN % 16 == 0, "tiling");
+    static_assert(BK % 32 == 0, "k32 MFMA steps");
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WGN, wn = wave % WGN;
     const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
-    const int wg = xcd_remap(blockIdx.x, ntm * ntn);
-    const int tm = wg / ntn, tn = wg % ntn;
+    const int wg = xcd_remap(blockIdx.x, ntm * ntn * g.splits);
+    const int tile = wg / g.splits, split = wg - tile * g.splits;   // a tile's splits are adjacent
+    const int tm = tile / ntn, tn = tile % ntn;
     const int m0 = tm * BM, n0 = tn * BN;
 
     const T* A = reinterpret_cast<const T*>(g.A);
     const T* Bw = reinterpret_cast<const T*>(g.B);
-    const int K = g.K, nk = K / BK;
+    const int K = g.K, nk = g.kslice / BK, kbeg = split * g.kslice;
 
     // per-lane source rows for the LDS-DMA staging (fixed across k)
     const T* src[NLD];
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-        const int row = (wave * NLD + i) * 8 + (lane >> 3);
-        const int slot = lane & 7;
-        const int c = slot ^ swz(row);
+        const int row = (wave * NLD + i) * RPI + lane / CPR;
+        const int slot = lane % CPR;
+        const int c = slot ^ swz_row<ROWB>(row);
         const T* base;
         if (row < BM) {
             int gr = m0 + row;
@@ -165,7 +185,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         } else {
             base = Bw + (size_t)(n0 + row - BM) * K;
         }
-        src[i] = base + c * (16 / EB);
+        src[i] = base + kbeg + c * (16 / EB);
     }
     auto stage = [&](int buf, int kt) {
 #if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 2)
@@ -193,27 +213,30 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     // step's MFMAs; at a tile boundary the wait+barrier sit before the last step's MFMAs so the
     // next tile's first fragments load underneath them.
     constexpr int KS = BK / 32;                   // k32 steps per tile
-    static_assert(KS == 2 || S % 2 == 0, "register-set alternation");
+    // two fragment register sets (next step's reads under this step's MFMAs) unless the wave tile's
+    // accumulators leave no room (2 waves/SIMD: 256 registers per lane in all)
+    constexpr bool DB = TM * TN * 4 + 2 * (TM + TN) * (EB == 2 ? 4 : 8) <= 200;
+    static_assert(!DB || KS == 2 || S % 2 == 0, "register-set alternation");
     const int fr = lane & 15, fg = lane >> 4;
     // Fragment addressing is lane-constant: every fragment row is 16-aligned + fr, so the XOR
-    // swizzle term is (fr >> 1) & 7 for all of them.  Per lane one VGPR offset per (k32 step,
+    // swizzle term is swz_row(fr) for all of them.  Per lane one VGPR offset per (k32 step,
     // 16-B half); the wave's row block, the sub-tile and the stage buffer are immediates.
-    const int xs = (fr >> 1) & 7;
+    const int xs = swz_row<ROWB>(fr);
     int loff[KS][EB == 2 ? 1 : 2];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
         for (int c = 0; c < (EB == 2 ? 1 : 2); ++c) {
             const int ch = ((kk * 32 + 8 * fg) * EB >> 4) + c;
-            loff[kk][c] = fr * 128 + ((ch ^ xs) << 4);
+            loff[kk][c] = fr * ROWB + ((ch ^ xs) << 4);
         }
-    const char* abase = smem + wm * WM * 128;
-    const char* bbase = smem + (BM + wn * WN) * 128;
+    const char* abase = smem + wm * WM * ROWB;
+    const char* bbase = smem + (BM + wn * WN) * ROWB;
     auto load_frags = [&](auto bufc, int kk, typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
         constexpr int buf = decltype(bufc)::value;
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
-            const char* rp = abase + buf * STAGE + a * 2048;
+            const char* rp = abase + buf * STAGE + a * 16 * ROWB;
             if constexpr (EB == 2) {
                 af[a] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
             } else {
@@ -224,7 +247,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
-            const char* rp = bbase + buf * STAGE + b * 2048;
+            const char* rp = bbase + buf * STAGE + b * 16 * ROWB;
             if constexpr (EB == 2) {
                 bf[b] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
             } else {
@@ -273,12 +296,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
                     typename E::Frag (&an)[TM], typename E::Frag (&bn)[TN]) {
         constexpr int buf = decltype(bufc)::value;
         constexpr bool tail = decltype(tailc)::value;
+        if constexpr (!DB) mma_all(ac, bc);      // single fragment set: consume, then refill it
         if (kk + 1 < KS) {
             load_frags(bufc, kk + 1, an, bn);
         } else if (!tail || kt + 1 < nk) {
             sync_tile(kt + 1, tailc);
             if (!tail || kt + S < nk) stage(buf, kt + S);
             load_frags(std::integral_constant<int, (buf + 1) % S>{}, 0, an, bn);
+        }
+        if constexpr (!DB) {
+            __builtin_amdgcn_sched_barrier(0);
+            return;
         }
         mma_all(ac, bc);
         // keep the next step's fragment reads ahead of (interleaved with) this step's MFMAs and
@@ -298,7 +326,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             constexpr int s = decltype(sc)::value;
             const int kt = kt0 + s;
             if (!decltype(tailc)::value || kt < nk) {
-                if constexpr (KS == 2) {
+                if constexpr (!DB) {
+                    static_for<0, KS>([&](auto kc) { step(sc, tailc, kt, decltype(kc)::value, a0, b0, a0, b0); });
+                } else if constexpr (KS == 2) {
                     step(sc, tailc, kt, 0, a0, b0, a1, b1);
                     step(sc, tailc, kt, 1, a1, b1, a0, b0);
                 } else if constexpr ((s & 1) == 0) {
@@ -313,29 +343,71 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
     for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
 
-    // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i]
-    TO* C = reinterpret_cast<TO*>(g.C);
-    if constexpr (lds_epilogue<BM, BN, S>()) {
-        // Stage the f32 tile through LDS (row pitch BN+4 floats: conflict-free b128 writes), then
-        // every thread finishes 8 consecutive columns of a row: coalesced 16-B loads of resid/aux
-        // and 16-B (or 2x16-B) stores, 4-8x fewer store instructions than the fragment layout.
-        constexpr int EPL = BN + 4;
-        constexpr int NT = 64 * NW;
-        float* ep = reinterpret_cast<float*>(smem);
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __syncthreads();
+    if (g.splits > 1) {
+        // split-K: publish this split's f32 partial (lane-major: the reader has the same lane map,
+        // so every access is a coalesced 16-B per lane), count the arrival; the last arriver sums
+        // the others and runs the epilogue, the rest exit.  Agent-scope fences order the partial
+        // stores before the count and the count before the reads (L2s are per XCD).
+        constexpr int PT = NW * TM * TN * 64;     // f32x4 per partial tile
+        // one buffer resource over this tile's `splits` partials; aux 16 = sc1
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<f32x4*>(g.part) + (size_t)tile * g.splits * PT, 0, 0x7fffffff, 0x00020000);
+        // MI355X_MICROARCH.md cross-CU hand-off, sc1 form: sc1 (write-through) 16-B stores, every
+        // wave's vmcnt(0), a barrier, ONE agent-scope atomic add; the last adder's waves read with
+        // sc1 loads after a barrier.  No agent fences (a buffer_wbl2 per workgroup costs ~microseconds).
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
             for (int b = 0; b < TN; ++b)
-                *reinterpret_cast<float4*>(ep + (wm * WM + a * 16 + fr) * EPL + wn * WN + b * 16 + 4 * fg) =
-                    make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rs,
+                                                       ((split * PT) + ((wave * TM + a) * TN + b) * 64 + lane) * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        constexpr int C8 = BN / 8;
+        __shared__ int last;
+        if (tid == 0) last = atomicAdd(&g.cnt[tile], 1) == g.splits - 1;
+        __syncthreads();
+        if (!last) return;
+        for (int sp = 0; sp < g.splits; ++sp) {
+            if (sp == split) continue;
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, ((sp * PT) + ((wave * TM + a) * TN + b) * 64 + lane) * 16, 0, 16));
+        }
+        if (tid == 0) atomicExch(&g.cnt[tile], 0);   // re-armed for the next launch
+    }
+
+    // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i].
+    // Staged through LDS in passes of EPR rows (row pitch BN+4 floats: conflict-free b128 writes),
+    // then every thread finishes 8 consecutive columns of a row: coalesced 16-B loads of resid/aux
+    // and 16-B (or 2x16-B) stores, 4-8x fewer store instructions than the fragment layout.
+    TO* C = reinterpret_cast<TO*>(g.C);
+    constexpr int EPR = ep_rows<BM, BN, S, ROWB, WM>();
+    static_assert(EPR % WM == 0 && BM % EPR == 0, "epilogue passes");
+    constexpr int EPL = BN + 4;
+    constexpr int NT = 64 * NW;
+    constexpr int C8 = BN / 8;
+    float* ep = reinterpret_cast<float*>(smem);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#pragma unroll 1
+    for (int pass = 0; pass < BM / EPR; ++pass) {
+        __syncthreads();
+        if ((wm * WM) / EPR == pass) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    *reinterpret_cast<float4*>(ep + (wm * WM - pass * EPR + a * 16 + fr) * EPL + wn * WN + b * 16 + 4 * fg) =
+                        make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+        }
+        __syncthreads();
 #pragma unroll 2
-        for (int c = tid; c < BM * C8; c += NT) {
+        for (int c = tid; c < EPR * C8; c += NT) {
             const int r = c / C8, col = (c % C8) * 8;
-            const int m = m0 + r;
+            const int m = m0 + pass * EPR + r;
             if (m >= g.M) continue;
             const int n = n0 + col;
             const size_t off = (size_t)m * g.N + n;
@@ -365,83 +437,104 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             }
             store8<TO>(C + off, v);
         }
-        return;
-    }
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-        const int m = m0 + wm * WM + a * 16 + fr;
-        if (m >= g.M) continue;
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const int n = n0 + wn * WN + b * 16 + 4 * fg;
-            const size_t off = (size_t)m * g.N + n;
-            float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-            if (g.bias) {
-                const float4 bb = *reinterpret_cast<const float4*>(g.bias + n);
-                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-            }
-            if constexpr (EPI == EPI_GELU) {
-                if (g.aux) store4<T>(reinterpret_cast<T*>(g.aux) + off, v);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = quick_gelu(v[i]);
-            } else if constexpr (EPI == EPI_GELU_BWD) {
-                float pa[4];
-                load4<T>(reinterpret_cast<const T*>(g.aux) + off, pa);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] *= quick_gelu_grad(pa[i]);
-            } else if constexpr (EPI == EPI_RESID) {
-                float r[4];
-                load4<float>(g.resid + off, r);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] += r[i];
-            }
-            store4<TO>(C + off, v);
-        }
     }
 }
 
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2>
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128>
 int launch_gemm(const GemmArgs& g, hipStream_t st)
 {
-    constexpr int LDS = gemm_lds_bytes<BM, BN, S>();
+    constexpr int WM = BM / WGM;
+    constexpr int LDS = gemm_lds_bytes<BM, BN, S, ROWB, WM>();
     static_assert(LDS <= 160 * 1024, "LDS");
+    constexpr int BK = ROWB / E::BYTES;
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN>,
+        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
             return EBC_E_LAUNCH;
         attr = true;
     }
-    if (g.N % BN) return EBC_E_UNSUPPORTED;
-    const int nwg = ((g.M + BM - 1) / BM) * (g.N / BN);
-    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
+    if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
+    const int nwg = ((g.M + BM - 1) / BM) * (g.N / BN) * g.splits;
+    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
 
-// Tile configuration: 0 = heuristic; EBC_GEMM_CFG=<1..7> forces one (tuning runs).
+// Tile configurations (EBC_GEMM_CFG=<n> forces one; EBC_GEMM_SPLITS=<s> forces the split count):
 //   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   6: 256x128/8w
-//   7: 256x256/8w   (2-stage LDS-DMA rings; 128-B K slabs)
+//   7: 256x256/8w   (2-stage rings of 128-B K rows)
 //   8: 128x64 S3   9: 128x128 S3   10: 256x128/8w S3   11: 192x128/8w S3   12: 128x64 S4   13: 128x96 S3
-int forced_cfg() {
-    static int cfg = -1;
-    if (cfg < 0) {
-        const char* e = getenv("EBC_GEMM_CFG");
-        cfg = e ? atoi(e) : 0;
-    }
-    return cfg;
+//   20: 256x256/8w  21: 256x128/8w  22: 128x256/8w  24: 128x128/4w   (4-stage rings
+//       of 64-B K rows, 16-bit only)
+// The L2 -> LDS fill rate per CU (~70 GB/s, MI355X_MICROARCH.md "gather into LDS") bounds a tile at
+// BM*BN/(BM+BN) flop per byte, so the default takes the 256-wide tiles and splits K where the
+// output has too few tiles to fill the 256 CUs.
+struct TileCfg { int id, bm, bn; };
+constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {6, 256, 128},
+                            {7, 256, 256}, {8, 128, 64}, {9, 128, 128}, {10, 256, 128}, {11, 192, 128}, {12, 128, 64},
+                            {13, 128, 96}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128}};
+const TileCfg* find_cfg(int id) {
+    for (const TileCfg& c : CFGS) if (c.id == id) return &c;
+    return nullptr;
+}
+int env_int(const char* name) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : 0;
+}
+int forced_cfg() { static const int v = env_int("EBC_GEMM_CFG"); return v; }
+int forced_splits() { static const int v = env_int("EBC_GEMM_SPLITS"); return v; }
+
+constexpr int NUM_CU = 256;
+// split-K workspace: [0, GEMM_CNT_BYTES) per-tile arrival counters (zero on entry, left zero),
+// then the f32 partial tiles
+constexpr size_t GEMM_CNT_BYTES = 16 * 1024;
+
+// heuristic tile choice for the 16-bit path; f32 (parity mode) always uses cfg 2
+inline long ntiles(int M, int N, int bm, int bn) { return (long)((M + bm - 1) / bm) * (N / bn); }
+int pick_cfg(int M, int N, int K, bool wide) {
+    // Measured on MI355X at the ViT-B/16 shapes (M = 16 x 229; tools/gemm_bench.py, r01): the
+    // 128x64 two-stage tile is best or within noise everywhere except the QKV projection (192x192,
+    // 8 waves) and the long-K N = 768 products (128x96, 3 stages).  The 256-wide / split-K tiles
+    // (cfg 20-24) are correct but slower here (their epilogue and split fix-up dominate) and are
+    // kept for forced runs only.
+    if (!wide) return 2;
+    if (N % 192 == 0 && N % 256 != 0 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
+    if (N % 96 == 0 && N < 2048 && K >= 2048) return 13;
+    return 2;
+}
+int pick_splits(int M, int N, int K, const TileCfg& c, int bk) {
+    if (c.id != 20 && c.id != 21) return 1;
+    const long tiles = ntiles(M, N, c.bm, c.bn);
+    int s = 1;
+    // more splits while the grid stays within ~1.2 waves of CUs and each slice keeps >= 512 of K
+    while (tiles * (s + 1) <= NUM_CU * 6 / 5 && K % (bk * (s + 1)) == 0 && K / (s + 1) >= 512) ++s;
+    return s;
 }
 
 template <class E, class TO, int EPI>
-int dispatch_tile(const GemmArgs& g, hipStream_t st)
+int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
 {
+    constexpr bool SIXTEEN = E::BYTES == 2;
     int cfg = forced_cfg();
-    const int bns[14] = {0, 128, 64, 192, 192, 96, 128, 256, 64, 128, 128, 128, 64, 96};
-    if (cfg > 13 || (cfg > 0 && g.N % bns[cfg] != 0)) cfg = 0;
-    if (cfg == 0) cfg = 2;
-    if constexpr (E::BYTES == 4) {                  // f32 (exact parity mode): one k32 step per
-        if (cfg >= 8) cfg = 2;                      // tile, register sets need an even ring
+    const TileCfg* c = find_cfg(cfg);
+    if (!c || g.N % c->bn != 0 || (cfg >= 8 && !SIXTEEN)) cfg = 0;
+    if (cfg == 0) cfg = pick_cfg(g.M, g.N, g.K, SIXTEEN);
+    c = find_cfg(cfg);
+    const int bk = cfg >= 20 ? 32 : 128 / E::BYTES;
+    int splits = forced_splits() > 0 ? forced_splits() : (cfg >= 20 ? pick_splits(g.M, g.N, g.K, *c, bk) : 1);
+    if (splits > 1) {
+        const int tiles = ((g.M + c->bm - 1) / c->bm) * (g.N / c->bn);
+        const size_t need = GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
+        if (!ws || ws_bytes < need || g.K % (splits * bk) || tiles > GEMM_CNT_BYTES / 4) {
+            splits = 1;
+        } else {
+            g.cnt = reinterpret_cast<int*>(ws);                                   // zero, re-armed by the kernel
+            g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
+        }
     }
+    g.splits = splits;
+    g.kslice = g.K / splits;
     switch (cfg) {
         case 1: return launch_gemm<E, TO, EPI, 128, 128, 2>(g, st);
         case 2: return launch_gemm<E, TO, EPI, 128, 64, 2>(g, st);
@@ -451,7 +544,7 @@ int dispatch_tile(const GemmArgs& g, hipStream_t st)
         case 6: return launch_gemm<E, TO, EPI, 256, 128, 2, 4, 2>(g, st);
         case 7: return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2>(g, st);
     }
-    if constexpr (E::BYTES == 2) {
+    if constexpr (SIXTEEN) {
         switch (cfg) {
             case 8: return launch_gemm<E, TO, EPI, 128, 64, 3>(g, st);
             case 9: return launch_gemm<E, TO, EPI, 128, 128, 3>(g, st);
@@ -459,26 +552,30 @@ int dispatch_tile(const GemmArgs& g, hipStream_t st)
             case 11: return launch_gemm<E, TO, EPI, 192, 128, 3, 4, 2>(g, st);
             case 12: return launch_gemm<E, TO, EPI, 128, 64, 4>(g, st);
             case 13: return launch_gemm<E, TO, EPI, 128, 96, 3>(g, st);
+            case 20: return launch_gemm<E, TO, EPI, 256, 256, 4, 4, 2, 64>(g, st);
+            case 21: return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64>(g, st);
+            case 22: return launch_gemm<E, TO, EPI, 128, 256, 4, 2, 4, 64>(g, st);
+            case 24: return launch_gemm<E, TO, EPI, 128, 128, 4, 2, 2, 64>(g, st);
         }
     }
     return EBC_E_UNSUPPORTED;
 }
 
 template <class E, int EPI>
-int dispatch_out(const GemmArgs& g, int out_f32, hipStream_t st)
+int dispatch_out(const GemmArgs& g, int out_f32, void* ws, size_t wsb, hipStream_t st)
 {
-    if (out_f32) return dispatch_tile<E, float, EPI>(g, st);
-    return dispatch_tile<E, typename E::T, EPI>(g, st);
+    if (out_f32) return dispatch_tile<E, float, EPI>(g, ws, wsb, st);
+    return dispatch_tile<E, typename E::T, EPI>(g, ws, wsb, st);
 }
 
 template <class E>
-int dispatch_epi(const GemmArgs& g, int epi, int out_f32, hipStream_t st)
+int dispatch_epi(const GemmArgs& g, int epi, int out_f32, void* ws, size_t wsb, hipStream_t st)
 {
     switch (epi) {
-        case EPI_STORE: return dispatch_out<E, EPI_STORE>(g, out_f32, st);
-        case EPI_GELU: return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_GELU>(g, st);
-        case EPI_RESID: return dispatch_tile<E, float, EPI_RESID>(g, st);
-        case EPI_GELU_BWD: return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_GELU_BWD>(g, st);
+        case EPI_STORE: return dispatch_out<E, EPI_STORE>(g, out_f32, ws, wsb, st);
+        case EPI_GELU: return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_GELU>(g, ws, wsb, st);
+        case EPI_RESID: return dispatch_tile<E, float, EPI_RESID>(g, ws, wsb, st);
+        case EPI_GELU_BWD: return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_GELU_BWD>(g, ws, wsb, st);
     }
     return EBC_E_ARG;
 }
@@ -486,17 +583,31 @@ int dispatch_epi(const GemmArgs& g, int epi, int out_f32, hipStream_t st)
 }  // namespace
 
 namespace ebc {
+size_t gemm_workspace_bytes(int dtype, int M, int N, int K)
+{
+    if (dtype == EBC_F32 || M <= 0 || N <= 0 || K <= 0) return 0;
+    int cfg = forced_cfg();
+    const TileCfg* c = find_cfg(cfg);
+    if (!c || N % c->bn != 0) cfg = pick_cfg(M, N, K, true);
+    c = find_cfg(cfg);
+    if (cfg < 20) return 0;
+    const int splits = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, 32);
+    if (splits <= 1) return 0;
+    const size_t tiles = (size_t)((M + c->bm - 1) / c->bm) * (N / c->bn);
+    return GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
+}
+
 int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
-            const float* resid, void* aux, int M, int N, int K, hipStream_t st)
+            const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws, size_t ws_bytes)
 {
     const int bk = dtype == EBC_F32 ? 32 : 64;
     if (M <= 0 || N <= 0 || K <= 0 || K % bk != 0 || N % 64 != 0 || !A || !B || !C) return EBC_E_ARG;
     if ((epi == EPI_RESID && !resid) || (epi == EPI_GELU_BWD && !aux)) return EBC_E_ARG;
     GemmArgs g{A, B, C, bias, resid, aux, M, N, K};
     switch (dtype) {
-        case EBC_F32: return dispatch_epi<EF32>(g, epi, 0, st);   // element type is already f32
-        case EBC_F16: return dispatch_epi<EF16>(g, epi, out_f32, st);
-        case EBC_BF16: return dispatch_epi<EBF16>(g, epi, out_f32, st);
+        case EBC_F32: return dispatch_epi<EF32>(g, epi, 0, nullptr, 0, st);   // element type is already f32
+        case EBC_F16: return dispatch_epi<EF16>(g, epi, out_f32, ws, ws_bytes, st);
+        case EBC_BF16: return dispatch_epi<EBF16>(g, epi, out_f32, ws, ws_bytes, st);
     }
     return EBC_E_ARG;
 }
@@ -506,5 +617,20 @@ extern "C" int ebc_gemm(int dtype, int epilogue, int out_f32, const void* A, con
                         const float* bias, const float* resid, void* aux, int M, int N, int K,
                         ebc_stream_t stream)
 {
-    return ebc::gemm_nt(dtype, epilogue, out_f32, A, B, C, bias, resid, aux, M, N, K, (hipStream_t)stream);
+    return ebc::gemm_nt(dtype, epilogue, out_f32, A, B, C, bias, resid, aux, M, N, K, (hipStream_t)stream, nullptr, 0);
+}
+
+extern "C" size_t ebc_gemm_workspace_bytes(int dtype, int M, int N, int K)
+{
+    return ebc::gemm_workspace_bytes(dtype, M, N, K);
+}
+
+extern "C" int ebc_gemm_ws(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
+                           const float* bias, const float* resid, void* aux, int M, int N, int K,
+                           void* workspace, size_t workspace_bytes, ebc_stream_t stream)
+{
+    // workspace contract (include/ebc_hip.h): zero-filled before its first use, then owned by the
+    // caller's stream; the kernels leave its counter block zero again after every call
+    return ebc::gemm_nt(dtype, epilogue, out_f32, A, B, C, bias, resid, aux, M, N, K, (hipStream_t)stream,
+                        workspace, workspace_bytes);
 }

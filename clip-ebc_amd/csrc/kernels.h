@@ -5,7 +5,10 @@
 
 namespace ebc {
 int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
-            const float* resid, void* aux, int M, int N, int K, hipStream_t st);
+            const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws = nullptr,
+            size_t ws_bytes = 0);
+// split-K workspace the heuristic wants for this shape (0: no split); zero-filled counter block first
+size_t gemm_workspace_bytes(int dtype, int M, int N, int K);
 int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,
                   void* out, float* outf, float* mean, float* rstd, int M, int D, hipStream_t st);
 int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg, int gstride, int goff,

@@ -14,6 +14,8 @@
 // overwritten in place before each block (and their gradient rows reduced + zeroed in backward).
 #include <vector>
 
+#include <algorithm>
+
 #include "ebc_common.h"
 #include "kernels.h"
 
@@ -46,6 +48,8 @@ struct Layout {
     // backward transients
     float *dXa, *dXb, *delta;
     void *dXt, *dH, *dA, *dO, *dQKV;
+    void* gws;                      // split-K GEMM workspace (leading counter block zeroed per call)
+    size_t gws_bytes;
     size_t bytes;
 };
 
@@ -94,6 +98,13 @@ Layout carve(void* ws, int B, int L, int G, int layers, int dtype, int training)
         lay.dXa = lay.dXb = lay.delta = nullptr;
         lay.dXt = lay.dH = lay.dA = lay.dO = lay.dQKV = nullptr;
     }
+    // the largest split-K workspace any of the encoder GEMMs asks for
+    size_t g = ebc::gemm_workspace_bytes(dtype, B * G, WIDTH, WIDTH);          // patch embedding
+    const int Mi = (int)M;
+    const int shapes[][2] = {{QKVW, WIDTH}, {WIDTH, WIDTH}, {MLP, WIDTH}, {WIDTH, MLP}, {WIDTH, QKVW}};
+    for (const auto& sh : shapes) g = std::max(g, ebc::gemm_workspace_bytes(dtype, Mi, sh[0], sh[1]));
+    lay.gws_bytes = g;
+    lay.gws = g ? c.take<void>(g) : nullptr;
     lay.bytes = c.off;
     return lay;
 }
@@ -122,11 +133,16 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
     Layout lay = carve(ws, B, L, G, layers, dtype, training);
     if (lay.bytes > ws_bytes) return EBC_E_ARG;
     if (NV > 0 && (!vpt || !vpt[0])) return EBC_E_ARG;
+    if (lay.gws && hipMemsetAsync(lay.gws, 0, std::min<size_t>(lay.gws_bytes, 16 * 1024), st) != hipSuccess)
+        return EBC_E_LAUNCH;
+    auto gemm = [&](int epi, int out_f32, const void* A, const void* Bm, void* C, const float* bias, const float* resid,
+                    void* aux, int m, int n, int k) {
+        return ebc::gemm_nt(dtype, epi, out_f32, A, Bm, C, bias, resid, aux, m, n, k, st, lay.gws, lay.gws_bytes);
+    };
 
     // patch embedding: im2col + GEMM with conv1 weight [768, 3*16*16] (image_encoder.py:141)
     EBC_TRY(ebc::im2col(dtype, image, lay.patch_t, B, H, W, 16, st));
-    EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 1, lay.patch_t, w->w_patch, lay.patch_f, nullptr, nullptr, nullptr,
-                         B * G, WIDTH, WIDTH, st));
+    EBC_TRY(gemm(EBC_EPI_STORE, 1, lay.patch_t, w->w_patch, lay.patch_f, nullptr, nullptr, nullptr, B * G, WIDTH, WIDTH));
     // CLS + pos + ln_pre, VPT_0 rows (model.py:150-168)
     EBC_TRY(ebc::embed_tokens(lay.patch_f, w->cls, w->pos, w->ln_pre_g, w->ln_pre_b, NV ? vpt[0] : nullptr,
                               vpt_bstride, lay.X[0], B, L, G, NV, WIDTH, st));
@@ -139,14 +155,13 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
             EBC_TRY(ebc::insert_vpt(X, vpt[l], vpt_bstride, B, L, NV, WIDTH, st));
         // x = x + out_proj(attn(ln_1(x)))
         EBC_TRY(ebc::layernorm_fwd(dtype, X, 0, 0, 0, p.ln1_g, p.ln1_b, lay.H, nullptr, s.m1, s.r1, M, WIDTH, st));
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.H, p.w_qkv, s.QKV, p.b_qkv, nullptr, nullptr, M, QKVW, WIDTH, st));
+        EBC_TRY(gemm(EBC_EPI_STORE, 0, lay.H, p.w_qkv, s.QKV, p.b_qkv, nullptr, nullptr, M, QKVW, WIDTH));
         EBC_TRY(ebc::attention_fwd(dtype, s.QKV, s.O, s.lse, B, L, HEADS, st));
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_RESID, 1, s.O, p.w_out, s.X1, p.b_out, X, nullptr, M, WIDTH, WIDTH, st));
+        EBC_TRY(gemm(EBC_EPI_RESID, 1, s.O, p.w_out, s.X1, p.b_out, X, nullptr, M, WIDTH, WIDTH));
         // x = x + c_proj(QuickGELU(c_fc(ln_2(x))))
         EBC_TRY(ebc::layernorm_fwd(dtype, s.X1, 0, 0, 0, p.ln2_g, p.ln2_b, lay.H, nullptr, s.m2, s.r2, M, WIDTH, st));
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_GELU, 0, lay.H, p.w_fc, lay.G, p.b_fc, nullptr, training ? s.A : nullptr,
-                             M, MLP, WIDTH, st));
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_RESID, 1, lay.G, p.w_proj, Xn, p.b_proj, s.X1, nullptr, M, WIDTH, MLP, st));
+        EBC_TRY(gemm(EBC_EPI_GELU, 0, lay.H, p.w_fc, lay.G, p.b_fc, nullptr, training ? s.A : nullptr, M, MLP, WIDTH));
+        EBC_TRY(gemm(EBC_EPI_RESID, 1, lay.G, p.w_proj, Xn, p.b_proj, s.X1, nullptr, M, WIDTH, MLP));
     }
     // ln_post on the patch rows only (CLS and prompt rows are dropped, model.py:185-188)
     EBC_TRY(ebc::layernorm_fwd(EBC_F32, lay.X[layers], G, L, 1 + NV, w->ln_post_g, w->ln_post_b, feat, nullptr,
@@ -170,6 +185,11 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
     float* dX = lay.dXa;
     float* dXo = lay.dXb;
     if (hipMemsetAsync(dX, 0, (size_t)M * WIDTH * 4, st) != hipSuccess) return EBC_E_LAUNCH;
+    if (lay.gws && hipMemsetAsync(lay.gws, 0, std::min<size_t>(lay.gws_bytes, 16 * 1024), st) != hipSuccess)
+        return EBC_E_LAUNCH;
+    auto gemm = [&](int epi, const void* A, const void* Bm, void* C, void* aux, int m, int n, int k) {
+        return ebc::gemm_nt(dtype, epi, 0, A, Bm, C, nullptr, nullptr, aux, m, n, k, st, lay.gws, lay.gws_bytes);
+    };
     if (hipMemsetAsync(lay.dXt, 0, (size_t)M * WIDTH * es, st) != hipSuccess) return EBC_E_LAUNCH;
     EBC_TRY(ebc::layernorm_bwd(dtype, 1, dfeat, lay.X[layers], G, L, 1 + NV, lay.mpost, lay.rpost, w->ln_post_g,
                                nullptr, dX, lay.dXt, B * G, WIDTH, st));
@@ -177,15 +197,15 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         const EbcVitLayer& p = w->layer[l];
         LayerSave& s = lay.s[l];
         // MLP half: dA = (dX . W_proj) * QuickGELU'(A);  dH2 = dA . W_fc;  dX1 = dX + LN2'(dH2)
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_GELU_BWD, 0, lay.dXt, p.wt_proj, lay.dA, nullptr, nullptr, s.A, M, MLP, WIDTH, st));
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dA, p.wt_fc, lay.dH, nullptr, nullptr, nullptr, M, WIDTH, MLP, st));
+        EBC_TRY(gemm(EBC_EPI_GELU_BWD, lay.dXt, p.wt_proj, lay.dA, s.A, M, MLP, WIDTH));
+        EBC_TRY(gemm(EBC_EPI_STORE, lay.dA, p.wt_fc, lay.dH, nullptr, M, WIDTH, MLP));
         EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, s.X1, 0, 0, 0, s.m2, s.r2, p.ln2_g, dX, dXo, lay.dXt, M, WIDTH, st));
         { float* t = dX; dX = dXo; dXo = t; }
         // attention half: dO = dX1 . W_out;  dQKV = attn'(...);  dH = dQKV . W_qkv;  dX = dX1 + LN1'(dH)
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dXt, p.wt_out, lay.dO, nullptr, nullptr, nullptr, M, WIDTH, WIDTH, st));
+        EBC_TRY(gemm(EBC_EPI_STORE, lay.dXt, p.wt_out, lay.dO, nullptr, M, WIDTH, WIDTH));
         EBC_TRY(ebc::attn_delta(dtype, lay.dO, s.O, lay.delta, B, L, HEADS, st));
         EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st));
-        EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dQKV, p.wt_qkv, lay.dH, nullptr, nullptr, nullptr, M, WIDTH, QKVW, st));
+        EBC_TRY(gemm(EBC_EPI_STORE, lay.dQKV, p.wt_qkv, lay.dH, nullptr, M, WIDTH, QKVW));
         EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, lay.X[l], 0, 0, 0, s.m1, s.r1, p.ln1_g, dX, dXo, lay.dXt, M, WIDTH, st));
         { float* t = dX; dX = dXo; dXo = t; }
         // prompt rows: dvpt_l = sum_b dX[b, 1..NV]; they were replaced at this block's input, so the

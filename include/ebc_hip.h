@@ -78,6 +78,14 @@ int ebc_dace_loss(const float* pred_class, const float* pred_density, const floa
 enum { EBC_EPI_STORE = 0, EBC_EPI_GELU = 1, EBC_EPI_RESID = 2, EBC_EPI_GELU_BWD = 3 };
 int ebc_gemm(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
              const float* bias, const float* resid, void* aux, int M, int N, int K, ebc_stream_t stream);
+/* Same, allowed to split K over workgroups (16-bit dtypes) when the output has too few 256-wide
+ * tiles to fill the GPU.  `workspace` (>= ebc_gemm_workspace_bytes; 0 = no split for this shape)
+ * must be zero-filled before its first use and is then owned by the stream: every call leaves
+ * its leading counter block zero again, the rest is scratch. */
+size_t ebc_gemm_workspace_bytes(int dtype, int M, int N, int K);
+int ebc_gemm_ws(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
+                const float* bias, const float* resid, void* aux, int M, int N, int K,
+                void* workspace, size_t workspace_bytes, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * CLIP ViT-B/16 + deep VPT encoder: CLIP_EBC._forward_vpt (models/clip/model.py:142-189), whole

@@ -88,3 +88,71 @@ def test_gemm_rejects_bad_shapes():
     C = torch.zeros(16, 64, device="cuda", dtype=torch.float16)
     rc = _lib.lib().ebc_gemm(1, 0, 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), None, None, None, 16, 64, 48, _lib.stream())
     assert rc == -1
+
+
+def _gemm_ws(dt, epi, out_f32, A, B, ws, bias=None, resid=None, aux=None, C=None):
+    M, K = A.shape
+    N = B.shape[0]
+    if C is None:
+        od = torch.float32 if (out_f32 or epi == 2) else dt
+        C = torch.empty(M, N, device=A.device, dtype=od)
+    rc = _lib.lib().ebc_gemm_ws(_lib.dtype_code(dt), epi, int(out_f32), _lib.ptr(A), _lib.ptr(B), _lib.ptr(C),
+                                _lib.ptr(bias), _lib.ptr(resid), _lib.ptr(aux), M, N, K, _lib.ptr(ws), ws.numel(),
+                                _lib.stream())
+    _lib.check(rc, "ebc_gemm_ws")
+    return C
+
+
+@pytest.mark.parametrize("dname", ["f16", "bf16"])
+def test_gemm_wide_tile_gelu(dname):
+    """M=3664, N=3072 picks the 256x256 tile (4-stage ring of 64-B K rows, single fragment set)."""
+    dt = DT[dname]
+    M, N, K = 3664, 3072, 768
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn(M, K, device="cuda", generator=g).to(dt)
+    B = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(dt)
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    aux = torch.empty(M, N, device="cuda", dtype=dt)
+    C = _gemm(dt, 1, 0, A, B, bias=bias, aux=aux)
+    pre = A.double() @ B.double().t() + bias.double()
+    assert _rel(aux, pre) < TOL[dname] + 4e-3
+    assert _rel(C, pre * torch.sigmoid(1.702 * pre)) < TOL[dname] + 4e-3
+
+
+@pytest.mark.parametrize("dname", ["f16", "bf16"])
+@pytest.mark.parametrize("M,N,K,epi", [(3664, 768, 3072, 2), (3664, 768, 2304, 0), (3136, 768, 3072, 0),
+                                       (3664, 3072, 768, 3)])
+def test_gemm_split_k(dname, M, N, K, epi):
+    """Split-K through ebc_gemm_ws: partial tiles + last-arriver reduction, counters re-armed."""
+    dt = DT[dname]
+    lib = _lib.lib()
+    nbytes = lib.ebc_gemm_workspace_bytes(_lib.dtype_code(dt), M, N, K)
+    ws = torch.zeros(max(nbytes, 16), device="cuda", dtype=torch.uint8)
+    g = torch.Generator(device="cuda").manual_seed(M + K + epi)
+    A = torch.randn(M, K, device="cuda", generator=g).to(dt)
+    B = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(dt)
+    bias = torch.randn(N, device="cuda", generator=g) if epi != 3 else None
+    ref = A.double() @ B.double().t()
+    if bias is not None:
+        ref = ref + bias.double()
+    if epi == 2:
+        X = torch.randn(M, N, device="cuda", generator=g)
+        ref = ref + X.double()
+        for _ in range(2):                          # the second call reuses the re-armed counters
+            Xi = X.clone()
+            _gemm_ws(dt, 2, 1, A, B, ws, bias=bias, resid=Xi, C=Xi)
+            assert _rel(Xi, ref) < TOL[dname]
+    elif epi == 3:
+        aux = torch.randn(M, N, device="cuda", generator=g).to(dt)
+        a = aux.double()
+        s = torch.sigmoid(1.702 * a)
+        ref = ref * (s + 1.702 * a * s * (1 - s))
+        C = _gemm_ws(dt, 3, 0, A, B, ws, aux=aux)
+        assert _rel(C, ref) < TOL[dname] + 4e-3
+    else:
+        for _ in range(2):
+            C = _gemm_ws(dt, 0, 1, A, B, ws, bias=bias)
+            assert _rel(C, ref) < TOL[dname]
+    torch.cuda.synchronize()
+    if nbytes:
+        assert int(ws[:16384].view(torch.int32).abs().sum()) == 0, "split-K counters not re-armed"

@@ -39,9 +39,12 @@ def main():
         C = torch.empty(M, N, device="cuda", dtype=torch.float32 if epi == 2 else dt)
         R = torch.randn(M, N, device="cuda")
 
+        nb = L.ebc_gemm_workspace_bytes(1, M, N, K)
+        ws = torch.zeros(max(nb, 16), device="cuda", dtype=torch.uint8)
+
         def ours():
-            _lib.check(L.ebc_gemm(1, epi, 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), _lib.ptr(bias), _lib.ptr(R),
-                                  _lib.ptr(aux), M, N, K, _lib.stream()), "gemm")
+            _lib.check(L.ebc_gemm_ws(1, epi, 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), _lib.ptr(bias), _lib.ptr(R),
+                                     _lib.ptr(aux), M, N, K, _lib.ptr(ws), ws.numel(), _lib.stream()), "gemm")
 
         def theirs():
             torch.nn.functional.linear(A, B)
