@@ -114,17 +114,9 @@ def probe_kernels(dtype, device, reps=50):
             "achieved": flops / t / 1e12, "flops_per_launch": flops}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
-    device = torch.device(f"cuda:{local}")
+def setup(args, rank, world, local, device):
+    """Model, loss, optimizer and the per-step closure (shared with tools/torch_prof.py)."""
     torch.manual_seed(42 + rank)
-
     from ebc_amd.model import get_model
     from ebc_amd.losses import DACELoss
     model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
@@ -158,6 +150,20 @@ def main():
         torch.stack([info[k] for k in ("loss", "ot_loss", "tv_loss", "count_loss", "ce_loss")], out=info_buf)
         if world > 1:
             dist.all_reduce(info_buf)
+    return step
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    device = torch.device(f"cuda:{local}")
+    step = setup(args, rank, world, local, device)
+    B = args.crops_per_gpu
 
     for i in range(args.warmup):
         step(i)

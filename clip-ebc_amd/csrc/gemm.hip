@@ -13,16 +13,18 @@
 // ds_read_b128 fragment reads are bank-conflict free; XCD-aware bijective tile remap.
 // The MFMA is issued "swapped" (weights as the A operand) so each lane ends with 4 consecutive
 // output columns of one row: vector epilogue loads/stores.
+#include <algorithm>
 #include <type_traits>
 
 #include "ebc_common.h"
 #include "mfma.h"
+#include "kernels.h"
 
 using namespace ebc;
 
 namespace {
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3 };
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4 };
 
 struct GemmArgs {
     const void* A; const void* B; void* C;
@@ -35,6 +37,16 @@ struct GemmArgs {
     int splits = 1, kslice = 0;
     float* part = nullptr;
     int* cnt = nullptr;
+    // implicit-GEMM 3x3 convolutions (stride 1, pad 1; decoder BasicBlock, models/utils.py:254-303):
+    //  MODE 1 (forward / data gradient): A row m = output pixel (b, y, x) of a [B][cHp][cWp][cC]
+    //    zero-padded NHWC image, K = 9 taps x cC (tap-major), k-tile kt reads the row shifted by
+    //    tap (ky, kx): ((ky-1)*cWp + kx-1) pixels;  B = weights [N][3][3][cC].
+    //  MODE 2 (weight gradient): A = dz^T [M][cQs], B = three kx-shifted copies x^T [3][cC][cQs] of
+    //    the padded image (x_kx^T[c][cG + q] = x[q + kx - 1][c]), row n = (ky, kx, c) starts at
+    //    (ky-1)*cWp; K runs over the interior image rows, kpi k-tiles per image.
+    int cH = 0, cW = 0, cC = 0, cHp = 0, cWp = 0, kpi = 0;
+    long cQs = 0, cG = 0;
+    float* stats = nullptr;  // EPI_STATS: [ceil(M/BM)][2][N] per-tile column sums / sums of squares
 };
 
 // Slab rows are ROWB bytes (one BK-deep K slice): 128 (BK = 64 for 16-bit, 32 for f32) or 64
@@ -139,7 +151,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB>
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
 {
     static_assert(S >= 2 && S <= 5, "stages");
@@ -168,34 +180,63 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
 
     const T* A = reinterpret_cast<const T*>(g.A);
     const T* Bw = reinterpret_cast<const T*>(g.B);
-    const int K = g.K, nk = g.kslice / BK, kbeg = split * g.kslice;
+    const int K = g.K, nk = g.kslice / BK, ktbase = split * nk;
 
-    // per-lane source rows for the LDS-DMA staging (fixed across k)
+    // per-lane source rows for the LDS-DMA staging (fixed across k; the k-tile offset is added by stage())
     const T* src[NLD];
+    bool isa[NLD];
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
         const int row = (wave * NLD + i) * RPI + lane / CPR;
         const int slot = lane % CPR;
         const int c = slot ^ swz_row<ROWB>(row);
         const T* base;
+        isa[i] = row < BM;
         if (row < BM) {
             int gr = m0 + row;
             gr = gr < g.M ? gr : g.M - 1;           // clamp: rows >= M are computed, never stored
-            base = A + (size_t)gr * K;
+            if constexpr (MODE == 1) {
+                const int hw = g.cH * g.cW;
+                const int b = gr / hw, r = gr - b * hw, y = r / g.cW, x = r - y * g.cW;
+                base = A + ((size_t)(b * g.cHp + y + 1) * g.cWp + x + 1) * g.cC;
+            } else if constexpr (MODE == 2) {
+                base = A + (size_t)gr * g.cQs + g.cG;
+            } else {
+                base = A + (size_t)gr * K;
+            }
         } else {
-            base = Bw + (size_t)(n0 + row - BM) * K;
+            const int n = n0 + row - BM;
+            if constexpr (MODE == 2) {
+                const int t = n / g.cC, cc = n - t * g.cC, ky = t / 3, kx = t - 3 * ky;
+                base = Bw + (size_t)(kx * g.cC + cc) * g.cQs + g.cG + (long)(ky - 1) * g.cWp;
+            } else {
+                base = Bw + (size_t)n * K;
+            }
         }
-        src[i] = base + kbeg + c * (16 / EB);
+        src[i] = base + c * (16 / EB);
     }
     auto stage = [&](int buf, int kt) {
 #if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 2)
         return;                                   // experiment build: no global->LDS traffic
 #endif
+        const int ktg = ktbase + kt;
+        long oa, ob;
+        if constexpr (MODE == 1) {
+            const int tpc = g.cC / BK;                // k-tiles per tap
+            const int tap = ktg / tpc, ky = tap / 3, kx = tap - 3 * ky;
+            oa = ((long)(ky - 1) * g.cWp + (kx - 1)) * g.cC + (long)(ktg - tap * tpc) * BK;
+            ob = (long)ktg * BK;
+        } else if constexpr (MODE == 2) {
+            const int img = ktg / g.kpi;
+            oa = ob = (long)img * g.cHp * g.cWp + g.cWp + (long)(ktg - img * g.kpi) * BK;
+        } else {
+            oa = ob = (long)ktg * BK;
+        }
         char* dst = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src[i] + (size_t)kt * BK),
+                (const __attribute__((address_space(1))) void*)(src[i] + (isa[i] ? oa : ob)),
                 EBC_LDS(dst + (wave * NLD + i) * 1024), 16, 0, 0);
         }
     };
@@ -391,6 +432,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     constexpr int NT = 64 * NW;
     constexpr int C8 = BN / 8;
     float* ep = reinterpret_cast<float*>(smem);
+    float col_s = 0.f, col_q = 0.f;               // EPI_STATS: column tid's sums over the tile's rows
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #pragma unroll 1
     for (int pass = 0; pass < BM / EPR; ++pass) {
@@ -437,10 +479,30 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             }
             store8<TO>(C + off, v);
         }
+        if constexpr (EPI == EPI_STATS) {
+            // BatchNorm batch statistics of the conv output (models/utils.py:254-303 bn1/bn2): per-tile
+            // column partials of sum and sum of squares, from the f32 accumulators (+ bias)
+            const int rows = min(EPR, g.M - (m0 + pass * EPR));
+            if (tid < BN) {
+                const float bc = g.bias ? g.bias[n0 + tid] : 0.f;
+#pragma unroll 4
+                for (int r = 0; r < rows; ++r) {
+                    const float x = ep[r * EPL + tid] + bc;
+                    col_s += x;
+                    col_q = fmaf(x, x, col_q);
+                }
+            }
+        }
+    }
+    if constexpr (EPI == EPI_STATS) {
+        if (tid < BN) {
+            g.stats[(size_t)tm * 2 * g.N + n0 + tid] = col_s;
+            g.stats[((size_t)tm * 2 + 1) * g.N + n0 + tid] = col_q;
+        }
     }
 }
 
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128>
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0>
 int launch_gemm(const GemmArgs& g, hipStream_t st)
 {
     constexpr int WM = BM / WGM;
@@ -449,14 +511,14 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
     constexpr int BK = ROWB / E::BYTES;
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB>,
+        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
             return EBC_E_LAUNCH;
         attr = true;
     }
     if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
     const int nwg = ((g.M + BM - 1) / BM) * (g.N / BN) * g.splits;
-    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
+    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -500,6 +562,10 @@ int pick_cfg(int M, int N, int K, bool wide) {
     // kept for forced runs only.
     if (!wide) return 2;
     if (N % 192 == 0 && N % 256 != 0 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
+    // r01 sweep: MLP c_fc / GELU' (N = 3072, K = 768): 256x192 27.6 / 31.9 us vs 34.3 / 37.0 (128x64)
+    if (N % 192 == 0 && N >= 2048 && K <= 1024 && ntiles(M, N, 256, 192) >= 160) return 3;
+    // decoder 3x3 convs as implicit GEMM (M = B*784, K = 9*768): one wave of 256x192 tiles
+    if (N % 192 == 0 && K >= 4096 && ntiles(M, N, 256, 192) >= 160) return 3;
     if (N % 96 == 0 && N < 2048 && K >= 2048) return 13;
     return 2;
 }
@@ -580,9 +646,102 @@ int dispatch_epi(const GemmArgs& g, int epi, int out_f32, void* ws, size_t wsb, 
     return EBC_E_ARG;
 }
 
+// implicit-GEMM 3x3 convolution tiles (MODE 1 / 2): 256x192 (8 waves) for the big decoder shapes,
+// 128x96 / 128x64 otherwise; f32 (parity mode) 128x64
+template <class E, class TO, int EPI, int MODE>
+int launch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st)
+{
+    if (cfg == 2) return launch_gemm<E, TO, EPI, 128, 64, 2, 2, 2, 128, MODE>(g, st);
+    if constexpr (E::BYTES == 2) {
+        if (cfg == 3) return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2, 128, MODE>(g, st);
+        if (cfg == 13) return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, MODE>(g, st);
+    }
+    return EBC_E_UNSUPPORTED;
+}
+
+int conv_cfg(bool sixteen, int mode, int M, int N)
+{
+    if (!sixteen) return 2;
+    if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;
+    return N % 96 == 0 ? 13 : 2;
+}
+int conv_splits(int cfg, int mode, int M, int N, int nk)
+{
+    if (mode != 2) return 1;
+    const TileCfg* c = find_cfg(cfg);
+    const long tiles = ntiles(M, N, c->bm, c->bn);
+    int s = 1;
+    while (tiles * (s + 1) <= NUM_CU * 6 / 5 && nk % (s + 1) == 0 && nk / (s + 1) >= 16) ++s;
+    return s;
+}
+
+template <class E>
+int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream_t st)
+{
+    constexpr bool SIXTEEN = E::BYTES == 2;
+    constexpr int BK = 128 / E::BYTES;
+    const int cfg = conv_cfg(SIXTEEN, mode, g.M, g.N);
+    const TileCfg* c = find_cfg(cfg);
+    if (g.N % c->bn || g.K % BK) return EBC_E_UNSUPPORTED;
+    int splits = conv_splits(cfg, mode, g.M, g.N, g.K / BK);
+    if (splits > 1) {
+        const size_t tiles = (size_t)ntiles(g.M, g.N, c->bm, c->bn);
+        const size_t need = GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
+        if (!ws || wsb < need || tiles > GEMM_CNT_BYTES / 4) {
+            splits = 1;
+        } else {
+            g.cnt = reinterpret_cast<int*>(ws);
+            g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
+        }
+    }
+    g.splits = splits;
+    g.kslice = g.K / splits;
+    using T = typename E::T;
+    if (mode == 1 && epi == EPI_STORE) return launch_conv_tile<E, T, EPI_STORE, 1>(g, cfg, st);
+    if (mode == 1 && epi == EPI_STATS) return launch_conv_tile<E, T, EPI_STATS, 1>(g, cfg, st);
+    if (mode == 2 && epi == EPI_STORE) return launch_conv_tile<E, float, EPI_STORE, 2>(g, cfg, st);
+    return EBC_E_UNSUPPORTED;
+}
+
 }  // namespace
 
 namespace ebc {
+size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K)
+{
+    const bool sixteen = dtype != EBC_F32;
+    const int cfg = conv_cfg(sixteen, mode, M, N);
+    const TileCfg* c = find_cfg(cfg);
+    const int bk = sixteen ? 64 : 32;
+    size_t need = GEMM_CNT_BYTES;
+    if (mode == 1) need += (size_t)((M + 127) / 128) * 2 * N * 4;     // EPI_STATS partials (BM >= 128)
+    const int s = conv_splits(cfg, mode, M, N, K / bk);
+    if (s > 1) need = std::max(need, GEMM_CNT_BYTES + (size_t)s * ntiles(M, N, c->bm, c->bn) * c->bm * c->bn * 4);
+    return need;
+}
+
+int conv_gemm(int dtype, int mode, int epi, const void* A, const void* B, void* C, const ConvGeom& geo, int M, int N,
+              int K, void* ws, size_t wsb, int* stats_tiles, hipStream_t st)
+{
+    const int bk = dtype == EBC_F32 ? 32 : 64;
+    if (M <= 0 || N <= 0 || K <= 0 || K % bk || N % 64 || !A || !B || !C || (mode != 1 && mode != 2)) return EBC_E_ARG;
+    GemmArgs g{A, B, C, nullptr, nullptr, nullptr, M, N, K};
+    g.cH = geo.H; g.cW = geo.W; g.cC = geo.C; g.cHp = geo.Hp; g.cWp = geo.Wp; g.kpi = geo.kpi;
+    g.cQs = geo.Qs; g.cG = geo.G;
+    if (mode == 1 && geo.C % bk) return EBC_E_UNSUPPORTED;
+    if (epi == EPI_STATS) {
+        if (!ws || wsb < conv_gemm_workspace_bytes(dtype, mode, M, N, K)) return EBC_E_ARG;
+        g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
+        const TileCfg* c = find_cfg(conv_cfg(dtype != EBC_F32, mode, M, N));
+        if (stats_tiles) *stats_tiles = (M + c->bm - 1) / c->bm;
+    }
+    switch (dtype) {
+        case EBC_F32: return dispatch_conv<EF32>(g, mode, epi, ws, wsb, st);
+        case EBC_F16: return dispatch_conv<EF16>(g, mode, epi, ws, wsb, st);
+        case EBC_BF16: return dispatch_conv<EBF16>(g, mode, epi, ws, wsb, st);
+    }
+    return EBC_E_ARG;
+}
+
 size_t gemm_workspace_bytes(int dtype, int M, int N, int K)
 {
     if (dtype == EBC_F32 || M <= 0 || N <= 0 || K <= 0) return 0;

@@ -9,6 +9,20 @@ int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void*
             size_t ws_bytes = 0);
 // split-K workspace the heuristic wants for this shape (0: no split); zero-filled counter block first
 size_t gemm_workspace_bytes(int dtype, int M, int N, int K);
+// implicit-GEMM 3x3 convolution geometry (gemm.hip MODE 1 / MODE 2)
+struct ConvGeom {
+    int H, W, C;      // output image (stride 1, pad 1), channels per tap
+    int Hp, Wp;       // padded operand image geometry (MODE 1: NHWC [B][Hp][Wp][C]; MODE 2: transposed rows)
+    int kpi;          // MODE 2: k-tiles per image
+    long Qs, G;       // MODE 2: row stride and leading guard (elements) of the transposed images
+};
+// mode 1: C[M = B*H*W, N] = conv(A = padded NHWC image, B = weights [N][9*C]), epi 0 store / 4 + BN stats
+//         (per-tile column partials at ws + 16 KiB: [stats_tiles][2][N]);
+// mode 2: C[M, N = 9*C] f32 = A^T-image . B^T-images (weight gradient), split-K through ws
+int conv_gemm(int dtype, int mode, int epi, const void* A, const void* B, void* C, const ConvGeom& geo, int M, int N,
+              int K, void* ws, size_t wsb, int* stats_tiles, hipStream_t st);
+size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K);
+constexpr size_t CONV_WS_STATS_OFFSET = 16 * 1024;
 int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,
                   void* out, float* outf, float* mean, float* rstd, int M, int D, hipStream_t st);
 int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg, int gstride, int goff,

@@ -23,6 +23,10 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
 _Z = ctypes.c_size_t
+_D = ctypes.c_double
+_L = ctypes.c_long
+_D = ctypes.c_double
+_L = ctypes.c_long
 
 # name -> (restype, argtypes); must mirror include/ebc_hip.h
 SIGNATURES = {
@@ -45,6 +49,19 @@ SIGNATURES = {
     "ebc_cast_f32": (_I, [_I, _P, _P, _Z, _P]),
     "ebc_tile_gather": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "ebc_tile_assemble": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "ebc_dec_geometry": (_I, [_I, _I, _I, _I, _I, _P]),
+    "ebc_dec_workspace_bytes": (_Z, [_I, _I, _I, _I, _I, _I]),
+    "ebc_dec_upsample_pad": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "ebc_conv3x3_fwd": (_I, [_I, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _P]),
+    "ebc_conv3x3_wgrad": (_I, [_I, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _P]),
+    "ebc_bn_finalize": (_I, [_P, _D, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "ebc_bn_relu_pad": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_bn_add_relu": (_I, [_I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P]),
+    "ebc_bn_bwd_reduce": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _L, _I, _P]),
+    "ebc_bn_bwd_finalize": (_I, [_P, _D, _P, _P, _P, _P, _P, _I, _P]),
+    "ebc_bn_bwd_apply": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_dec_transpose3": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }
 
 

@@ -208,15 +208,24 @@ class _VitFn(torch.autograd.Function):
 
 
 class _HeadFn(torch.autograd.Function):
-    """Projection (1x1 conv as MFMA GEMM) + similarity head (models/clip/model.py:198-217)."""
+    """Projection (1x1 conv as MFMA GEMM) + similarity head (models/clip/model.py:198-217).
+
+    `y` is the decoder output, NHWC [B,H,W,C] in the compute dtype when `nhwc` (the fused decoder's
+    layout: the GEMM reads it in place), else NCHW; the input gradient comes back in the same layout."""
 
     @staticmethod
-    def forward(ctx, y, weight, bias, logit_scale, text, anchors, cdtype):
+    def forward(ctx, y, weight, bias, logit_scale, text, anchors, cdtype, nhwc=False):
         L = _lib.lib()
-        B, C, Hh, Ww = y.shape
+        if nhwc:
+            B, Hh, Ww, C = y.shape
+        else:
+            B, C, Hh, Ww = y.shape
         P, HW, NB = B * Hh * Ww, Hh * Ww, text.shape[0]
         dt = _lib.dtype_code(cdtype)
-        Y = y.detach().permute(0, 2, 3, 1).to(cdtype).reshape(P, C).contiguous()
+        if nhwc and y.dtype == cdtype and y.is_contiguous():
+            Y = y.detach().reshape(P, C)
+        else:
+            Y = (y.detach() if nhwc else y.detach().permute(0, 2, 3, 1)).to(cdtype).reshape(P, C).contiguous()
         Wc = weight.detach().reshape(EMBED, C).to(cdtype).contiguous()
         bf = bias.detach().float().contiguous()
         Z = torch.empty(P, EMBED, device=y.device, dtype=torch.float32)
@@ -228,14 +237,14 @@ class _HeadFn(torch.autograd.Function):
         _lib.check(L.ebc_head_fwd(_lib.EBC_F32, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
                                   _lib.ptr(logits), _lib.ptr(expo), P, HW, NB, _lib.stream()), "ebc_head_fwd")
         ctx.save_for_backward(Y, Wc, Z, ls, text, anchors)
-        ctx.meta = (B, C, Hh, Ww, cdtype, y.dtype, weight.shape)
+        ctx.meta = (B, C, Hh, Ww, cdtype, y.dtype, weight.shape, nhwc)
         return logits, expo
 
     @staticmethod
     def backward(ctx, dlogits, dexp):
         L = _lib.lib()
         Y, Wc, Z, ls, text, anchors = ctx.saved_tensors
-        B, C, Hh, Ww, cdtype, ydt, wshape = ctx.meta
+        B, C, Hh, Ww, cdtype, ydt, wshape, nhwc = ctx.meta
         P, HW, NB = B * Hh * Ww, Hh * Ww, text.shape[0]
         dev = Z.device
         dl = torch.zeros(B, NB, Hh, Ww, device=dev) if dlogits is None else dlogits.float().contiguous()
@@ -252,8 +261,153 @@ class _HeadFn(torch.autograd.Function):
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dZ), _lib.ptr(Wt), _lib.ptr(dY), None, None, None,
                               P, C, EMBED, _lib.stream()), "ebc_gemm(projection dX)")
         dW = torch.mm(dZ.t(), Y).float().reshape(wshape)         # dW = dZ^T Y (library GEMM, K = B*H*W)
-        dy = dY.view(B, Hh, Ww, C).permute(0, 3, 1, 2).to(ydt)
-        return dy, dW, dbias, dscale.reshape(()), None, None, None
+        dy = dY.view(B, Hh, Ww, C) if nhwc else dY.view(B, Hh, Ww, C).permute(0, 3, 1, 2).to(ydt)
+        return dy, dW, dbias, dscale.reshape(()), None, None, None, None
+
+
+# ----------------------------------------------------------------------------- decoder
+_DEC_WS: Dict[torch.device, Tensor] = {}
+
+
+def _dec_workspace(dev: torch.device, nbytes: int) -> Tensor:
+    """Stream-owned scratch of the decoder calls; its first 16 KiB (split-K counters) start zeroed."""
+    ws = _DEC_WS.get(dev)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(max(nbytes, 1 << 20), device=dev, dtype=torch.uint8)
+        _DEC_WS[dev] = ws
+    return ws
+
+
+def _bn_group(bn: nn.Module):
+    """SyncBatchNorm (DDP, trainer.py:147): statistics are all-reduced over its process group."""
+    if isinstance(bn, nn.SyncBatchNorm) and torch.distributed.is_available() and torch.distributed.is_initialized():
+        pg = bn.process_group or torch.distributed.group.WORLD
+        if torch.distributed.get_world_size(pg) > 1:
+            return pg
+    return None
+
+
+def _bn_momentum(bn: nn.Module) -> float:
+    """nn.BatchNorm2d's exponential_average_factor (momentum None: cumulative average)."""
+    if bn.momentum is not None:
+        return float(bn.momentum)
+    return 1.0 / float(bn.num_batches_tracked.item())
+
+
+class _DecoderFn(torch.autograd.Function):
+    """BasicBlock(768, 768) (models/utils.py:254-303) after the x`up` bilinear reduction adapt
+    (models/clip/model.py:195-196), on libebc_hip.so: implicit-GEMM 3x3 convs, BatchNorm statistics in
+    the conv epilogue, fused BN/ReLU/residual kernels and the whole backward (ebc_dec_* / ebc_conv3x3_* /
+    ebc_bn_* in include/ebc_hip.h).  feat [B,h,w,C] f32 (NHWC) -> y [B,H,W,C] in the compute dtype."""
+
+    @staticmethod
+    def forward(ctx, feat, w1, g1, b1, w2, g2, b2, blk, up, cdtype, training):
+        L = _lib.lib()
+        feat = feat.detach().contiguous()
+        B, h, w, C = feat.shape
+        H, W, N = h * up, w * up, w1.shape[0]
+        if N != C or w2.shape[0] != C or C % 64:
+            raise NotImplementedError("fused decoder: BasicBlock(C, C) with C % 64 == 0 only")
+        dev, dt, st = feat.device, _lib.dtype_code(cdtype), _lib.stream()
+        geo = (ctypes.c_long * 6)()
+        _lib.check(L.ebc_dec_geometry(dt, B, H, W, C, geo), "ebc_dec_geometry")
+        Q, Qs = geo[4], geo[5]
+        P = B * H * W
+        nbytes = L.ebc_dec_workspace_bytes(dt, B, H, W, C, N)
+        ws = _dec_workspace(dev, nbytes)
+        f32 = dict(device=dev, dtype=torch.float32)
+        xpad = torch.empty(Q, C, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_dec_upsample_pad(dt, _lib.ptr(feat), _lib.ptr(xpad), B, h, w, C, up, st), "upsample_pad")
+        outs = []
+        inp = xpad
+        bns = (blk.bn1, blk.bn2)
+        for i, (wt, gm, bt) in enumerate(((w1, g1, b1), (w2, g2, b2))):
+            bn = bns[i]
+            wk = wt.detach().permute(0, 2, 3, 1).to(cdtype).contiguous()           # [N][3][3][C]
+            z = torch.empty(P, N, device=dev, dtype=cdtype)
+            use_batch = training or not bn.track_running_stats
+            colsum = torch.empty(2, N, device=dev, dtype=torch.float64) if use_batch else None
+            _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(inp), _lib.ptr(wk), _lib.ptr(z), _lib.ptr(colsum), _lib.ptr(ws),
+                                         ws.numel(), B, H, W, C, N, st), "ebc_conv3x3_fwd")
+            count = float(P)
+            pg = _bn_group(bn) if use_batch else None
+            if pg is not None:
+                torch.distributed.all_reduce(colsum, group=pg)
+                count *= torch.distributed.get_world_size(pg)
+            mean, rstd, scale, shift = (torch.empty(N, **f32) for _ in range(4))
+            upd = use_batch and training and bn.track_running_stats
+            if upd:
+                bn.num_batches_tracked.add_(1)
+            mom = _bn_momentum(bn) if upd else 0.0
+            _lib.check(L.ebc_bn_finalize(_lib.ptr(colsum), count, float(bn.eps), mom, _lib.ptr(gm.detach()),
+                                         _lib.ptr(bt.detach()), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale),
+                                         _lib.ptr(shift), _lib.ptr(bn.running_mean) if (upd or not use_batch) else None,
+                                         _lib.ptr(bn.running_var) if (upd or not use_batch) else None, N, st),
+                       "ebc_bn_finalize")
+            outs.append((z, mean, rstd, scale, shift, count, pg))
+            if i == 0:
+                hpad = torch.empty(Q, N, device=dev, dtype=cdtype)
+                _lib.check(L.ebc_bn_relu_pad(dt, _lib.ptr(z), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(hpad),
+                                             B, H, W, N, st), "ebc_bn_relu_pad")
+                inp = hpad
+        z2, _, _, scale2, shift2, _, _ = outs[1]
+        y = torch.empty(B, H, W, N, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_bn_add_relu(dt, _lib.ptr(z2), _lib.ptr(scale2), _lib.ptr(shift2), _lib.ptr(feat), up,
+                                     _lib.ptr(y), B, H, W, N, st), "ebc_bn_add_relu")
+        ctx.save_for_backward(xpad, hpad, y, w1, g1, w2, g2)
+        ctx.outs = outs
+        ctx.meta = (B, h, w, H, W, C, N, up, cdtype, Q, Qs, P)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        L = _lib.lib()
+        xpad, hpad, y, w1, g1, w2, g2 = ctx.saved_tensors
+        B, h, w, H, W, C, N, up, cdtype, Q, Qs, P = ctx.meta
+        dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream()
+        gy = gy.to(cdtype).contiguous()
+        ws = _dec_workspace(dev, L.ebc_dec_workspace_bytes(dt, B, H, W, C, N))
+        f32 = dict(device=dev, dtype=torch.float32)
+        grads = []
+        dnext = gy                                    # gradient at the current BN output's ReLU
+        mask = y                                      # ReLU mask source (None: recompute from z)
+        for i in (1, 0):
+            z, mean, rstd, scale, shift, count, pg = ctx.outs[i]
+            gm = (g1, g2)[i]
+            sums = torch.empty(2, N, device=dev, dtype=torch.float64)
+            _lib.check(L.ebc_bn_bwd_reduce(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
+                                           _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(sums),
+                                           _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce")
+            if pg is not None:
+                torch.distributed.all_reduce(sums, group=pg)
+            dg, db, coef = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty(3, N, **f32)
+            _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
+                                             _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize")
+            dzpad = torch.empty(Q, N, device=dev, dtype=cdtype)
+            dzT = torch.empty(N, Qs, device=dev, dtype=cdtype)
+            _lib.check(L.ebc_bn_bwd_apply(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
+                                          _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(coef),
+                                          _lib.ptr(dzpad), _lib.ptr(dzT), B, H, W, N, st), "ebc_bn_bwd_apply")
+            src = hpad if i == 1 else xpad                # the conv's input image
+            xT3 = torch.empty(3, C, Qs, device=dev, dtype=cdtype)
+            _lib.check(L.ebc_dec_transpose3(dt, _lib.ptr(src), _lib.ptr(xT3), B, H, W, C, st), "ebc_dec_transpose3")
+            dw = torch.empty(N, 3, 3, C, **f32)
+            _lib.check(L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws), ws.numel(),
+                                           B, H, W, C, N, st), "ebc_conv3x3_wgrad")
+            del xT3, dzT
+            wt = (w1, w2)[i]
+            wf = wt.detach().flip(2, 3).permute(1, 2, 3, 0).to(cdtype).contiguous()    # [C][3][3][N]
+            dx = torch.empty(P, C, device=dev, dtype=cdtype)
+            _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(dzpad), _lib.ptr(wf), _lib.ptr(dx), None, _lib.ptr(ws),
+                                         ws.numel(), B, H, W, N, C, st), "ebc_conv3x3_fwd(dgrad)")
+            grads.append((dw.permute(0, 3, 1, 2).contiguous(), dg, db))
+            dnext, mask = dx, None
+        dfeat = torch.empty(B, h, w, C, **f32)
+        _lib.check(L.ebc_dec_upsample_bwd(dt, _lib.ptr(dnext), _lib.ptr(gy), _lib.ptr(y), _lib.ptr(dfeat), B, h, w, C,
+                                          up, st), "ebc_dec_upsample_bwd")
+        (dw2, dg2, db2), (dw1, dg1, db1) = grads
+        ctx.outs = None
+        return dfeat, dw1, dg1, db1, dw2, dg2, db2, None, None, None, None
 
 
 # ----------------------------------------------------------------------------- model
@@ -290,6 +444,10 @@ class CLIP_EBC(nn.Module):
         self.reduction = self.encoder_reduction if reduction is None else reduction
         self.channels, self.clip_embed_dim = WIDTH, EMBED
         decoder_cfg = decoder_cfg or [WIDTH]
+        if list(decoder_cfg) != [WIDTH]:
+            raise NotImplementedError("vit_b_16 decoder is BasicBlock [768] (models/clip/model.py:250-251)")
+        if reduction is not None and (PATCH % reduction or PATCH // reduction not in (1, 2)):
+            raise NotImplementedError("reduction must be 16 or 8 for vit_b_16 (x1 / x2 bilinear adapt)")
         layers, cin = [], WIDTH
         for v in decoder_cfg:
             layers.append(BasicBlock(cin, v))
@@ -364,27 +522,32 @@ class CLIP_EBC(nn.Module):
             return vpts, self.num_vpt * WIDTH
         return vpts, 0
 
-    def _forward_vpt(self, x: Tensor) -> Tensor:
-        """[B,3,H,W] -> [B,768,H/16,W/16] (channels_last memory), models/clip/model.py:142-189."""
+    def _forward_vpt_nhwc(self, x: Tensor) -> Tensor:
+        """[B,3,H,W] -> ln_post patch tokens [B,H/16,W/16,768] f32 (NHWC), models/clip/model.py:142-189."""
         B, _, H, W = x.shape
         cache = self._encoder_cache(self._compute_dtype(x), x.device)
         vpts, bstride = self._prepare_vpts(B)
         training = torch.is_grad_enabled() and any(v.requires_grad for v in vpts)
         with torch.autocast("cuda", enabled=False):
             feat = _VitFn.apply(cache, x, bstride, training, *vpts)
-        return feat.view(B, H // PATCH, W // PATCH, WIDTH).permute(0, 3, 1, 2)
+        return feat.view(B, H // PATCH, W // PATCH, WIDTH)
+
+    def _forward_vpt(self, x: Tensor) -> Tensor:
+        """[B,3,H,W] -> [B,768,H/16,W/16] (channels_last memory), models/clip/model.py:142-189."""
+        return self._forward_vpt_nhwc(x).permute(0, 3, 1, 2)
 
     def forward(self, x: Tensor) -> Union[Tensor, Tuple[Tensor, Tensor]]:
         if not x.is_cuda:
             raise RuntimeError("ebc_amd.CLIP_EBC runs on the MI355X HIP path only (input is on the CPU)")
         cdt = self._compute_dtype(x)
-        x = self._forward_vpt(x)
-        if self.reduction != self.encoder_reduction:
-            x = F.interpolate(x, scale_factor=self.encoder_reduction / self.reduction, mode="bilinear")
-        x = self.image_decoder(x)
+        feat = self._forward_vpt_nhwc(x)
+        up = self.encoder_reduction // self.reduction                      # model.py:195-196 (x2 for reduction 8)
+        blk = self.image_decoder[0]
         with torch.autocast("cuda", enabled=False):
-            logits, exp = _HeadFn.apply(x, self.projection.weight, self.projection.bias, self.logit_scale,
-                                        self.text_features, self._anchors, cdt)
+            y = _DecoderFn.apply(feat, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight,
+                                 blk.bn2.weight, blk.bn2.bias, blk, up, cdt, self.training)
+            logits, exp = _HeadFn.apply(y, self.projection.weight, self.projection.bias, self.logit_scale,
+                                        self.text_features, self._anchors, cdt, True)
         return (logits, exp) if self.training else exp
 
 

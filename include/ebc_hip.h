@@ -161,6 +161,57 @@ int ebc_tile_gather(const float* image, float* tiles, int C, int H, int W, int w
 int ebc_tile_assemble(const float* preds, float* out, int Cp, int H, int W, int wh, int ww, int sh, int sw,
                       int reduction, ebc_stream_t stream);
 
+
+/* ------------------------------------------------------------------------------------------
+ * Decoder BasicBlock (models/utils.py:254-303, cfg [768] for vit_b_16, models/clip/model.py:250-251)
+ * with the reduction adapt F.interpolate(x2, bilinear, align_corners=False) (model.py:195-196),
+ * training-mode BatchNorm2d (batch statistics, running stats; SyncBatchNorm = caller all-reduces
+ * `colsum` / `sums` between the two calls that bracket them) and the whole backward.
+ * Layouts (T = dtype): feat [B][h][w][C] f32; padded NHWC images [Q][C] T with Q = B*Hp*Wp;
+ * z / dx / y [B*H*W][C] T; transposed images xT3 [3][C][Qs], dzT [N][Qs] T; conv weights
+ * [N][3][3][C] T (forward) and [C][3][3][N] T (flipped, data gradient); dw [N][3][3][C] f32.
+ * ebc_dec_geometry writes {Hp, Wp, G, kpi, Q, Qs}.  The workspace's first 16 KiB must be zero before
+ * the first call (split-K arrival counters, re-armed by every call); it is stream-owned scratch. */
+int ebc_dec_geometry(int dtype, int B, int H, int W, int C, long* out6);
+size_t ebc_dec_workspace_bytes(int dtype, int B, int H, int W, int C, int N);
+/* xpad = zero-padded bilinear x`up` upsample of feat (H = h*up) */
+int ebc_dec_upsample_pad(int dtype, const float* feat, void* xpad, int B, int h, int w, int C, int up,
+                         ebc_stream_t stream);
+/* out[B*H*W][N] = conv3x3(xpad, weight) (nn.Conv2d(C, N, 3, padding=1, bias=False)); colsum != NULL:
+ * also the f64 column sums [2][N] (sum, sum of squares) for BatchNorm */
+int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, double* colsum, void* ws,
+                    size_t wsb, int B, int H, int W, int C, int N, ebc_stream_t stream);
+/* dw[N][3][3][C] f32 = weight gradient from dzT and xT3 */
+int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, float* dw, void* ws, size_t wsb, int B, int H,
+                      int W, int C, int N, ebc_stream_t stream);
+/* BatchNorm2d statistics -> mean, rstd, scale = gamma*rstd, shift = beta - mean*scale; running stats
+ * updated (momentum, unbiased variance) when colsum != NULL, read (eval) when colsum == NULL */
+int ebc_bn_finalize(const double* colsum, double count, float eps, float momentum, const float* gamma,
+                    const float* beta, float* mean, float* rstd, float* scale, float* shift, float* running_mean,
+                    float* running_var, int C, ebc_stream_t stream);
+/* hpad = zero-padded relu(z*scale + shift) */
+int ebc_bn_relu_pad(int dtype, const void* z, const float* scale, const float* shift, void* hpad, int B, int H,
+                    int W, int C, ebc_stream_t stream);
+/* y = relu(z*scale + shift + bilinear_up(feat)) */
+int ebc_bn_add_relu(int dtype, const void* z, const float* scale, const float* shift, const float* feat, int up,
+                    void* y, int B, int H, int W, int C, ebc_stream_t stream);
+/* sums[2][C] f64 = (sum g, sum g*xhat), g = gy * relu'(mask_y, or z*scale+shift when mask_y == NULL) */
+int ebc_bn_bwd_reduce(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
+                      const float* rstd, const float* scale, const float* shift, double* sums, void* ws, size_t wsb,
+                      long P, int C, ebc_stream_t stream);
+/* dgamma, dbeta (may be NULL) and coef[3][C] for ebc_bn_bwd_apply */
+int ebc_bn_bwd_finalize(const double* sums, double count, const float* gamma, const float* rstd, float* dgamma,
+                        float* dbeta, float* coef, int C, ebc_stream_t stream);
+/* dz = BatchNorm input gradient -> dzpad (padded NHWC) and dzT (transposed) */
+int ebc_bn_bwd_apply(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
+                     const float* rstd, const float* scale, const float* shift, const float* coef, void* dzpad,
+                     void* dzT, int B, int H, int W, int C, ebc_stream_t stream);
+/* xT3 = kx-shifted transposed copies of a padded NHWC image (weight-gradient operand) */
+int ebc_dec_transpose3(int dtype, const void* xpad, void* xT3, int B, int H, int W, int C, ebc_stream_t stream);
+/* dfeat = bilinear_up^T(dx + gy * relu'(mask_y)), dx may be NULL */
+int ebc_dec_upsample_bwd(int dtype, const void* dx, const void* gy, const void* mask_y, float* dfeat, int B, int h,
+                         int w, int C, int up, ebc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

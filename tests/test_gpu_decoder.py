@@ -1,0 +1,126 @@
+"""Decoder BasicBlock on the HIP implicit-GEMM path vs a torch f64 CPU restatement.
+
+Reference semantics: F.interpolate(x, scale_factor=up, mode="bilinear") (models/clip/model.py:195-196)
+then BasicBlock (models/utils.py:254-303): conv3x3-bn-relu-conv3x3-bn-(+x)-relu, BatchNorm2d in
+training mode (batch statistics, running-stat update) or eval mode (running statistics).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+# forward rel-L2 bars; gradients get GTOL (BatchNorm backward subtracts batch means: f32 summation-order
+# differences of the 7k-deep convolutions are amplified ~10x)
+TOL = {torch.float32: 2e-5, torch.float16: 2e-2, torch.bfloat16: 6e-2}
+GTOL = {torch.float32: 5e-4, torch.float16: 4e-2, torch.bfloat16: 1.2e-1}
+
+
+def _ref(feat, w1, g1, b1, w2, g2, b2, up, rm, rv, training):
+    x = feat.permute(0, 3, 1, 2)
+    if up > 1:
+        x = F.interpolate(x, scale_factor=up, mode="bilinear")
+    o = F.conv2d(x, w1, padding=1)
+    o = F.relu(F.batch_norm(o, rm[0], rv[0], g1, b1, training, 0.1, 1e-5))
+    o = F.conv2d(o, w2, padding=1)
+    o = F.batch_norm(o, rm[1], rv[1], g2, b2, training, 0.1, 1e-5)
+    return F.relu(o + x).permute(0, 2, 3, 1)
+
+
+def _block(C):
+    from ebc_amd.model import BasicBlock
+    torch.manual_seed(0)
+    blk = BasicBlock(C, C)
+    with torch.no_grad():
+        for bn in (blk.bn1, blk.bn2):
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+            bn.running_mean.uniform_(-0.1, 0.1)
+            bn.running_var.uniform_(0.5, 2.0)
+    return blk
+
+
+@pytest.mark.parametrize("dtype,B,h,C,up", [(torch.float32, 2, 14, 768, 2), (torch.float16, 2, 14, 768, 2),
+                                            (torch.bfloat16, 2, 14, 768, 2), (torch.float32, 3, 7, 128, 1),
+                                            (torch.float16, 3, 10, 192, 2)])
+def test_decoder_train_fwd_bwd(dtype, B, h, C, up):
+    from ebc_amd.model import _DecoderFn
+    blk = _block(C)
+    g = torch.Generator().manual_seed(1)
+    feat = torch.randn(B, h, h, C, generator=g)
+    H = h * up
+    gy = torch.randn(B, H, H, C, generator=g)
+    # reference (f64, CPU)
+    params = [p.detach().double().requires_grad_() for p in
+              (blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias)]
+    fr = feat.double().requires_grad_()
+    rm = [blk.bn1.running_mean.double().clone(), blk.bn2.running_mean.double().clone()]
+    rv = [blk.bn1.running_var.double().clone(), blk.bn2.running_var.double().clone()]
+    yr = _ref(fr, *params, up, rm, rv, True)
+    (yr * gy.double()).sum().backward()
+    # HIP
+    blk = blk.cuda().train()
+    fd = feat.cuda().requires_grad_()
+    y = _DecoderFn.apply(fd, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+                         blk.bn2.bias, blk, up, dtype, True)
+    assert y.shape == (B, H, H, C) and y.dtype == dtype
+    (y.float() * gy.cuda()).sum().backward()
+    tol = TOL[dtype]
+    assert rel_l2(y.detach().float().cpu().numpy(), yr.detach().numpy()) < tol
+    assert rel_l2(fd.grad.cpu().numpy(), fr.grad.numpy()) < GTOL[dtype]
+    for p, r in zip((blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias),
+                    params):
+        assert rel_l2(p.grad.cpu().numpy(), r.grad.numpy()) < GTOL[dtype], p.shape
+    for bn, m, v in zip((blk.bn1, blk.bn2), rm, rv):
+        assert rel_l2(bn.running_mean.cpu().numpy(), m.numpy()) < tol
+        assert rel_l2(bn.running_var.cpu().numpy(), v.numpy()) < tol
+        assert int(bn.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_decoder_eval_uses_running_stats(dtype):
+    from ebc_amd.model import _DecoderFn
+    C, B, h, up = 256, 2, 14, 2
+    blk = _block(C)
+    feat = torch.randn(B, h, h, C, generator=torch.Generator().manual_seed(2))
+    rm = [blk.bn1.running_mean.double().clone(), blk.bn2.running_mean.double().clone()]
+    rv = [blk.bn1.running_var.double().clone(), blk.bn2.running_var.double().clone()]
+    with torch.no_grad():
+        yr = _ref(feat.double(), *(p.double() for p in (blk.conv1.weight, blk.bn1.weight, blk.bn1.bias,
+                                                         blk.conv2.weight, blk.bn2.weight, blk.bn2.bias)),
+                  up, rm, rv, False)
+        blk = blk.cuda().eval()
+        y = _DecoderFn.apply(feat.cuda(), blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight,
+                             blk.bn2.weight, blk.bn2.bias, blk, up, dtype, False)
+    assert rel_l2(y.float().cpu().numpy(), yr.numpy()) < TOL[dtype]
+    assert int(blk.bn1.num_batches_tracked) == 0
+
+
+def test_conv3x3_abi_matches_torch():
+    """ebc_conv3x3_fwd (implicit GEMM, f16) on a padded NHWC image vs torch conv2d, incl. BN column sums."""
+    from ebc_amd import _lib
+    import ctypes
+    L = _lib.lib()
+    B, H, W, C, N = 2, 28, 28, 768, 768
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, C, H, W, generator=g)
+    wt = torch.randn(N, C, 3, 3, generator=g) / 80
+    geo = (ctypes.c_long * 6)()
+    _lib.check(L.ebc_dec_geometry(_lib.EBC_F16, B, H, W, C, geo), "geo")
+    Hp, Wp, Q = geo[0], geo[1], geo[4]
+    xpad = torch.zeros(B, Hp, Wp, C)
+    xpad[:, 1:H + 1, 1:W + 1] = x.permute(0, 2, 3, 1)
+    xpad = xpad.reshape(Q, C).half().cuda()
+    wk = wt.permute(0, 2, 3, 1).half().contiguous().cuda()
+    out = torch.empty(B * H * W, N, dtype=torch.float16, device="cuda")
+    colsum = torch.empty(2, N, dtype=torch.float64, device="cuda")
+    ws = torch.zeros(L.ebc_dec_workspace_bytes(_lib.EBC_F16, B, H, W, C, N), dtype=torch.uint8, device="cuda")
+    _lib.check(L.ebc_conv3x3_fwd(_lib.EBC_F16, _lib.ptr(xpad), _lib.ptr(wk), _lib.ptr(out), _lib.ptr(colsum),
+                                 _lib.ptr(ws), ws.numel(), B, H, W, C, N, _lib.stream()), "conv")
+    ref = F.conv2d(x.half().double(), wt.half().double(), padding=1).permute(0, 2, 3, 1).reshape(-1, N)
+    assert rel_l2(out.float().cpu().numpy(), ref.numpy()) < 2e-3
+    np.testing.assert_allclose(colsum[0].cpu().numpy(), ref.sum(0).numpy(), rtol=1e-2, atol=1e-1)
+    np.testing.assert_allclose(colsum[1].cpu().numpy(), (ref ** 2).sum(0).numpy(), rtol=2e-3)
