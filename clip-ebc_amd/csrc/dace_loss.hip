@@ -22,6 +22,7 @@
 //    never flushes f32 denormals).  The err pass's K^T u is reused by the next iteration.
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "ebc_common.h"
 
@@ -41,10 +42,13 @@ template <int G> struct Cfg {
     // ~3 cycles per lane).
     static constexpr int NB = (G / 4) * (G / 4);
     static constexpr int KSPLIT = NT / NB;
-    // fixed LDS (floats): pd, td, b, v0, v1, partial[KSPLIT][GG], misc[64]
-    static constexpr int FIXED = 5 * GG + KSPLIT * GG + 64;
+    // home buckets of the sorted Sinkhorn: one per BSxBS cell block; a <= 9-cell window starting in
+    // block B reaches block B + HALO
+    static constexpr int BS = 4, NB1 = G / BS, NBK = NB1 * NB1, HALO = 8 / BS;
+    // fixed LDS (floats): pd, td, b, v0, v1, partial[KSPLIT][GG], misc[64], bucket counts/starts
+    static constexpr int FIXED = 5 * GG + KSPLIT * GG + 64 + ((2 * NBK + 4 + 3) & ~3);
     static constexpr size_t FIXED_BYTES = (size_t)FIXED * 4;
-    static constexpr int PER_POINT = 2 * G + 4;          // Ey, Ex (16-B aligned rows), u0, u1, window, pad
+    static constexpr int PER_POINT = 2 * G + 6;          // Ey, Ex (16-B aligned rows), u0, u1, window, key, x, y
 };
 
 struct Params {
@@ -270,6 +274,284 @@ __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter
     misc[1] = __int_as_float(WY);                            // for the wd pass
 }
 
+// sum over aligned groups of 4 lanes (quad xor-1, xor-2), every lane gets the sum
+__device__ __forceinline__ float sum4_dpp(float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, true));
+    return x;
+}
+
+// Sinkhorn-Knopp, bucketed form (LDS-resident crops whose K windows are <= 9 cells, i.e. reg = 10 and
+// cell pitch 8: exp underflows beyond 32 px).  Same iteration, same control flow and epsilons as
+// sinkhorn_crop / bregman_pytorch.py:102-126; only the summation order of the two products changes:
+//  * the points are stably sorted into (G/4)^2 home buckets (the 4x4 cell block of their window
+//    start); a window of <= 9 cells spans <= 3 blocks per axis, so K^T u of block (BY, BX) gathers
+//    only the points of home buckets (BY-2..BY) x (BX-2..BX): 3 contiguous ranges of the sorted order;
+//  * 8 adjacent lanes own a 4x4 block: they split its candidates, meet by DPP and form
+//    v = b / (K^T u + eps) for it (no LDS partials), so an iteration is two phases and two barriers:
+//    [K^T u, v] then [K v, u];
+//  * K v: 4 lanes per point, each lane <= 3 window rows read as three aligned 16-B chunks of v.
+// Returns false (nothing iterated) when a window is wider than 9 cells; the caller then runs
+// sinkhorn_crop.  On return the factors, u (u0), windows and point coordinates (spts) are sorted.
+template <int G>
+__device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
+                                const float* __restrict__ pts, float* Ey, float* Ex, float* u0, float* u1, int* win,
+                                int* key, float* spts, int* bk, const float* b, float* v0, float* v1, float* part,
+                                float* misc, int* iters_out, int* rolled_out, float* err_last_out,
+                                unsigned long long* pr)
+{
+    using C = Cfg<G>;
+    constexpr int GG = G * G, NB1 = C::NB1, NBK = C::NBK, HALO = C::HALO;
+    const int t = threadIdx.x;
+    unsigned long long tk = 0;
+    auto tick = [&](int k) {
+        if (pr && t == 0) { const unsigned long long c = clock64(); if (k >= 0) pr[k] += c - tk; tk = c; }
+    };
+    int* cnt = bk;                 // [NBK] bucket sizes
+    int* start = bk + NBK;         // [NBK + 1] bucket starts in the sorted order
+    int* tmpwin = reinterpret_cast<int*>(u1);
+    for (int k = t; k < NBK; k += NT) cnt[k] = 0;
+    __syncthreads();
+    // 1. windows (read off the computed factors, as sinkhorn_crop) and home buckets, original order
+    int wide = 0;
+    for (int i = t; i < n; i += NT) {
+        const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
+        int ylo = G, yhi = -1, xlo = G, xhi = -1;
+        for (int k = 0; k < G; ++k) {
+            const float c = cood(k, size, norm);
+            const float yd = (-2.0f * (y * c) + y * y) + c * c;
+            const float xd = (-2.0f * (x * c) + x * x) + c * c;
+            if (expf(yd / -reg) != 0.f) { ylo = min(ylo, k); yhi = k; }
+            if (expf(xd / -reg) != 0.f) { xlo = min(xlo, k); xhi = k; }
+        }
+        const int ylen = yhi >= ylo ? yhi - ylo + 1 : 0, xlen = xhi >= xlo ? xhi - xlo + 1 : 0;
+        wide |= (ylen > 9) | (xlen > 9);
+        const int kk = (ylen && xlen) ? (ylo / C::BS) * NB1 + (xlo / C::BS) : 0;
+        key[i] = kk;
+        tmpwin[i] = (ylen ? ylo : 0) | (ylen << 8) | ((xlen ? xlo : 0) << 16) | (xlen << 24);
+        atomicAdd(&cnt[kk], 1);
+    }
+    if (block_or(wide, reinterpret_cast<int*>(misc))) return false;
+    if (t == 0) {
+        int s = 0;
+        for (int k = 0; k < NBK; ++k) { start[k] = s; s += cnt[k]; }
+        start[NBK] = s;
+    }
+    __syncthreads();
+    // 2. stable scatter: slot = bucket start + rank among the earlier points of the same bucket
+    for (int i = t; i < n; i += NT) {
+        const int kk = key[i];
+        int r = 0;
+        for (int j = 0; j < i; ++j) r += key[j] == kk;
+        const int slot = start[kk] + r;
+        const float px = pts[2 * i], py = pts[2 * i + 1];
+        const float x = pcoord(px, size, norm), y = pcoord(py, size, norm);
+        for (int k = 0; k < G; ++k) {
+            const float c = cood(k, size, norm);
+            const float yd = (-2.0f * (y * c) + y * y) + c * c;
+            const float xd = (-2.0f * (x * c) + x * x) + c * c;
+            Ey[slot * G + k] = expf(yd / -reg);
+            Ex[slot * G + k] = expf(xd / -reg);
+        }
+        spts[2 * slot] = px;
+        spts[2 * slot + 1] = py;
+        win[slot] = tmpwin[i];
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += NT) u0[i] = 1.0f / (float)n;
+    for (int j = t; j < GG; j += NT) v0[j] = 1.0f / (float)GG;
+    const float a = 1.0f / (float)n;
+
+    // candidate ranges of block blk: home rows BY-HALO..BY, columns BX-HALO..BX (contiguous per row)
+    struct Ranges { int s[HALO + 1], pre[HALO + 2]; };
+    auto ranges = [&](int blk, Ranges& R) {
+        const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1;
+        R.pre[0] = 0;
+#pragma unroll
+        for (int d = 0; d <= HALO; ++d) {
+            const int hy = BY - HALO + d;
+            int s0 = 0, e0 = 0;
+            if (hy >= 0) { s0 = start[hy * NB1 + max(BX - HALO, 0)]; e0 = start[hy * NB1 + BX + 1]; }
+            R.s[d] = s0;
+            R.pre[d + 1] = R.pre[d] + (e0 - s0);
+        }
+    };
+    // 8 adjacent lanes per 4x4 block: lane kg takes candidates kg, kg+8, ... four at a time (all LDS
+    // reads before the FMAs); the 16 block sums meet by DPP and lane kg keeps cells 2kg, 2kg+1
+    constexpr int LPB = 8;
+    const int kg = t & (LPB - 1);
+    auto ktu_block = [&](int blk, const Ranges& R, const float* uu, float& k0, float& k1) {
+        const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1, by = BY * 4, bx = BX * 4;
+        float4 acc[4] = {};
+        const int nc = R.pre[HALO + 1];
+        for (int c0 = kg; c0 < nc; c0 += 4 * LPB) {
+            float ui[4];
+            float4 ey[4], ex[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = c0 + k * LPB;
+                int i = 0;
+#pragma unroll
+                for (int d = 0; d <= HALO; ++d)
+                    if (c >= R.pre[d] && c < R.pre[d + 1]) i = R.s[d] + c - R.pre[d];
+                ui[k] = c < nc ? uu[i] : 0.f;
+                ey[k] = *reinterpret_cast<const float4*>(&Ey[i * G + by]);
+                ex[k] = *reinterpret_cast<const float4*>(&Ex[i * G + bx]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float wy[4] = {ui[k] * ey[k].x, ui[k] * ey[k].y, ui[k] * ey[k].z, ui[k] * ey[k].w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    acc[r].x = fmaf(wy[r], ex[k].x, acc[r].x);
+                    acc[r].y = fmaf(wy[r], ex[k].y, acc[r].y);
+                    acc[r].z = fmaf(wy[r], ex[k].z, acc[r].z);
+                    acc[r].w = fmaf(wy[r], ex[k].w, acc[r].w);
+                }
+            }
+        }
+        // transposing butterfly over the 8 lanes (half-row mirror, then quad xor-2, xor-1): each stage
+        // keeps half of the cells and adds the partner's copy of them; lane kg ends with cells 2kg, 2kg+1
+        float c16[16];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            c16[4 * r] = acc[r].x; c16[4 * r + 1] = acc[r].y; c16[4 * r + 2] = acc[r].z; c16[4 * r + 3] = acc[r].w;
+        }
+        auto dpp = [](float x, auto ctl) {
+            return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x),
+                                                                      decltype(ctl)::value, 0xF, 0xF, true));
+        };
+        const bool b2 = kg & 4, b1 = kg & 2, b0 = kg & 1;
+        float c8[8], c4[4];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float send = b2 ? c16[k] : c16[k + 8];
+            c8[k] = (b2 ? c16[k + 8] : c16[k]) + dpp(send, std::integral_constant<int, 0x141>{});
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float send = b1 ? c8[k] : c8[k + 4];
+            c4[k] = (b1 ? c8[k + 4] : c8[k]) + dpp(send, std::integral_constant<int, 0x4E>{});
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const float send = b0 ? c4[k] : c4[k + 2];
+            const float keep = (b0 ? c4[k + 2] : c4[k]) + dpp(send, std::integral_constant<int, 0xB1>{});
+            if (k == 0) k0 = keep; else k1 = keep;
+        }
+    };
+    // cell index of lane kg's first cell (cells 2kg, 2kg+1: row 2kg/4, columns 2kg%4, +1)
+    auto cell0 = [&](int blk) {
+        const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1;
+        return (BY * 4 + (2 * kg) / 4) * G + BX * 4 + (2 * kg) % 4;
+    };
+    constexpr int BPP = NT / LPB;                             // blocks per pass
+    constexpr bool ONE = NBK <= BPP;                          // one block per 8-lane group (G = 28)
+    Ranges R0;
+    if (t / LPB < NBK) ranges(t / LPB, R0);
+
+    float* u = u0; float* un = u1;
+    float* v = v0; float* vn = v1;
+    int have_ktu = 0, it = 1, rolled = 0;
+    float err = 1.0f, err_last = -1.0f;
+    int* flag = reinterpret_cast<int*>(misc) + 16;
+    if (t < 2) flag[t] = 0;
+    __syncthreads();
+    const int q = t & 3;
+    int to_eval = eval_freq;
+    tick(-1);
+    while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
+        int* fl = flag + (it & 1);
+        // phase A: v = b / (K^T u + eps) (K^T u reused from the err pass)
+        int bad = 0;
+        for (int blk = t / LPB; blk < NBK; blk += BPP) {
+            Ranges R;
+            if (!ONE) ranges(blk, R); else R = R0;
+            const int j = cell0(blk);
+            float k0, k1;
+            if (have_ktu) { k0 = part[j]; k1 = part[j + 1]; }
+            else ktu_block(blk, R, u, k0, k1);
+            tick(1);                                          // diagnostics: "v" = K^T u gather time
+            const float v0n = b[j] / (k0 + M_EPS), v1n = b[j + 1] / (k1 + M_EPS);
+            vn[j] = v0n;
+            vn[j + 1] = v1n;
+            bad |= (int)!isfinite(v0n) | (int)!isfinite(v1n);
+        }
+        have_ktu = 0;
+        if (bad) *fl = 1;
+        __syncthreads();
+        if (t == 0) flag[(it + 1) & 1] = 0;
+        tick(0);
+        // phase B: u = a / (K v + eps)
+        for (int i0 = 0; i0 < n; i0 += NT / 4) {
+            const int i = i0 + (t >> 2);
+            float acc = 0.f;
+            if (i < n) {
+                const int w = win[i];
+                const int ylo = w & 255, ylen = (w >> 8) & 255, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
+                if (xlen) {
+                    const int x4 = min(xlo & ~3, G - 12);
+                    const float* exr = Ex + i * G + x4;
+                    const float4 e0 = *reinterpret_cast<const float4*>(exr);
+                    const float4 e1 = *reinterpret_cast<const float4*>(exr + 4);
+                    const float4 e2 = *reinterpret_cast<const float4*>(exr + 8);
+                    for (int r = q; r < ylen; r += 4) {
+                        const float* vr = vn + (ylo + r) * G + x4;
+                        const float4 a0 = *reinterpret_cast<const float4*>(vr);
+                        const float4 a1 = *reinterpret_cast<const float4*>(vr + 4);
+                        const float4 a2 = *reinterpret_cast<const float4*>(vr + 8);
+                        float sum = e0.x * a0.x;
+                        sum = fmaf(e0.y, a0.y, sum); sum = fmaf(e0.z, a0.z, sum); sum = fmaf(e0.w, a0.w, sum);
+                        sum = fmaf(e1.x, a1.x, sum); sum = fmaf(e1.y, a1.y, sum); sum = fmaf(e1.z, a1.z, sum);
+                        sum = fmaf(e1.w, a1.w, sum); sum = fmaf(e2.x, a2.x, sum); sum = fmaf(e2.y, a2.y, sum);
+                        sum = fmaf(e2.z, a2.z, sum); sum = fmaf(e2.w, a2.w, sum);
+                        acc = fmaf(Ey[i * G + ylo + r], sum, acc);
+                    }
+                }
+            }
+            acc = sum4_dpp(acc);
+            if (i < n && q == 0) {
+                const float val = a / (acc + M_EPS);
+                un[i] = val;
+                if (!isfinite(val)) *fl = 1;
+            }
+        }
+        __syncthreads();
+        tick(2);
+        if (*fl) { rolled = 1; break; }                       // keep (u, v): rollback, :111-115
+        { float* tu = u; u = un; un = tu; float* tv = v; v = vn; vn = tv; }
+        if (--to_eval == 0) {                                 // it % eval_freq == 0 (:117-126); K^T u kept
+            to_eval = eval_freq;
+            float e = 0.f;
+            for (int blk = t / LPB; blk < NBK; blk += BPP) {
+                Ranges R;
+                if (!ONE) ranges(blk, R); else R = R0;
+                const int j = cell0(blk);
+                float k0, k1;
+                ktu_block(blk, R, u, k0, k1);
+                part[j] = k0;
+                part[j + 1] = k1;
+                const float d0 = b[j] - k0 * v[j], d1 = b[j + 1] - k1 * v[j + 1];
+                e = fmaf(d0, d0, e);
+                e = fmaf(d1, d1, e);
+            }
+            err = block_sum(e, misc);
+            err_last = err;
+            have_ktu = 1;
+            tick(3);
+        }
+        ++it;
+    }
+    if (v != v0) { for (int j = t; j < GG; j += NT) v0[j] = v[j]; }
+    if (u != u0) { for (int i = t; i < n; i += NT) u0[i] = u[i]; }
+    __syncthreads();
+    *iters_out = rolled ? it : it - 1;
+    *rolled_out = rolled;
+    *err_last_out = err_last;
+    misc[1] = __int_as_float(9);                             // window rows bound for the wd pass
+    return true;
+}
+
 // Wasserstein distance sum(C * P) over the windows (dm_loss.py:77; reported, unused by training)
 template <int G, typename FP, typename IP>
 __device__ float transport_cost(int n, int size, int norm, const float* pts, FP Ey, FP Ex, FP u, IP win,
@@ -311,7 +593,8 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     float* v1 = v0 + GG;
     float* part = v1 + GG;      // K^T u partials [KSPLIT][GG]
     float* misc = part + C::KSPLIT * GG;
-    float* fac = misc + 64;     // LDS factors (if they fit)
+    int* bkt = reinterpret_cast<int*>(misc + 64);             // sorted-Sinkhorn bucket counts / starts
+    float* fac = misc + 64 + ((2 * C::NBK + 4 + 3) & ~3);     // LDS factors (if they fit)
 
     const int p0 = P.offsets[b], n = P.offsets[b + 1] - p0;
     if (P.prof && t == 0) { for (int k = 0; k < 16; ++k) P.prof[b * 16 + k] = 0; P.prof[b * 16 + 6] = clock64(); P.prof[b * 16 + 5] = n; }
@@ -389,11 +672,21 @@ __device__ void crop_body(const Params& P, int b, float* lds)
             const float* pts = P.points + 2 * (size_t)p0;
             // Two inlined copies so each sees one address space for the factors: LDS-resident
             // crops get ds_* accesses (a select between LDS and global would make them flat_*).
-            auto ot = [&](float* base) {
+            auto ot = [&](float* base, auto in_lds) {
                 float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
                 int* win = reinterpret_cast<int*>(u1 + n);
-                sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0, u1,
-                                 win, bb, v0, v1, part, misc, &iters, &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr);
+                int* key = win + n;
+                float* spts = reinterpret_cast<float*>(key + n);
+                bool sorted = false;
+                if constexpr (decltype(in_lds)::value)
+                    sorted = sinkhorn_sorted<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
+                                                Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc, &iters,
+                                                &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr);
+                if (!sorted)
+                    sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
+                                     u1, win, bb, v0, v1, part, misc, &iters, &rolled, &err_last,
+                                     P.prof ? P.prof + b * 16 : nullptr);
+                const float* cpts = sorted ? spts : pts;
                 if (P.prof && t == 0) P.prof[b * 16 + 8] = clock64();
                 const int WY = __float_as_int(misc[1]);
                 __syncthreads();
@@ -415,10 +708,10 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                     v1[j] = og;
                 }
                 ot_b = block_sum(ol, misc);
-                wd_b = transport_cost<G>(n, S, P.norm_cood, pts, Ey, Ex, u0, win, v0, WY, misc);
+                wd_b = transport_cost<G>(n, S, P.norm_cood, cpts, Ey, Ex, u0, win, v0, WY, misc);
             };
-            if (n <= P.lds_cap) ot(fac);
-            else ot(P.ws_factors + (size_t)C::PER_POINT * p0);
+            if (n <= P.lds_cap) ot(fac, std::true_type{});
+            else ot(P.ws_factors + (size_t)C::PER_POINT * p0, std::false_type{});
         } else {
             for (int j = t; j < GG; j += NT) v1[j] = 0.f;
             __syncthreads();
@@ -509,7 +802,7 @@ template <int G> int launch(const Params& P0, hipStream_t st)
 extern "C" size_t ebc_dace_workspace_bytes(int B, int total_points, int size, int reduction)
 {
     const int g = size / reduction;
-    return sizeof(float) * ((size_t)(2 * g + 4) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
+    return sizeof(float) * ((size_t)(2 * g + 6) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
 }
 
 extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,

@@ -14,6 +14,7 @@
 //   xT3    [3][C][Qs] T                kx-shifted transposed copies for the weight gradient:
 //                                      xT3[kx][c][G + q] = xpad[q + kx - 1][c] (0 outside)
 //   dzT    [N][Qs] T                   transposed padded dz (0 outside the interior)
+//   dw     [N][C][3][3] f32            weight gradient, nn.Conv2d layout
 // Every kernel is HBM-bound elementwise / transpose work (4-wide vector accesses).
 #include <algorithm>
 
@@ -402,6 +403,29 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__
     *reinterpret_cast<float4*>(dfeat + cell * C + c) = acc;
 }
 
+// conv weight [N][C][3][3] f32 (nn.Conv2d) -> forward operand wk [N][3][3][C] and flipped data-gradient
+// operand wf [C][3][3][N] (wf[c][t][o] = w[o][c][8 - t]) in the compute dtype; 32x32 (o, c) tiles in LDS
+template <class T>
+__global__ __launch_bounds__(256) void prep_weights_kernel(const float* __restrict__ w, T* __restrict__ wk,
+                                                           T* __restrict__ wf, int N, int C)
+{
+    __shared__ float sm[32][32 * 9 + 1];           // [o][c*9 + t]
+    const int o0 = blockIdx.x * 32, c0 = blockIdx.y * 32, t = threadIdx.x;
+    for (int e = t; e < 32 * 32 * 9; e += 256) {
+        const int ol = e / (32 * 9), r = e - ol * 32 * 9;
+        sm[ol][r] = (o0 + ol < N && c0 + r / 9 < C) ? w[((size_t)(o0 + ol) * C + c0) * 9 + r] : 0.f;
+    }
+    __syncthreads();
+    for (int e = t; e < 32 * 9 * 32; e += 256) {   // wk rows (o, tap): 32 contiguous c
+        const int cl = e & 31, r = e >> 5, ol = r / 9, tap = r - ol * 9;
+        if (o0 + ol < N && c0 + cl < C) wk[((size_t)(o0 + ol) * 9 + tap) * C + c0 + cl] = (T)sm[ol][cl * 9 + tap];
+    }
+    for (int e = t; e < 32 * 9 * 32; e += 256) {   // wf rows (c, tap): 32 contiguous o
+        const int ol = e & 31, r = e >> 5, cl = r / 9, tap = r - cl * 9;
+        if (o0 + ol < N && c0 + cl < C) wf[((size_t)(c0 + cl) * 9 + tap) * N + o0 + ol] = (T)sm[ol][cl * 9 + 8 - tap];
+    }
+}
+
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 template <class T>
@@ -594,6 +618,16 @@ extern "C" int ebc_dec_upsample_bwd(int dtype, const void* dx, const void* gy, c
     EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(upsample_bwd_kernel<T>, dim3(nblk(cells * (C / 4))), dim3(256), 0,
                                                (hipStream_t)stream, (const T*)dx, (const T*)gy, (const T*)mask_y,
                                                dfeat, B, h, w, h * up, w * up, C, up, 1.0f / (float)up));
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+extern "C" int ebc_dec_prep_weights(int dtype, const float* w, void* wk, void* wf, int N, int C, ebc_stream_t stream)
+{
+    if (!w || !wk || !wf || N <= 0 || C <= 0) return EBC_E_ARG;
+    const dim3 grid((unsigned)((N + 31) / 32), (unsigned)((C + 31) / 32));
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(prep_weights_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, w,
+                                               (T*)wk, (T*)wf, N, C));
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

@@ -42,8 +42,8 @@ struct GemmArgs {
     //    zero-padded NHWC image, K = 9 taps x cC (tap-major), k-tile kt reads the row shifted by
     //    tap (ky, kx): ((ky-1)*cWp + kx-1) pixels;  B = weights [N][3][3][cC].
     //  MODE 2 (weight gradient): A = dz^T [M][cQs], B = three kx-shifted copies x^T [3][cC][cQs] of
-    //    the padded image (x_kx^T[c][cG + q] = x[q + kx - 1][c]), row n = (ky, kx, c) starts at
-    //    (ky-1)*cWp; K runs over the interior image rows, kpi k-tiles per image.
+    //    the padded image (x_kx^T[c][cG + q] = x[q + kx - 1][c]), row n = (c, ky, kx) (the nn.Conv2d
+    //    weight layout) starts at (ky-1)*cWp; K runs over the interior image rows, kpi k-tiles per image.
     int cH = 0, cW = 0, cC = 0, cHp = 0, cWp = 0, kpi = 0;
     long cQs = 0, cG = 0;
     float* stats = nullptr;  // EPI_STATS: [ceil(M/BM)][2][N] per-tile column sums / sums of squares
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         } else {
             const int n = n0 + row - BM;
             if constexpr (MODE == 2) {
-                const int t = n / g.cC, cc = n - t * g.cC, ky = t / 3, kx = t - 3 * ky;
+                const int cc = n / 9, t = n - 9 * cc, ky = t / 3, kx = t - 3 * ky;   // nn.Conv2d [o][c][ky][kx]
                 base = Bw + (size_t)(kx * g.cC + cc) * g.cQs + g.cG + (long)(ky - 1) * g.cWp;
             } else {
                 base = Bw + (size_t)n * K;
@@ -562,8 +562,10 @@ int pick_cfg(int M, int N, int K, bool wide) {
     // kept for forced runs only.
     if (!wide) return 2;
     if (N % 192 == 0 && N % 256 != 0 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
-    // r01 sweep: MLP c_fc / GELU' (N = 3072, K = 768): 256x192 27.6 / 31.9 us vs 34.3 / 37.0 (128x64)
-    if (N % 192 == 0 && N >= 2048 && K <= 1024 && ntiles(M, N, 256, 192) >= 160) return 3;
+    // r01 sweep: MLP c_fc / GELU' (N = 3072, K = 768): 256x192 27.6 / 31.9 us vs 34.3 / 37.0 (128x64);
+    // QKV (N = 2304): 192x192 20.1 us vs 23.3 (256x192)
+    if (N % 192 == 0 && N >= 3072 && K <= 1024 && ntiles(M, N, 256, 192) >= 160) return 3;
+    if (N % 192 == 0 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
     // decoder 3x3 convs as implicit GEMM (M = B*784, K = 9*768): one wave of 256x192 tiles
     if (N % 192 == 0 && K >= 4096 && ntiles(M, N, 256, 192) >= 160) return 3;
     if (N % 96 == 0 && N < 2048 && K >= 2048) return 13;
@@ -655,13 +657,20 @@ int launch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st)
     if constexpr (E::BYTES == 2) {
         if (cfg == 3) return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2, 128, MODE>(g, st);
         if (cfg == 13) return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, MODE>(g, st);
+        if (cfg == 20) return launch_gemm<E, TO, EPI, 256, 256, 4, 4, 2, 64, MODE>(g, st);
+        if (cfg == 21) return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64, MODE>(g, st);
     }
     return EBC_E_UNSUPPORTED;
 }
 
+int forced_conv_cfg() { static const int v = env_int("EBC_CONV_CFG"); return v; }
 int conv_cfg(bool sixteen, int mode, int M, int N)
 {
     if (!sixteen) return 2;
+    if (const int f = forced_conv_cfg()) {
+        const TileCfg* c = find_cfg(f);
+        if (c && N % c->bn == 0 && (f == 2 || f == 3 || f == 13 || f == 20 || f == 21)) return f;
+    }
     if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;
     return N % 96 == 0 ? 13 : 2;
 }
@@ -679,10 +688,11 @@ template <class E>
 int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream_t st)
 {
     constexpr bool SIXTEEN = E::BYTES == 2;
-    constexpr int BK = 128 / E::BYTES;
     const int cfg = conv_cfg(SIXTEEN, mode, g.M, g.N);
+    const int BK = cfg >= 20 ? 32 : 128 / E::BYTES;           // 64-B K rows for the 4-stage rings
     const TileCfg* c = find_cfg(cfg);
     if (g.N % c->bn || g.K % BK) return EBC_E_UNSUPPORTED;
+    if (mode == 2) g.kpi *= (128 / E::BYTES) / BK;             // geometry counts 128-B k-tiles
     int splits = conv_splits(cfg, mode, g.M, g.N, g.K / BK);
     if (splits > 1) {
         const size_t tiles = (size_t)ntiles(g.M, g.N, c->bm, c->bn);
@@ -711,7 +721,7 @@ size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K)
     const bool sixteen = dtype != EBC_F32;
     const int cfg = conv_cfg(sixteen, mode, M, N);
     const TileCfg* c = find_cfg(cfg);
-    const int bk = sixteen ? 64 : 32;
+    const int bk = !sixteen ? 32 : (cfg >= 20 ? 32 : 64);
     size_t need = GEMM_CNT_BYTES;
     if (mode == 1) need += (size_t)((M + 127) / 128) * 2 * N * 4;     // EPI_STATS partials (BM >= 128)
     const int s = conv_splits(cfg, mode, M, N, K / bk);

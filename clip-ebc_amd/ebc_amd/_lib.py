@@ -61,6 +61,7 @@ SIGNATURES = {
     "ebc_bn_bwd_finalize": (_I, [_P, _D, _P, _P, _P, _P, _P, _I, _P]),
     "ebc_bn_bwd_apply": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_dec_transpose3": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_dec_prep_weights": (_I, [_I, _P, _P, _P, _I, _I, _P]),
     "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }
 

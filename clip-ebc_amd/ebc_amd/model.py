@@ -318,12 +318,16 @@ class _DecoderFn(torch.autograd.Function):
         f32 = dict(device=dev, dtype=torch.float32)
         xpad = torch.empty(Q, C, device=dev, dtype=cdtype)
         _lib.check(L.ebc_dec_upsample_pad(dt, _lib.ptr(feat), _lib.ptr(xpad), B, h, w, C, up, st), "upsample_pad")
-        outs = []
+        outs, wflip = [], []
         inp = xpad
         bns = (blk.bn1, blk.bn2)
         for i, (wt, gm, bt) in enumerate(((w1, g1, b1), (w2, g2, b2))):
             bn = bns[i]
-            wk = wt.detach().permute(0, 2, 3, 1).to(cdtype).contiguous()           # [N][3][3][C]
+            wk = torch.empty(N, 3, 3, C, device=dev, dtype=cdtype)                 # [N][3][3][C]
+            wf = torch.empty(C, 3, 3, N, device=dev, dtype=cdtype)                 # [C][3][3][N], flipped
+            _lib.check(L.ebc_dec_prep_weights(dt, _lib.ptr(wt.detach().float().contiguous()), _lib.ptr(wk),
+                                              _lib.ptr(wf), N, C, st), "ebc_dec_prep_weights")
+            wflip.append(wf)
             z = torch.empty(P, N, device=dev, dtype=cdtype)
             use_batch = training or not bn.track_running_stats
             colsum = torch.empty(2, N, device=dev, dtype=torch.float64) if use_batch else None
@@ -354,7 +358,7 @@ class _DecoderFn(torch.autograd.Function):
         y = torch.empty(B, H, W, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_bn_add_relu(dt, _lib.ptr(z2), _lib.ptr(scale2), _lib.ptr(shift2), _lib.ptr(feat), up,
                                      _lib.ptr(y), B, H, W, N, st), "ebc_bn_add_relu")
-        ctx.save_for_backward(xpad, hpad, y, w1, g1, w2, g2)
+        ctx.save_for_backward(xpad, hpad, y, wflip[0], g1, wflip[1], g2)
         ctx.outs = outs
         ctx.meta = (B, h, w, H, W, C, N, up, cdtype, Q, Qs, P)
         return y
@@ -362,7 +366,7 @@ class _DecoderFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         L = _lib.lib()
-        xpad, hpad, y, w1, g1, w2, g2 = ctx.saved_tensors
+        xpad, hpad, y, wf1, g1, wf2, g2 = ctx.saved_tensors
         B, h, w, H, W, C, N, up, cdtype, Q, Qs, P = ctx.meta
         dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream()
         gy = gy.to(cdtype).contiguous()
@@ -391,16 +395,15 @@ class _DecoderFn(torch.autograd.Function):
             src = hpad if i == 1 else xpad                # the conv's input image
             xT3 = torch.empty(3, C, Qs, device=dev, dtype=cdtype)
             _lib.check(L.ebc_dec_transpose3(dt, _lib.ptr(src), _lib.ptr(xT3), B, H, W, C, st), "ebc_dec_transpose3")
-            dw = torch.empty(N, 3, 3, C, **f32)
+            dw = torch.empty(N, C, 3, 3, **f32)
             _lib.check(L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws), ws.numel(),
                                            B, H, W, C, N, st), "ebc_conv3x3_wgrad")
             del xT3, dzT
-            wt = (w1, w2)[i]
-            wf = wt.detach().flip(2, 3).permute(1, 2, 3, 0).to(cdtype).contiguous()    # [C][3][3][N]
+            wf = (wf1, wf2)[i]                                                    # [C][3][3][N]
             dx = torch.empty(P, C, device=dev, dtype=cdtype)
             _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(dzpad), _lib.ptr(wf), _lib.ptr(dx), None, _lib.ptr(ws),
                                          ws.numel(), B, H, W, N, C, st), "ebc_conv3x3_fwd(dgrad)")
-            grads.append((dw.permute(0, 3, 1, 2).contiguous(), dg, db))
+            grads.append((dw, dg, db))
             dnext, mask = dx, None
         dfeat = torch.empty(B, h, w, C, **f32)
         _lib.check(L.ebc_dec_upsample_bwd(dt, _lib.ptr(dnext), _lib.ptr(gy), _lib.ptr(y), _lib.ptr(dfeat), B, h, w, C,

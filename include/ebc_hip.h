@@ -169,7 +169,7 @@ int ebc_tile_assemble(const float* preds, float* out, int Cp, int H, int W, int 
  * `colsum` / `sums` between the two calls that bracket them) and the whole backward.
  * Layouts (T = dtype): feat [B][h][w][C] f32; padded NHWC images [Q][C] T with Q = B*Hp*Wp;
  * z / dx / y [B*H*W][C] T; transposed images xT3 [3][C][Qs], dzT [N][Qs] T; conv weights
- * [N][3][3][C] T (forward) and [C][3][3][N] T (flipped, data gradient); dw [N][3][3][C] f32.
+ * [N][3][3][C] T (forward) and [C][3][3][N] T (flipped, data gradient); dw [N][C][3][3] f32 (nn.Conv2d layout).
  * ebc_dec_geometry writes {Hp, Wp, G, kpi, Q, Qs}.  The workspace's first 16 KiB must be zero before
  * the first call (split-K arrival counters, re-armed by every call); it is stream-owned scratch. */
 int ebc_dec_geometry(int dtype, int B, int H, int W, int C, long* out6);
@@ -181,7 +181,7 @@ int ebc_dec_upsample_pad(int dtype, const float* feat, void* xpad, int B, int h,
  * also the f64 column sums [2][N] (sum, sum of squares) for BatchNorm */
 int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, double* colsum, void* ws,
                     size_t wsb, int B, int H, int W, int C, int N, ebc_stream_t stream);
-/* dw[N][3][3][C] f32 = weight gradient from dzT and xT3 */
+/* dw[N][C][3][3] f32 = weight gradient from dzT and xT3 */
 int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, float* dw, void* ws, size_t wsb, int B, int H,
                       int W, int C, int N, ebc_stream_t stream);
 /* BatchNorm2d statistics -> mean, rstd, scale = gamma*rstd, shift = beta - mean*scale; running stats
@@ -208,6 +208,8 @@ int ebc_bn_bwd_apply(int dtype, const void* gy, const void* mask_y, const void* 
                      void* dzT, int B, int H, int W, int C, ebc_stream_t stream);
 /* xT3 = kx-shifted transposed copies of a padded NHWC image (weight-gradient operand) */
 int ebc_dec_transpose3(int dtype, const void* xpad, void* xT3, int B, int H, int W, int C, ebc_stream_t stream);
+/* conv weight [N][C][3][3] f32 -> wk [N][3][3][C] (forward) and wf [C][3][3][N] (flipped, data gradient) */
+int ebc_dec_prep_weights(int dtype, const float* w, void* wk, void* wf, int N, int C, ebc_stream_t stream);
 /* dfeat = bilinear_up^T(dx + gy * relu'(mask_y)), dx may be NULL */
 int ebc_dec_upsample_bwd(int dtype, const void* dx, const void* gy, const void* mask_y, float* dfeat, int B, int h,
                          int w, int C, int up, ebc_stream_t stream);

@@ -34,6 +34,13 @@ def main():
     print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=a.top,
                                                              max_name_column_width=60, max_shapes_column_width=70))
     print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=25, max_name_column_width=60))
+    # every copy / fill / cast with its shapes (where the glue time goes)
+    rows = [e for e in prof.key_averages(group_by_input_shape=True)
+            if any(k in e.key for k in ("copy", "fill", "zero", "_to_copy", "clone", "cat", "stack", "flip", "Memcpy", "Memset"))]
+    rows.sort(key=lambda e: -e.device_time_total)
+    print("\n== glue ops (per profiled window of %d steps)" % a.steps)
+    for e in rows[:40]:
+        print(f"{e.device_time_total:10.1f} us  n={e.count:4d}  {e.key[:40]:40s} {str(e.input_shapes)[:150]}")
 
 
 if __name__ == "__main__":
