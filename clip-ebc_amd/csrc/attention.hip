@@ -12,7 +12,9 @@
 // column reads); scores for 16 query rows x 256 keys live in registers, so no online softmax.
 // Operand orientation ("swapped" S^T = K Q^T) puts each query on one lane, so the probability
 // accumulators are directly the A operand of P.V with no LDS round trip (mfma.h).
-//   grid: B * H * ceil(L/128) workgroups of 8 waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
+//   grid: B * H * ceil(L/(16 NW)) workgroups of NW waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
+#include <cstdlib>
+
 #include "ebc_common.h"
 #include "mfma.h"
 
@@ -23,8 +25,8 @@ namespace {
 constexpr int HD = 64;          // head dim
 constexpr int LP = 256;         // padded sequence (>= L)
 constexpr int NKT = LP / 16;    // 16-row tiles
-constexpr int NWV = 8;          // waves per workgroup (16 queries / keys each)
-constexpr int QB = 16 * NWV;    // queries (fwd, dQ) or keys (dKV) per workgroup
+// NW waves per workgroup (16 queries / keys each): 16 for the ViT-B/16 sequence (one workgroup per
+// (crop, head), K/V or Q/dO staged once), 8 for short sequences
 constexpr float LOG2E = 1.4426950408889634f;
 
 template <class E> struct AttnCfg {
@@ -35,7 +37,7 @@ template <class E> struct AttnCfg {
     static constexpr size_t TILE_BYTES = (size_t)LP * LDR * EB;
 };
 
-template <class E>
+template <class E, int NWV>
 __device__ __forceinline__ void load_rows(typename E::T* dst, const typename E::T* src, int ld, int L)
 {
     // dst[s][0..63] = src[s*ld + 0..63] for s < L, zero for L <= s < LP
@@ -72,7 +74,7 @@ __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* bas
 }
 
 // ------------------------------------------------------------------------------ forward
-template <class E>
+template <class E, int NWV>
 __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T* __restrict__ qkv, typename E::T* __restrict__ out,
                                                        float* __restrict__ lse, int B, int L, int H, float scale)
 {
@@ -81,13 +83,14 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    constexpr int QB = 16 * NWV;
     const int nqb = (L + QB - 1) / QB;
     const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
-    load_rows<E>(Ks, base + D, D3, L);
-    load_rows<E>(Vs, base + 2 * D, D3, L);
+    load_rows<E, NWV>(Ks, base + D, D3, L);
+    load_rows<E, NWV>(Vs, base + 2 * D, D3, L);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
     const int q0 = qb * QB + w * 16;
@@ -97,30 +100,45 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     for (int ks = 0; ks < 2; ++ks) qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qme < L);
     __syncthreads();
 
+    if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
+    // key tiles past L are skipped; only the ragged last tile is masked; the softmax scale is folded
+    // into the exp2 argument: p = 2^(s*c - max*c), c = scale*log2(e)
+    const int nkt = (L + 15) >> 4;
+    const bool ragged = (L & 15) != 0;
+    const float c2 = scale * LOG2E;
     f32x4 s[NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
         s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (kt < nkt) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) s[kt] = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], s[kt]);
+            for (int ks = 0; ks < 2; ++ks) s[kt] = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], s[kt]);
+        }
     }
     // s[kt][i] = S[q = qme][key = 16 kt + 4 fg + i]
     float mx = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NKT; ++kt) {
+        if (kt < nkt) {
+            if (ragged && kt == nkt - 1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int key = 16 * kt + 4 * fg + i;
-            s[kt][i] = key < L ? s[kt][i] * scale : -INFINITY;
-            mx = fmaxf(mx, s[kt][i]);
+                for (int i = 0; i < 4; ++i)
+                    if (16 * kt + 4 * fg + i >= L) s[kt][i] = -INFINITY;
+            }
+            mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
         }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mc = mx * c2;
     float sum = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NKT; ++kt) {
+        if (kt < nkt) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { s[kt][i] = __builtin_amdgcn_exp2f((s[kt][i] - mx) * LOG2E); sum += s[kt][i]; }
+            for (int i = 0; i < 4; ++i) { s[kt][i] = __builtin_amdgcn_exp2f(fmaf(s[kt][i], c2, -mc)); sum += s[kt][i]; }
+        }
+    }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
 
@@ -129,6 +147,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int st = 0; st < NKT / 2; ++st) {
+        if (2 * st >= nkt) continue;
         const float pv[8] = {s[2 * st][0], s[2 * st][1], s[2 * st][2], s[2 * st][3],
                              s[2 * st + 1][0], s[2 * st + 1][1], s[2 * st + 1][2], s[2 * st + 1][3]};
         const typename E::Frag pf = pack8<E>(pv);
@@ -148,11 +167,11 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
             for (int dt = 0; dt < HD / 16; ++dt) orow[16 * dt + fr] = E::from(o[dt][i] * iv);
         }
     }
-    if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx + logf(sum);
+    if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx * scale + logf(sum);   // natural-log units of the scaled scores
 }
 
 // ------------------------------------------------------------------------------ backward dQ
-template <class E>
+template <class E, int NWV>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                                           typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
@@ -162,13 +181,14 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    constexpr int QB = 16 * NWV;
     const int nqb = (L + QB - 1) / QB;
     const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
-    load_rows<E>(Ks, base + D, D3, L);
-    load_rows<E>(Vs, base + 2 * D, D3, L);
+    load_rows<E, NWV>(Ks, base + D, D3, L);
+    load_rows<E, NWV>(Vs, base + 2 * D, D3, L);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
     const int q0 = qb * QB + w * 16;
@@ -185,15 +205,25 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
     const float dq = qv ? delta[((size_t)b * H + h) * L + qme] : 0.f;
     __syncthreads();
 
+    if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
+    const int nkt = (L + 15) >> 4;
+    const bool ragged = (L & 15) != 0;
+    const float c2 = scale * LOG2E, lq2 = lq * LOG2E;          // p = 2^(s*c - lse*log2 e)
     f32x4 dq_acc[HD / 16];
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int st = 0; st < NKT / 2; ++st) {
+        if (2 * st >= nkt) continue;
         float ds[8];
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int kt = 2 * st + hf;
+            if (kt >= nkt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ds[4 * hf + i] = 0.f;
+                continue;
+            }
             f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
@@ -202,8 +232,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int key = 16 * kt + 4 * fg + i;
-                const float p = key < L ? __builtin_amdgcn_exp2f((sv[i] * scale - lq) * LOG2E) : 0.f;
+                float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq2));
+                if (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i >= L) p = 0.f;
                 ds[4 * hf + i] = p * (pv[i] - dq);
             }
         }
@@ -223,7 +253,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
 }
 
 // ------------------------------------------------------------------------------ backward dK, dV
-template <class E>
+template <class E, int NWV>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                            const float* __restrict__ lse, const float* __restrict__ delta,
                                                            typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
@@ -235,15 +265,16 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
     T* Ds = reinterpret_cast<T*>(smem + C::TILE_BYTES);
     float* ls = reinterpret_cast<float*>(smem + 2 * C::TILE_BYTES);
     float* dl = ls + LP;
+    constexpr int QB = 16 * NWV;
     const int nkb = (L + QB - 1) / QB;
     const int bh = blockIdx.x / nkb, kb = blockIdx.x % nkb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
-    load_rows<E>(Qs, base, D3, L);
-    load_rows<E>(Ds, dout + (size_t)b * L * D + h * HD, D, L);
-    for (int q = threadIdx.x; q < LP; q += blockDim.x) {
-        ls[q] = q < L ? lse[((size_t)b * H + h) * L + q] : INFINITY;
+    load_rows<E, NWV>(Qs, base, D3, L);
+    load_rows<E, NWV>(Ds, dout + (size_t)b * L * D + h * HD, D, L);
+    for (int q = threadIdx.x; q < LP; q += blockDim.x) {              // lse pre-scaled by log2(e)
+        ls[q] = q < L ? lse[((size_t)b * H + h) * L + q] * LOG2E : INFINITY;
         dl[q] = q < L ? delta[((size_t)b * H + h) * L + q] : 0.f;
     }
 
@@ -259,11 +290,15 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
     }
     __syncthreads();
 
+    if (k0 >= L) return;                                       // no live key in this wave (no barrier follows)
+    const int nqt = (L + 15) >> 4;                             // query tiles past L: lse = +inf, p = 0
+    const float c2 = scale * LOG2E;
     f32x4 dk[HD / 16], dv[HD / 16];
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
 #pragma unroll 2
     for (int st = 0; st < NKT / 2; ++st) {
+        if (2 * st >= nqt) break;
         float pp[8], ds[8];
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
@@ -279,7 +314,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
             const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float p = __builtin_amdgcn_exp2f((sv[i] * scale - lq[i]) * LOG2E);   // lse = +inf (padding) -> 0
+                const float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq[i]));   // lse = +inf (padding) -> 0
                 pp[4 * hf + i] = p;
                 ds[4 * hf + i] = p * (pv[i] - dq[i]);
             }
@@ -305,41 +340,57 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
     }
 }
 
-template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+int attn_waves(int L) {
+    static const int forced = getenv("EBC_ATTN_NW") ? atoi(getenv("EBC_ATTN_NW")) : 0;
+    if (forced == 8 || forced == 16) return forced;
+    return L > 128 ? 16 : 8;
+}
+
+template <class E, int NW> int attn_fwd_nw(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
 {
     using C = AttnCfg<E>;
     const size_t lds = 2 * C::TILE_BYTES;
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)attn_fwd_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
+        if (hipFuncSetAttribute((const void*)attn_fwd_kernel<E, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
         attr = true;
     }
-    const int grid = B * H * ((L + QB - 1) / QB);
-    hipLaunchKernelGGL(attn_fwd_kernel<E>, dim3(grid), dim3(64 * NWV), lds, st, (const typename E::T*)qkv,
+    const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
+    hipLaunchKernelGGL((attn_fwd_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
                        (typename E::T*)out, lse, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
+template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+{
+    return attn_waves(L) == 16 ? attn_fwd_nw<E, 16>(qkv, out, lse, B, L, H, st) : attn_fwd_nw<E, 8>(qkv, out, lse, B, L, H, st);
+}
 
-template <class E> int attn_bwd_t(const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
-                                  int B, int L, int H, hipStream_t st)
+template <class E, int NW> int attn_bwd_nw(const void* qkv, const void* dout, const float* lse, const float* delta,
+                                           void* dqkv, int B, int L, int H, hipStream_t st)
 {
     using C = AttnCfg<E>;
     const size_t lds_dq = 2 * C::TILE_BYTES, lds_kv = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dq) != hipSuccess) return EBC_E_LAUNCH;
-        if (hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv) != hipSuccess) return EBC_E_LAUNCH;
+        if (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<E, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dq) != hipSuccess) return EBC_E_LAUNCH;
+        if (hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<E, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv) != hipSuccess) return EBC_E_LAUNCH;
         attr = true;
     }
-    const int grid = B * H * ((L + QB - 1) / QB);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<E>, dim3(grid), dim3(64 * NWV), lds_dq, st, (const typename E::T*)qkv,
+    const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds_dq, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<E>, dim3(grid), dim3(64 * NWV), lds_kv, st, (const typename E::T*)qkv,
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds_kv, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
+}
+template <class E> int attn_bwd_t(const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
+                                  int B, int L, int H, hipStream_t st)
+{
+    return attn_waves(L) == 16 ? attn_bwd_nw<E, 16>(qkv, dout, lse, delta, dqkv, B, L, H, st)
+                               : attn_bwd_nw<E, 8>(qkv, dout, lse, delta, dqkv, B, L, H, st);
 }
 
 }  // namespace
