@@ -173,8 +173,9 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
 // ------------------------------------------------------------------------------ backward dQ
 template <class E, int NWV>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
-                                                          const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
+                                                          const typename E::T* __restrict__ out, const float* __restrict__ lse,
+                                                          float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
+                                                          int L, int H, float scale)
 {
     using T = typename E::T;
     using C = AttnCfg<E>;
@@ -202,7 +203,22 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
         df[ks] = gload8<E>(drow + 32 * ks + 8 * fg, qv);
     }
     const float lq = qv ? lse[((size_t)b * H + h) * L + qme] : INFINITY;
-    const float dq = qv ? delta[((size_t)b * H + h) * L + qme] : 0.f;
+    // delta = rowsum(dO * O) (FA2 D_i), computed here and published for the dK/dV kernel
+    float dq;
+    {
+        const T* orow = out + ((size_t)b * L + qme) * D + h * HD;
+        float dd = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const typename E::Frag of = gload8<E>(orow + 32 * ks + 8 * fg, qv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dd = fmaf((float)df[ks][j], (float)of[j], dd);
+        }
+        dd += __shfl_xor(dd, 16, 64);
+        dd += __shfl_xor(dd, 32, 64);
+        dq = qv ? dd : 0.f;
+        if (fg == 0 && qv) delta[((size_t)b * H + h) * L + qme] = dd;
+    }
     __syncthreads();
 
     if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
@@ -366,8 +382,8 @@ template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B,
     return attn_waves(L) == 16 ? attn_fwd_nw<E, 16>(qkv, out, lse, B, L, H, st) : attn_fwd_nw<E, 8>(qkv, out, lse, B, L, H, st);
 }
 
-template <class E, int NW> int attn_bwd_nw(const void* qkv, const void* dout, const float* lse, const float* delta,
-                                           void* dqkv, int B, int L, int H, hipStream_t st)
+template <class E, int NW> int attn_bwd_nw(const void* qkv, const void* dout, const void* out, const float* lse,
+                                           float* delta, void* dqkv, int B, int L, int H, hipStream_t st)
 {
     using C = AttnCfg<E>;
     const size_t lds_dq = 2 * C::TILE_BYTES, lds_kv = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
@@ -379,18 +395,19 @@ template <class E, int NW> int attn_bwd_nw(const void* qkv, const void* dout, co
     }
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
     hipLaunchKernelGGL((attn_bwd_dq_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds_dq, st, (const typename E::T*)qkv,
-                       (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
+                       (const typename E::T*)dout, (const typename E::T*)out, lse, delta, (typename E::T*)dqkv, B, L, H,
+                       0.125f);
     EBC_CHECK_LAUNCH();
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds_kv, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
-template <class E> int attn_bwd_t(const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
-                                  int B, int L, int H, hipStream_t st)
+template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
+                                  void* dqkv, int B, int L, int H, hipStream_t st)
 {
-    return attn_waves(L) == 16 ? attn_bwd_nw<E, 16>(qkv, dout, lse, delta, dqkv, B, L, H, st)
-                               : attn_bwd_nw<E, 8>(qkv, dout, lse, delta, dqkv, B, L, H, st);
+    return attn_waves(L) == 16 ? attn_bwd_nw<E, 16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st)
+                               : attn_bwd_nw<E, 8>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
 }
 
 }  // namespace
@@ -406,14 +423,14 @@ int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int 
     }
     return EBC_E_ARG;
 }
-int attention_bwd(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
-                  int B, int L, int H, hipStream_t st)
+int attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
+                  void* dqkv, int B, int L, int H, hipStream_t st)
 {
     if (L <= 0 || L > LP || B <= 0 || H <= 0) return EBC_E_UNSUPPORTED;
     switch (dtype) {
-        case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, lse, delta, dqkv, B, L, H, st);
-        case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, lse, delta, dqkv, B, L, H, st);
-        case EBC_BF16: return attn_bwd_t<EBF16>(qkv, dout, lse, delta, dqkv, B, L, H, st);
+        case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+        case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+        case EBC_BF16: return attn_bwd_t<EBF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
     }
     return EBC_E_ARG;
 }

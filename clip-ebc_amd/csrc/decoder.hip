@@ -346,12 +346,18 @@ __global__ __launch_bounds__(256) void transpose3_kernel(const T* __restrict__ x
     const int t = threadIdx.x;
     const long j0 = (long)blockIdx.x * TQ;
     const int c0 = blockIdx.y * TC;
-    for (int e = t; e < (TQ + 2) * (TC / 4); e += 256) {
-        const int ql = e / (TC / 4), cl = (e % (TC / 4)) * 4;
+    constexpr int NE = (TQ + 2) * (TC / 4), PER = (NE + 255) / 256;
+    float4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {                // all loads in flight before the LDS writes
+        const int e = t + 256 * k, ql = e / (TC / 4), cl = (e % (TC / 4)) * 4;
         const long q = j0 - g.G + ql - 1;
-        float4 v = f4(0.f);
-        if (q >= 0 && q < g.Q) v = ld4(xpad + q * g.C + c0 + cl);
-        sm[ql][cl] = v.x; sm[ql][cl + 1] = v.y; sm[ql][cl + 2] = v.z; sm[ql][cl + 3] = v.w;
+        v[k] = (e < NE && q >= 0 && q < g.Q) ? ld4(xpad + q * g.C + c0 + cl) : f4(0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int e = t + 256 * k, ql = e / (TC / 4), cl = (e % (TC / 4)) * 4;
+        if (e < NE) { sm[ql][cl] = v[k].x; sm[ql][cl + 1] = v[k].y; sm[ql][cl + 2] = v[k].z; sm[ql][cl + 3] = v[k].w; }
     }
     __syncthreads();
     const int cr = t >> 2, jl = (t & 3) * 16;
@@ -367,39 +373,46 @@ __global__ __launch_bounds__(256) void transpose3_kernel(const T* __restrict__ x
 }
 
 // dfeat = bilinear^T (dx + gy * relu'(y)): the residual branch and conv1's input gradient both
-// flow back through the x2 upsample (gather form: each input cell sums its output taps)
-template <class T>
+// flow back through the x`UP` upsample (gather form: input cell i collects output rows/columns
+// UP*(i-1) .. UP*(i+1), 2*UP+1 candidates with zero weight where a tap misses i; all loads issued
+// without data-dependent branches)
+template <class T, int UP>
 __global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__ dx, const T* __restrict__ gy,
                                                            const T* __restrict__ my, float* __restrict__ dfeat, int B,
-                                                           int h, int w, int H, int W, int C, int up, float scale)
+                                                           int h, int w, int H, int W, int C)
 {
+    constexpr int NCAND = 2 * UP + 1;
+    constexpr float scale = 1.0f / (float)UP;
     const int C4 = C / 4;
     const long e = (long)blockIdx.x * 256 + threadIdx.x;
     if (e >= (long)B * h * w * C4) return;
     const long cell = e / C4;
     const int c = (int)(e - cell * C4) * 4;
     const int b = (int)(cell / (h * w)), r = (int)(cell - (long)b * h * w), i = r / w, j = r - i * w;
+    float wy[NCAND], wx[NCAND];
+    int oy[NCAND], ox[NCAND];
+#pragma unroll
+    for (int k = 0; k < NCAND; ++k) {
+        const int y = UP * (i - 1) + k, x = UP * (j - 1) + k;
+        oy[k] = min(max(y, 0), H - 1);
+        ox[k] = min(max(x, 0), W - 1);
+        const Taps ty = taps(oy[k], h, scale), tx = taps(ox[k], w, scale);
+        wy[k] = (y >= 0 && y < H) ? (ty.i0 == i ? ty.l0 : 0.f) + (ty.i1 == i ? ty.l1 : 0.f) : 0.f;
+        wx[k] = (x >= 0 && x < W) ? (tx.i0 == j ? tx.l0 : 0.f) + (tx.i1 == j ? tx.l1 : 0.f) : 0.f;
+    }
     float4 acc = f4(0.f);
-    const int oy0 = std::max(0, i * up - up), oy1 = std::min(H - 1, i * up + 2 * up);
-    const int ox0 = std::max(0, j * up - up), ox1 = std::min(W - 1, j * up + 2 * up);
-    for (int oy = oy0; oy <= oy1; ++oy) {
-        const Taps ty = taps(oy, h, scale);
-        const float wy = (ty.i0 == i ? ty.l0 : 0.f) + (ty.i1 == i ? ty.l1 : 0.f);
-        if (wy == 0.f) continue;
-        for (int ox = ox0; ox <= ox1; ++ox) {
-            const Taps tx = taps(ox, w, scale);
-            const float wx = (tx.i0 == j ? tx.l0 : 0.f) + (tx.i1 == j ? tx.l1 : 0.f);
-            if (wx == 0.f) continue;
-            const long off = (((long)b * H + oy) * W + ox) * C + c;
+#pragma unroll
+    for (int a = 0; a < NCAND; ++a)
+#pragma unroll
+        for (int k = 0; k < NCAND; ++k) {
+            const long off = (((long)b * H + oy[a]) * W + ox[k]) * C + c;
             float4 v = masked_grad<T>(gy, my, nullptr, nullptr, nullptr, off, c);
             if (dx) {
                 const float4 d = ld4(dx + off);
                 v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
             }
-            const float wt = wy * wx;
-            acc = fma4(f4(wt), v, acc);
+            acc = fma4(f4(wy[a] * wx[k]), v, acc);
         }
-    }
     *reinterpret_cast<float4*>(dfeat + cell * C + c) = acc;
 }
 
@@ -411,9 +424,17 @@ __global__ __launch_bounds__(256) void prep_weights_kernel(const float* __restri
 {
     __shared__ float sm[32][32 * 9 + 1];           // [o][c*9 + t]
     const int o0 = blockIdx.x * 32, c0 = blockIdx.y * 32, t = threadIdx.x;
-    for (int e = t; e < 32 * 32 * 9; e += 256) {
-        const int ol = e / (32 * 9), r = e - ol * 32 * 9;
-        sm[ol][r] = (o0 + ol < N && c0 + r / 9 < C) ? w[((size_t)(o0 + ol) * C + c0) * 9 + r] : 0.f;
+    constexpr int PER = 32 * 32 * 9 / 256;         // 36 loads per thread, all issued before the LDS writes
+    float v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int e = t + 256 * k, ol = e / (32 * 9), r = e - ol * 32 * 9;
+        v[k] = (o0 + ol < N && c0 + r / 9 < C) ? w[((size_t)(o0 + ol) * C + c0) * 9 + r] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int e = t + 256 * k, ol = e / (32 * 9), r = e - ol * 32 * 9;
+        sm[ol][r] = v[k];
     }
     __syncthreads();
     for (int e = t; e < 32 * 9 * 32; e += 256) {   // wk rows (o, tap): 32 contiguous c
@@ -615,9 +636,18 @@ extern "C" int ebc_dec_upsample_bwd(int dtype, const void* dx, const void* gy, c
 {
     if (!gy || !mask_y || !dfeat || up < 1 || C % 4) return EBC_E_ARG;
     const long cells = (long)B * h * w;
-    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(upsample_bwd_kernel<T>, dim3(nblk(cells * (C / 4))), dim3(256), 0,
-                                               (hipStream_t)stream, (const T*)dx, (const T*)gy, (const T*)mask_y,
-                                               dfeat, B, h, w, h * up, w * up, C, up, 1.0f / (float)up));
+    if (up != 1 && up != 2) return EBC_E_UNSUPPORTED;
+    const unsigned grid = nblk(cells * (C / 4));
+    const hipStream_t st = (hipStream_t)stream;
+    if (up == 2) {
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 2>), dim3(grid), dim3(256), 0, st,
+                                                   (const T*)dx, (const T*)gy, (const T*)mask_y, dfeat, B, h, w, 2 * h,
+                                                   2 * w, C));
+    } else {
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 1>), dim3(grid), dim3(256), 0, st,
+                                                   (const T*)dx, (const T*)gy, (const T*)mask_y, dfeat, B, h, w, h, w,
+                                                   C));
+    }
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

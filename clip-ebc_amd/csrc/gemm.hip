@@ -165,8 +165,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     constexpr int STAGE = ROWS * ROWB;           // bytes
     constexpr int RPI = 1024 / ROWB;             // slab rows per LDS-DMA wave-instruction (1 KiB)
     constexpr int CPR = ROWB / 16;               // 16-B chunks per row
-    constexpr int NLD = ROWS / (RPI * NW);       // glds wave-instructions per wave per stage
-    static_assert(ROWS % (RPI * NW) == 0 && WM % 16 == 0 && WN % 16 == 0, "tiling");
+    // glds wave-instructions per wave per stage: NLDF full 1-KiB pieces (16-B lanes), plus, when the
+    // rows do not divide, NT4 256-B pieces (4-B lanes; there is no 8-B LDS-DMA) per wave, e.g. 256x192
+    // tiles of 64-B rows: 3 x 1 KiB + 2 x 256 B
+    constexpr int NLDF = ROWS / (RPI * NW);
+    constexpr int REMR = ROWS - NLDF * RPI * NW;
+    constexpr int R4 = 256 / ROWB;               // rows per 256-B piece
+    constexpr int NT4 = REMR / (NW * R4);
+    constexpr bool TAIL = REMR != 0;
+    constexpr int NLD = NLDF + NT4;
+    static_assert(REMR == NT4 * NW * R4, "tail pieces");
+    static_assert(WM % 16 == 0 && WN % 16 == 0, "tiling");
     static_assert(BK % 32 == 0, "k32 MFMA steps");
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -187,8 +196,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     bool isa[NLD];
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-        const int row = (wave * NLD + i) * RPI + lane / CPR;
-        const int slot = lane % CPR;
+        const bool tail = TAIL && i >= NLDF;
+        // full pieces: rows (wave*NLDF + i)*RPI + lane/CPR; tail piece j: 4-B lanes, rows
+        // NLDF*RPI*NW + (wave*NT4 + j)*R4 + lane/(4*CPR)
+        const int row = tail ? NLDF * RPI * NW + (wave * NT4 + (i - NLDF)) * R4 + lane / (4 * CPR)
+                             : (wave * NLDF + i) * RPI + lane / CPR;
+        const int slot = tail ? (lane % (4 * CPR)) / 4 : lane % CPR;
         const int c = slot ^ swz_row<ROWB>(row);
         const T* base;
         isa[i] = row < BM;
@@ -213,7 +226,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
                 base = Bw + (size_t)n * K;
             }
         }
-        src[i] = base + c * (16 / EB);
+        src[i] = base + c * (16 / EB) + (tail ? (lane & 3) * (4 / EB) : 0);
     }
     auto stage = [&](int buf, int kt) {
 #if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 2)
@@ -234,10 +247,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         }
         char* dst = smem + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < NLD; ++i) {
+        for (int i = 0; i < NLDF; ++i) {
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src[i] + (isa[i] ? oa : ob)),
-                EBC_LDS(dst + (wave * NLD + i) * 1024), 16, 0, 0);
+                EBC_LDS(dst + (wave * NLDF + i) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NT4; ++j) {
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(src[NLDF + j] + (isa[NLDF + j] ? oa : ob)),
+                EBC_LDS(dst + NLDF * NW * 1024 + (wave * NT4 + j) * 256), 4, 0, 0);
         }
     };
 
@@ -528,7 +547,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 //   7: 256x256/8w   (2-stage rings of 128-B K rows)
 //   8: 128x64 S3   9: 128x128 S3   10: 256x128/8w S3   11: 192x128/8w S3   12: 128x64 S4   13: 128x96 S3
 //   20: 256x256/8w  21: 256x128/8w  22: 128x256/8w  24: 128x128/4w   (4-stage rings
-//       of 64-B K rows, 16-bit only)
+//       of 64-B K rows, 16-bit only; r01: a 256x192 4-stage ring measured 10-15 % slower than
+//       cfg 3's 2-stage 128-B ring on the decoder convs and the MLP, so no such config is built)
 // The L2 -> LDS fill rate per CU (~70 GB/s, MI355X_MICROARCH.md "gather into LDS") bounds a tile at
 // BM*BN/(BM+BN) flop per byte, so the default takes the 256-wide tiles and splits K where the
 // output has too few tiles to fill the 256 CUs.

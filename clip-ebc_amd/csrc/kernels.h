@@ -42,8 +42,9 @@ int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const 
 int attn_delta(int dtype, const void* dO, const void* O, float* delta, int B, int L, int H, hipStream_t st);
 int cast_f32(int dtype, const float* in, void* out, size_t n, hipStream_t st);
 int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st);
-int attention_bwd(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta, void* dqkv,
-                  int B, int L, int H, hipStream_t st);
+// delta (FA2 D_i = rowsum(dO * O)) is computed by the dQ kernel and written to `delta` [B,H,L]
+int attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
+                  void* dqkv, int B, int L, int H, hipStream_t st);
 }  // namespace ebc
 
 #define EBC_TRY(x)                  \

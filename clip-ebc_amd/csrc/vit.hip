@@ -203,8 +203,7 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         { float* t = dX; dX = dXo; dXo = t; }
         // attention half: dO = dX1 . W_out;  dQKV = attn'(...);  dH = dQKV . W_qkv;  dX = dX1 + LN1'(dH)
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dXt, p.wt_out, lay.dO, nullptr, M, WIDTH, WIDTH));
-        EBC_TRY(ebc::attn_delta(dtype, lay.dO, s.O, lay.delta, B, L, HEADS, st));
-        EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st));
+        EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st));
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dQKV, p.wt_qkv, lay.dH, nullptr, M, WIDTH, QKVW));
         EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, lay.X[l], 0, 0, 0, s.m1, s.r1, p.ln1_g, dX, dXo, lay.dXt, M, WIDTH, st));
         { float* t = dX; dX = dXo; dXo = t; }
@@ -240,8 +239,7 @@ extern "C" int ebc_attention_fwd(int dtype, const void* qkv, void* out, float* l
 extern "C" int ebc_attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse,
                                  float* delta_ws, void* dqkv, int B, int L, int H, ebc_stream_t stream)
 {
-    EBC_TRY(ebc::attn_delta(dtype, dout, out, delta_ws, B, L, H, (hipStream_t)stream));
-    return ebc::attention_bwd(dtype, qkv, dout, lse, delta_ws, dqkv, B, L, H, (hipStream_t)stream);
+    return ebc::attention_bwd(dtype, qkv, dout, out, lse, delta_ws, dqkv, B, L, H, (hipStream_t)stream);
 }
 extern "C" int ebc_head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
                             float* logits, float* expo, int P, int HW, int NB, ebc_stream_t stream)
