@@ -123,8 +123,8 @@ def setup(args, rank, world, local, device):
                       vpt_drop=0.0, deep_vpt=True).to(device)
     model.train()
     if world > 1:
-        model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], output_device=local)
+        from ebc_amd.distributed import wrap_ddp       # SyncBatchNorm + DDP, as trainer.py:147
+        model = wrap_ddp(model, device.index)
     loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=224).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
     try:
@@ -158,10 +158,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EBC_BENCH_ONE_DEVICE=1 EBC_BENCH_BACKEND=gloo: rehearse the N-rank path with every rank on cuda:0
+    # (a 1-GPU box); the measured numbers of such a run are not a scaling result
+    dev_index = 0 if os.environ.get("EBC_BENCH_ONE_DEVICE") == "1" else local
+    backend = os.environ.get("EBC_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
-    device = torch.device(f"cuda:{local}")
+        dist.init_process_group(backend, device_id=torch.device(f"cuda:{dev_index}") if backend == "nccl" else None)
+    torch.cuda.set_device(dev_index)
+    device = torch.device(f"cuda:{dev_index}")
     step = setup(args, rank, world, local, device)
     B = args.crops_per_gpu
 

@@ -372,16 +372,14 @@ __global__ __launch_bounds__(256) void transpose3_kernel(const T* __restrict__ x
     }
 }
 
-// dfeat = bilinear^T (dx + gy * relu'(y)): the residual branch and conv1's input gradient both
-// flow back through the x`UP` upsample (gather form: input cell i collects output rows/columns
-// UP*(i-1) .. UP*(i+1), 2*UP+1 candidates with zero weight where a tap misses i; all loads issued
-// without data-dependent branches)
+// dfeat = bilinear^T (g), g = conv1's input gradient + the residual branch's (already summed by the
+// dgrad GEMM epilogue): input cell i collects output rows/columns UP*i - UP/2 .. +2*UP-1 (zero weight
+// where a tap misses i); all loads issued without data-dependent branches
 template <class T, int UP>
-__global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__ dx, const T* __restrict__ gy,
-                                                           const T* __restrict__ my, float* __restrict__ dfeat, int B,
+__global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__ g, float* __restrict__ dfeat, int B,
                                                            int h, int w, int H, int W, int C)
 {
-    constexpr int NCAND = 2 * UP + 1;
+    constexpr int NCAND = 2 * UP;
     constexpr float scale = 1.0f / (float)UP;
     const int C4 = C / 4;
     const long e = (long)blockIdx.x * 256 + threadIdx.x;
@@ -393,7 +391,7 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__
     int oy[NCAND], ox[NCAND];
 #pragma unroll
     for (int k = 0; k < NCAND; ++k) {
-        const int y = UP * (i - 1) + k, x = UP * (j - 1) + k;
+        const int y = UP * i - UP / 2 + k, x = UP * j - UP / 2 + k;
         oy[k] = min(max(y, 0), H - 1);
         ox[k] = min(max(x, 0), W - 1);
         const Taps ty = taps(oy[k], h, scale), tx = taps(ox[k], w, scale);
@@ -404,15 +402,8 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__
 #pragma unroll
     for (int a = 0; a < NCAND; ++a)
 #pragma unroll
-        for (int k = 0; k < NCAND; ++k) {
-            const long off = (((long)b * H + oy[a]) * W + ox[k]) * C + c;
-            float4 v = masked_grad<T>(gy, my, nullptr, nullptr, nullptr, off, c);
-            if (dx) {
-                const float4 d = ld4(dx + off);
-                v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
-            }
-            acc = fma4(f4(wy[a] * wx[k]), v, acc);
-        }
+        for (int k = 0; k < NCAND; ++k)
+            acc = fma4(f4(wy[a] * wx[k]), ld4(g + (((long)b * H + oy[a]) * W + ox[k]) * C + c), acc);
     *reinterpret_cast<float4*>(dfeat + cell * C + c) = acc;
 }
 
@@ -513,16 +504,18 @@ extern "C" int ebc_dec_upsample_pad(int dtype, const float* feat, void* xpad, in
     return EBC_OK;
 }
 
-extern "C" int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, double* colsum, void* ws,
-                               size_t wsb, int B, int H, int W, int C, int N, ebc_stream_t stream)
+extern "C" int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, double* colsum,
+                               const void* add_gy, const void* add_y, void* ws, size_t wsb, int B, int H, int W, int C,
+                               int N, ebc_stream_t stream)
 {
-    if (!xpad || !weight || !out || C % 64 || N % 64) return EBC_E_ARG;
+    if (!xpad || !weight || !out || C % 64 || N % 64 || (colsum && add_gy) || (!add_gy != !add_y)) return EBC_E_ARG;
     const Geo g = make_geo(dtype, B, H, W, C);
     ebc::ConvGeom cg{H, W, C, g.Hp, g.Wp, 0, 0, 0};
     const int M = B * H * W;
     int tiles = 0;
     const hipStream_t st = (hipStream_t)stream;
-    EBC_TRY(ebc::conv_gemm(dtype, 1, colsum ? 4 : 0, xpad, weight, out, cg, M, N, 9 * C, ws, wsb, &tiles, st));
+    const int epi = colsum ? 4 : (add_gy ? 5 : 0);
+    EBC_TRY(ebc::conv_gemm(dtype, 1, epi, xpad, weight, out, cg, M, N, 9 * C, ws, wsb, &tiles, st, add_gy, add_y));
     if (colsum) {
         const float* part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(ws) + CONV_WS_STATS_OFFSET);
         hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * N + 63) / 64), dim3(1024), 0, st, part, tiles, 2 * N, colsum);
@@ -631,22 +624,20 @@ extern "C" int ebc_dec_transpose3(int dtype, const void* xpad, void* xT3, int B,
     return EBC_OK;
 }
 
-extern "C" int ebc_dec_upsample_bwd(int dtype, const void* dx, const void* gy, const void* mask_y, float* dfeat,
-                                    int B, int h, int w, int C, int up, ebc_stream_t stream)
+extern "C" int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int B, int h, int w, int C, int up,
+                                    ebc_stream_t stream)
 {
-    if (!gy || !mask_y || !dfeat || up < 1 || C % 4) return EBC_E_ARG;
-    const long cells = (long)B * h * w;
+    if (!g || !dfeat || C % 4) return EBC_E_ARG;
     if (up != 1 && up != 2) return EBC_E_UNSUPPORTED;
+    const long cells = (long)B * h * w;
     const unsigned grid = nblk(cells * (C / 4));
     const hipStream_t st = (hipStream_t)stream;
     if (up == 2) {
         EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 2>), dim3(grid), dim3(256), 0, st,
-                                                   (const T*)dx, (const T*)gy, (const T*)mask_y, dfeat, B, h, w, 2 * h,
-                                                   2 * w, C));
+                                                   (const T*)g, dfeat, B, h, w, 2 * h, 2 * w, C));
     } else {
         EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 1>), dim3(grid), dim3(256), 0, st,
-                                                   (const T*)dx, (const T*)gy, (const T*)mask_y, dfeat, B, h, w, h, w,
-                                                   C));
+                                                   (const T*)g, dfeat, B, h, w, h, w, C));
     }
     EBC_CHECK_LAUNCH();
     return EBC_OK;

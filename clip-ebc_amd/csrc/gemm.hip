@@ -24,13 +24,14 @@ using namespace ebc;
 
 namespace {
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4 };
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4, EPI_ADD_RELU_GRAD = 5 };
 
 struct GemmArgs {
     const void* A; const void* B; void* C;
     const float* bias;      // [N] or null
     const float* resid;     // [M,N] f32 (EPI_RESID), may alias C
-    void* aux;              // [M,N] element type: GELU pre-activation (written by EPI_GELU, read by EPI_GELU_BWD)
+    void* aux;              // [M,N] element type: GELU pre-activation (written by EPI_GELU, read by EPI_GELU_BWD);
+                            // EPI_ADD_RELU_GRAD: upstream gradient gy
     int M, N, K;
     // split-K: `splits` workgroups per output tile each take `kslice` of K; the last one to finish
     // (per-tile arrival counter `cnt`, re-armed to 0 by it) adds the others' f32 partials (`part`)
@@ -47,6 +48,7 @@ struct GemmArgs {
     int cH = 0, cW = 0, cC = 0, cHp = 0, cWp = 0, kpi = 0;
     long cQs = 0, cG = 0;
     float* stats = nullptr;  // EPI_STATS: [ceil(M/BM)][2][N] per-tile column sums / sums of squares
+    const void* aux2 = nullptr;   // EPI_ADD_RELU_GRAD: ReLU output y (mask y > 0): C = acc + gy * (y > 0)
 };
 
 // Slab rows are ROWB bytes (one BK-deep K slice): 128 (BK = 64 for 16-bit, 32 for f32) or 64
@@ -452,9 +454,32 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     constexpr int C8 = BN / 8;
     float* ep = reinterpret_cast<float*>(smem);
     float col_s = 0.f, col_q = 0.f;               // EPI_STATS: column tid's sums over the tile's rows
+    // Epilogue operands (resid / aux / aux2) of a pass are all loaded before the tile is staged through
+    // LDS (unconditional, row-clamped loads: no per-element branch or vmcnt(0)), so their latency
+    // hides under the staging stores and barriers instead of being paid per row chunk.
+    constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID || EPI == EPI_ADD_RELU_GRAD;
+    constexpr int NCH = EPR * C8;                // 8-column chunks per pass
+    constexpr int NIT = (NCH + NT - 1) / NT;
+    using PA = typename std::conditional<EPI == EPI_RESID, float, T>::type;
+    typedef PA pa8 __attribute__((ext_vector_type(8)));
+    typedef T t8v __attribute__((ext_vector_type(8)));
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #pragma unroll 1
     for (int pass = 0; pass < BM / EPR; ++pass) {
+        pa8 pre[PRE ? NIT : 1];
+        t8v pre2[EPI == EPI_ADD_RELU_GRAD ? NIT : 1];
+        if constexpr (PRE) {
+            const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
+#pragma unroll
+            for (int k = 0; k < NIT; ++k) {
+                const int c = min(tid + k * NT, NCH - 1), r = c / C8, col = (c % C8) * 8;
+                const int m = min(m0 + pass * EPR + r, g.M - 1);
+                const size_t off = (size_t)m * g.N + n0 + col;
+                pre[k] = *reinterpret_cast<const pa8*>(src + off);
+                if constexpr (EPI == EPI_ADD_RELU_GRAD)
+                    pre2[k] = *reinterpret_cast<const t8v*>(reinterpret_cast<const T*>(g.aux2) + off);
+            }
+        }
         __syncthreads();
         if ((wm * WM) / EPR == pass) {
 #pragma unroll
@@ -465,8 +490,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
                         make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
         }
         __syncthreads();
-#pragma unroll 2
-        for (int c = tid; c < EPR * C8; c += NT) {
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+            const int c = tid + k * NT;
+            if (NCH % NT != 0 && c >= NCH) break;
             const int r = c / C8, col = (c % C8) * 8;
             const int m = m0 + pass * EPR + r;
             if (m >= g.M) continue;
@@ -486,15 +513,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = quick_gelu(v[i]);
             } else if constexpr (EPI == EPI_GELU_BWD) {
-                float pa[8];
-                load8f<T>(reinterpret_cast<const T*>(g.aux) + off, pa);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] *= quick_gelu_grad(pa[i]);
+                for (int i = 0; i < 8; ++i) v[i] *= quick_gelu_grad((float)pre[k][i]);
+            } else if constexpr (EPI == EPI_ADD_RELU_GRAD) {
+                // decoder: conv1's input gradient plus the residual branch's (models/utils.py:300-302)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] += (float)pre2[k][i] > 0.f ? (float)pre[k][i] : 0.f;
             } else if constexpr (EPI == EPI_RESID) {
-                float rr[8];
-                load8f<float>(g.resid + off, rr);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] += rr[i];
+                for (int i = 0; i < 8; ++i) v[i] += pre[k][i];
             }
             store8<TO>(C + off, v);
         }
@@ -729,6 +756,7 @@ int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream
     using T = typename E::T;
     if (mode == 1 && epi == EPI_STORE) return launch_conv_tile<E, T, EPI_STORE, 1>(g, cfg, st);
     if (mode == 1 && epi == EPI_STATS) return launch_conv_tile<E, T, EPI_STATS, 1>(g, cfg, st);
+    if (mode == 1 && epi == EPI_ADD_RELU_GRAD) return launch_conv_tile<E, T, EPI_ADD_RELU_GRAD, 1>(g, cfg, st);
     if (mode == 2 && epi == EPI_STORE) return launch_conv_tile<E, float, EPI_STORE, 2>(g, cfg, st);
     return EBC_E_UNSUPPORTED;
 }
@@ -750,11 +778,13 @@ size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K)
 }
 
 int conv_gemm(int dtype, int mode, int epi, const void* A, const void* B, void* C, const ConvGeom& geo, int M, int N,
-              int K, void* ws, size_t wsb, int* stats_tiles, hipStream_t st)
+              int K, void* ws, size_t wsb, int* stats_tiles, hipStream_t st, const void* gy, const void* y)
 {
+    if (epi == EPI_ADD_RELU_GRAD && (!gy || !y)) return EBC_E_ARG;
     const int bk = dtype == EBC_F32 ? 32 : 64;
     if (M <= 0 || N <= 0 || K <= 0 || K % bk || N % 64 || !A || !B || !C || (mode != 1 && mode != 2)) return EBC_E_ARG;
-    GemmArgs g{A, B, C, nullptr, nullptr, nullptr, M, N, K};
+    GemmArgs g{A, B, C, nullptr, nullptr, const_cast<void*>(gy), M, N, K};
+    g.aux2 = y;
     g.cH = geo.H; g.cW = geo.W; g.cC = geo.C; g.cHp = geo.Hp; g.cWp = geo.Wp; g.kpi = geo.kpi;
     g.cQs = geo.Qs; g.cG = geo.G;
     if (mode == 1 && geo.C % bk) return EBC_E_UNSUPPORTED;

@@ -19,8 +19,10 @@ struct ConvGeom {
 // mode 1: C[M = B*H*W, N] = conv(A = padded NHWC image, B = weights [N][9*C]), epi 0 store / 4 + BN stats
 //         (per-tile column partials at ws + 16 KiB: [stats_tiles][2][N]);
 // mode 2: C[M, N = 9*C] f32 = A^T-image . B^T-images (weight gradient), split-K through ws
+// epi 5 (mode 1): C = conv + gy * (y > 0)   (decoder: conv1 input gradient + residual-branch gradient)
 int conv_gemm(int dtype, int mode, int epi, const void* A, const void* B, void* C, const ConvGeom& geo, int M, int N,
-              int K, void* ws, size_t wsb, int* stats_tiles, hipStream_t st);
+              int K, void* ws, size_t wsb, int* stats_tiles, hipStream_t st, const void* gy = nullptr,
+              const void* y = nullptr);
 size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K);
 constexpr size_t CONV_WS_STATS_OFFSET = 16 * 1024;
 int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,

@@ -52,7 +52,7 @@ SIGNATURES = {
     "ebc_dec_geometry": (_I, [_I, _I, _I, _I, _I, _P]),
     "ebc_dec_workspace_bytes": (_Z, [_I, _I, _I, _I, _I, _I]),
     "ebc_dec_upsample_pad": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
-    "ebc_conv3x3_fwd": (_I, [_I, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _P]),
+    "ebc_conv3x3_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _P]),
     "ebc_conv3x3_wgrad": (_I, [_I, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _P]),
     "ebc_bn_finalize": (_I, [_P, _D, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "ebc_bn_relu_pad": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
@@ -62,7 +62,7 @@ SIGNATURES = {
     "ebc_bn_bwd_apply": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_dec_transpose3": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_dec_prep_weights": (_I, [_I, _P, _P, _P, _I, _I, _P]),
-    "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
 }
 
 

@@ -266,16 +266,32 @@ class _HeadFn(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- decoder
-_DEC_WS: Dict[torch.device, Tensor] = {}
+_DEC_WS: Dict[Tuple[torch.device, int], Tensor] = {}
+# EBC_DEC_SIDE=1 runs the weight-gradient GEMMs on a side stream beside the data-gradient chain.  Off by
+# default: measured 2.7 % slower per step on MI355X (r01, interleaved A/B in one process: the two
+# 1-workgroup-per-CU GEMMs contend for CUs and the data-gradient chain is the critical path).
+_USE_SIDE = __import__("os").environ.get("EBC_DEC_SIDE", "0") == "1"
+_SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
 
 
-def _dec_workspace(dev: torch.device, nbytes: int) -> Tensor:
-    """Stream-owned scratch of the decoder calls; its first 16 KiB (split-K counters) start zeroed."""
-    ws = _DEC_WS.get(dev)
+def _dec_workspace(dev: torch.device, nbytes: int, slot: int = 0) -> Tensor:
+    """Stream-owned scratch of the decoder calls (slot 0: the caller's stream, slot 1: the side stream of the
+    weight-gradient GEMMs); its first 16 KiB (split-K counters) start zeroed."""
+    ws = _DEC_WS.get((dev, slot))
     if ws is None or ws.numel() < nbytes:
         ws = torch.zeros(max(nbytes, 1 << 20), device=dev, dtype=torch.uint8)
-        _DEC_WS[dev] = ws
+        _DEC_WS[(dev, slot)] = ws
     return ws
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """A second HIP stream: the decoder's weight-gradient GEMMs run on it beside the data-gradient chain
+    (nothing waits for dW until the end of the decoder backward)."""
+    s = _SIDE.get(dev)
+    if s is None:
+        s = torch.cuda.Stream(device=dev)
+        _SIDE[dev] = s
+    return s
 
 
 def _bn_group(bn: nn.Module):
@@ -331,8 +347,8 @@ class _DecoderFn(torch.autograd.Function):
             z = torch.empty(P, N, device=dev, dtype=cdtype)
             use_batch = training or not bn.track_running_stats
             colsum = torch.empty(2, N, device=dev, dtype=torch.float64) if use_batch else None
-            _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(inp), _lib.ptr(wk), _lib.ptr(z), _lib.ptr(colsum), _lib.ptr(ws),
-                                         ws.numel(), B, H, W, C, N, st), "ebc_conv3x3_fwd")
+            _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(inp), _lib.ptr(wk), _lib.ptr(z), _lib.ptr(colsum), None, None,
+                                         _lib.ptr(ws), ws.numel(), B, H, W, C, N, st), "ebc_conv3x3_fwd")
             count = float(P)
             pg = _bn_group(bn) if use_batch else None
             if pg is not None:
@@ -370,7 +386,11 @@ class _DecoderFn(torch.autograd.Function):
         B, h, w, H, W, C, N, up, cdtype, Q, Qs, P = ctx.meta
         dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream()
         gy = gy.to(cdtype).contiguous()
-        ws = _dec_workspace(dev, L.ebc_dec_workspace_bytes(dt, B, H, W, C, N))
+        nbytes = L.ebc_dec_workspace_bytes(dt, B, H, W, C, N)
+        ws = _dec_workspace(dev, nbytes)
+        ws_side = _dec_workspace(dev, nbytes, 1)
+        cur = torch.cuda.current_stream(dev)
+        side = _side_stream(dev) if _USE_SIDE else cur
         f32 = dict(device=dev, dtype=torch.float32)
         grads = []
         dnext = gy                                    # gradient at the current BN output's ReLU
@@ -396,18 +416,26 @@ class _DecoderFn(torch.autograd.Function):
             xT3 = torch.empty(3, C, Qs, device=dev, dtype=cdtype)
             _lib.check(L.ebc_dec_transpose3(dt, _lib.ptr(src), _lib.ptr(xT3), B, H, W, C, st), "ebc_dec_transpose3")
             dw = torch.empty(N, C, 3, 3, **f32)
-            _lib.check(L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws), ws.numel(),
-                                           B, H, W, C, N, st), "ebc_conv3x3_wgrad")
+            # weight gradient on the side stream, overlapping the data-gradient chain below
+            side.wait_stream(cur)
+            for t_ in (dzT, xT3, dw):
+                t_.record_stream(side)
+            _lib.check(L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws_side),
+                                           ws_side.numel(), B, H, W, C, N, ctypes.c_void_p(side.cuda_stream)),
+                       "ebc_conv3x3_wgrad")
             del xT3, dzT
             wf = (wf1, wf2)[i]                                                    # [C][3][3][N]
             dx = torch.empty(P, C, device=dev, dtype=cdtype)
-            _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(dzpad), _lib.ptr(wf), _lib.ptr(dx), None, _lib.ptr(ws),
+            # conv1's data gradient also takes the residual branch's gradient (gy through the final ReLU)
+            add = (_lib.ptr(gy), _lib.ptr(y)) if i == 0 else (None, None)
+            _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(dzpad), _lib.ptr(wf), _lib.ptr(dx), None, *add, _lib.ptr(ws),
                                          ws.numel(), B, H, W, N, C, st), "ebc_conv3x3_fwd(dgrad)")
             grads.append((dw, dg, db))
             dnext, mask = dx, None
         dfeat = torch.empty(B, h, w, C, **f32)
-        _lib.check(L.ebc_dec_upsample_bwd(dt, _lib.ptr(dnext), _lib.ptr(gy), _lib.ptr(y), _lib.ptr(dfeat), B, h, w, C,
-                                          up, st), "ebc_dec_upsample_bwd")
+        _lib.check(L.ebc_dec_upsample_bwd(dt, _lib.ptr(dnext), _lib.ptr(dfeat), B, h, w, C, up, st),
+                   "ebc_dec_upsample_bwd")
+        cur.wait_stream(side)                          # dW ready before autograd hands it on
         (dw2, dg2, db2), (dw1, dg1, db1) = grads
         ctx.outs = None
         return dfeat, dw1, dg1, db1, dw2, dg2, db2, None, None, None, None

@@ -178,9 +178,10 @@ size_t ebc_dec_workspace_bytes(int dtype, int B, int H, int W, int C, int N);
 int ebc_dec_upsample_pad(int dtype, const float* feat, void* xpad, int B, int h, int w, int C, int up,
                          ebc_stream_t stream);
 /* out[B*H*W][N] = conv3x3(xpad, weight) (nn.Conv2d(C, N, 3, padding=1, bias=False)); colsum != NULL:
- * also the f64 column sums [2][N] (sum, sum of squares) for BatchNorm */
-int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, double* colsum, void* ws,
-                    size_t wsb, int B, int H, int W, int C, int N, ebc_stream_t stream);
+ * also the f64 column sums [2][N] (sum, sum of squares) for BatchNorm; add_gy/add_y != NULL (data
+ * gradient of conv1): out += add_gy * (add_y > 0), the residual branch's gradient through the final ReLU */
+int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, double* colsum, const void* add_gy,
+                    const void* add_y, void* ws, size_t wsb, int B, int H, int W, int C, int N, ebc_stream_t stream);
 /* dw[N][C][3][3] f32 = weight gradient from dzT and xT3 */
 int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, float* dw, void* ws, size_t wsb, int B, int H,
                       int W, int C, int N, ebc_stream_t stream);
@@ -210,9 +211,9 @@ int ebc_bn_bwd_apply(int dtype, const void* gy, const void* mask_y, const void* 
 int ebc_dec_transpose3(int dtype, const void* xpad, void* xT3, int B, int H, int W, int C, ebc_stream_t stream);
 /* conv weight [N][C][3][3] f32 -> wk [N][3][3][C] (forward) and wf [C][3][3][N] (flipped, data gradient) */
 int ebc_dec_prep_weights(int dtype, const float* w, void* wk, void* wf, int N, int C, ebc_stream_t stream);
-/* dfeat = bilinear_up^T(dx + gy * relu'(mask_y)), dx may be NULL */
-int ebc_dec_upsample_bwd(int dtype, const void* dx, const void* gy, const void* mask_y, float* dfeat, int B, int h,
-                         int w, int C, int up, ebc_stream_t stream);
+/* dfeat [B][h][w][C] f32 = bilinear_up^T(g), g [B*H*W][C] (up = 1 or 2) */
+int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int B, int h, int w, int C, int up,
+                         ebc_stream_t stream);
 
 #ifdef __cplusplus
 }

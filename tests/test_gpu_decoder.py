@@ -118,8 +118,8 @@ def test_conv3x3_abi_matches_torch():
     out = torch.empty(B * H * W, N, dtype=torch.float16, device="cuda")
     colsum = torch.empty(2, N, dtype=torch.float64, device="cuda")
     ws = torch.zeros(L.ebc_dec_workspace_bytes(_lib.EBC_F16, B, H, W, C, N), dtype=torch.uint8, device="cuda")
-    _lib.check(L.ebc_conv3x3_fwd(_lib.EBC_F16, _lib.ptr(xpad), _lib.ptr(wk), _lib.ptr(out), _lib.ptr(colsum),
-                                 _lib.ptr(ws), ws.numel(), B, H, W, C, N, _lib.stream()), "conv")
+    _lib.check(L.ebc_conv3x3_fwd(_lib.EBC_F16, _lib.ptr(xpad), _lib.ptr(wk), _lib.ptr(out), _lib.ptr(colsum), None,
+                                 None, _lib.ptr(ws), ws.numel(), B, H, W, C, N, _lib.stream()), "conv")
     ref = F.conv2d(x.half().double(), wt.half().double(), padding=1).permute(0, 2, 3, 1).reshape(-1, N)
     assert rel_l2(out.float().cpu().numpy(), ref.numpy()) < 2e-3
     np.testing.assert_allclose(colsum[0].cpu().numpy(), ref.sum(0).numpy(), rtol=1e-2, atol=1e-1)

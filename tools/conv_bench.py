@@ -40,9 +40,9 @@ def main():
     dw = torch.empty(C, 3, 3, C, device="cuda")
     st = _lib.stream()
     f = 2.0 * B * H * W * C * C * 9
-    t1 = timeit(lambda: L.ebc_conv3x3_fwd(dt, _lib.ptr(x), _lib.ptr(wk), _lib.ptr(out), _lib.ptr(colsum), _lib.ptr(ws),
+    t1 = timeit(lambda: L.ebc_conv3x3_fwd(dt, _lib.ptr(x), _lib.ptr(wk), _lib.ptr(out), _lib.ptr(colsum), None, None, _lib.ptr(ws),
                                           ws.numel(), B, H, W, C, C, st))
-    t2 = timeit(lambda: L.ebc_conv3x3_fwd(dt, _lib.ptr(x), _lib.ptr(wk), _lib.ptr(out), None, _lib.ptr(ws),
+    t2 = timeit(lambda: L.ebc_conv3x3_fwd(dt, _lib.ptr(x), _lib.ptr(wk), _lib.ptr(out), None, None, None, _lib.ptr(ws),
                                           ws.numel(), B, H, W, C, C, st))
     t3 = timeit(lambda: L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws), ws.numel(),
                                             B, H, W, C, C, st))
