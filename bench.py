@@ -153,6 +153,20 @@ def setup(args, rank, world, local, device):
     return step
 
 
+def committed_traffic(dtype):
+    """HBM bytes per launch of the probe kernel from the committed PMC passes (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE, profiles/r01_gemm_fc_traffic.json); None when no profile matches."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_gemm_fc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if dtype != "fp16" or "EF16" not in rec.get("kernel", ""):
+        return None
+    return rec["traffic_bytes_per_launch"]
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,7 +217,9 @@ def main():
                                    f"{B} crops/GPU, AMP {args.dtype} (BASELINE configs[2]" + (", DDP configs[3] shape" if world > 1 else "") + ")",
                        "global_batch": B * world, "seq_len": 229, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(probe["achieved"], 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(probe["achieved"] / peak, 4), "traffic": None,
+                         "frac": round(probe["achieved"] / peak, 4), "traffic": committed_traffic(args.dtype),
+                         "traffic_unit": "bytes/launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_gemm_fc_traffic.json)",
+                         "algorithmic_bytes": 55369728,
                          "kernel": probe["kernel"], "avg_us": round(probe["avg_us"], 2)},
             "step_roofline": {"flop_per_crop": FLOP_PER_CROP, "achieved_tflops": round(value / world * FLOP_PER_CROP / 1e12, 2),
                               "frac": round(value / world * FLOP_PER_CROP / 1e12 / peak, 4)},
