@@ -48,6 +48,20 @@ template <> __device__ __forceinline__ float4 ld4<__bf16>(const __bf16* p) {
     const b4 v = *reinterpret_cast<const b4*>(p);
     return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
 }
+// 8 consecutive elements (16 B for 16-bit types, 32 B for f32) <-> float[8]
+template <class T> __device__ __forceinline__ void ld8(const T* p, float* v) {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const t8 x = *reinterpret_cast<const t8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)x[i];
+}
+template <class T> __device__ __forceinline__ void st8(T* p, const float* v) {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (T)v[i];
+    *reinterpret_cast<t8*>(p) = x;
+}
 __device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
 __device__ __forceinline__ float4 fma4(float4 a, float4 b, float4 c) {
     return make_float4(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z), fmaf(a.w, b.w, c.w));
@@ -218,22 +232,12 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __re
 }
 
 // ------------------------------------------------------------------ backward
-// g = gy * relu'(.)  with the ReLU mask from the stored output (mask_y) or recomputed from z
-template <class T>
-__device__ __forceinline__ float4 masked_grad(const T* gy, const T* my, const T* z, const float* scale,
-                                              const float* shift, long off, int c) {
-    const float4 gv = ld4(gy + off);
-    float4 m;
-    if (my) {
-        m = ld4(my + off);
-    } else {
-        m = fma4(ld4(z + off), ld4(scale + c), ld4(shift + c));
-    }
-    return make_float4(m.x > 0.f ? gv.x : 0.f, m.y > 0.f ? gv.y : 0.f, m.z > 0.f ? gv.z : 0.f, m.w > 0.f ? gv.w : 0.f);
-}
+// g = gy * relu'(.)  with the ReLU mask from the stored output (mask_y) or recomputed from z (HAS_MY false)
 
-// column partials of sum(g) and sum(g * xhat), xhat = (z - mean) * rstd; block = (C/4) x RL threads
-template <class T>
+// column partials of sum(g) and sum(g * xhat), xhat = (z - mean) * rstd; block = (C/8) x RL threads, 8
+// channels (one 16-B vector) per thread.  Each thread walks its rows UNR at a time with every load issued
+// first (row-clamped, unconditional); the sums keep the row order.
+template <class T, bool HAS_MY, int UNR>
 __global__ __launch_bounds__(512) void bn_bwd_partial_kernel(const T* __restrict__ gy, const T* __restrict__ my,
                                                              const T* __restrict__ z, const float* __restrict__ mean,
                                                              const float* __restrict__ rstd,
@@ -242,25 +246,42 @@ __global__ __launch_bounds__(512) void bn_bwd_partial_kernel(const T* __restrict
                                                              long P, int C, int rows_per_block)
 {
     extern __shared__ float red[];                // [RL][2][C]
-    const int C4 = C / 4, RL = blockDim.x / C4;
-    const int cg = threadIdx.x % C4, rl = threadIdx.x / C4, c = cg * 4;
+    const int C8 = C / 8, RL = blockDim.x / C8;
+    const int rl = threadIdx.x / C8, c = (threadIdx.x - rl * C8) * 8;
     const long r0 = (long)blockIdx.x * rows_per_block;
     const long r1 = std::min<long>(P, r0 + rows_per_block);
-    const float4 mu = ld4(mean + c), rs = ld4(rstd + c);
-    float4 s1 = f4(0.f), s2 = f4(0.f);
-    if (rl < RL) {
-        for (long r = r0 + rl; r < r1; r += RL) {
-            const long off = r * C + c;
-            const float4 gv = masked_grad(gy, my, z, scale, shift, off, c);
-            const float4 zv = ld4(z + off);
-            s1.x += gv.x; s1.y += gv.y; s1.z += gv.z; s1.w += gv.w;
-            s2.x = fmaf(gv.x, (zv.x - mu.x) * rs.x, s2.x);
-            s2.y = fmaf(gv.y, (zv.y - mu.y) * rs.y, s2.y);
-            s2.z = fmaf(gv.z, (zv.z - mu.z) * rs.z, s2.z);
-            s2.w = fmaf(gv.w, (zv.w - mu.w) * rs.w, s2.w);
+    float mu[8], rs[8], sc[8], sh[8], s1[8], s2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        mu[i] = mean[c + i]; rs[i] = rstd[c + i];
+        sc[i] = HAS_MY ? 0.f : scale[c + i]; sh[i] = HAS_MY ? 0.f : shift[c + i];
+        s1[i] = 0.f; s2[i] = 0.f;
+    }
+    for (long r = r0 + rl; r < r1; r += UNR * RL) {
+        float gv[UNR][8], zv[UNR][8], mv[HAS_MY ? UNR : 1][8];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            const long off = std::min<long>(r + k * RL, r1 - 1) * C + c;
+            ld8(gy + off, gv[k]);
+            ld8(z + off, zv[k]);
+            if (HAS_MY) ld8(my + off, mv[k]);
         }
-        *reinterpret_cast<float4*>(red + (size_t)rl * 2 * C + c) = s1;
-        *reinterpret_cast<float4*>(red + (size_t)rl * 2 * C + C + c) = s2;
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            if (r + k * RL >= r1) continue;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float m = HAS_MY ? mv[k][i] : fmaf(zv[k][i], sc[i], sh[i]);
+                const float g = m > 0.f ? gv[k][i] : 0.f;
+                s1[i] += g;
+                s2[i] = fmaf(g, (zv[k][i] - mu[i]) * rs[i], s2[i]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        red[(size_t)rl * 2 * C + c + i] = s1[i];
+        red[(size_t)rl * 2 * C + C + c + i] = s2[i];
     }
     __syncthreads();
     for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) {
@@ -290,8 +311,10 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
 // (rows of channels) and the transposed image (rows of positions) are written with contiguous rows.
 constexpr int TQ = 64, TC = 64;
 
-// dz = gamma*rstd * (g - mean(g) - xhat * mean(g*xhat)) -> dzpad [Q][C] and dzT [C][Qs]
-template <class T>
+// dz = gamma*rstd * (g - mean(g) - xhat * mean(g*xhat)) -> dzpad [Q][C] and dzT [C][Qs].  A 64-pixel x
+// 64-channel tile per block: the per-channel factors staged in LDS once, every thread's 16 channels of
+// gy / mask / z loaded up front (row-clamped: no load behind a branch), 16-B stores both ways.
+template <class T, bool HAS_MY>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ gy, const T* __restrict__ my,
                                                            const T* __restrict__ z, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
@@ -301,40 +324,50 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            T* __restrict__ dzT, DGeo g)
 {
     __shared__ float sm[TQ][TC + 1];
+    __shared__ float cf[7][TC];                   // gamma*rstd, mean(g), mean(g*xhat), mean, rstd, scale, shift
     const int t = threadIdx.x;
     const long j0 = (long)blockIdx.x * TQ;
     const int c0 = blockIdx.y * TC;
-    {
-        const int ql = t >> 2, cl = (t & 3) * 16;
-        const long q = j0 + ql - g.G;
-        const long p = interior(g, q);
+    const int ql = t >> 2, cl = (t & 3) * 16;
+    const long q = j0 + ql - g.G;
+    const long p = interior(g, q);
+    const long off = (p >= 0 ? p : 0) * g.C + c0 + cl;
+    float gv[16], zv[16], mv[HAS_MY ? 16 : 1];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c = c0 + cl + 4 * k;
-            float4 v = f4(0.f);
-            if (p >= 0) {
-                const long off = p * g.C + c;
-                const float4 gv = masked_grad(gy, my, z, scale, shift, off, c);
-                const float4 zv = ld4(z + off), mu = ld4(mean + c), rs = ld4(rstd + c);
-                const float4 a = ld4(coef + c), mg = ld4(coef + g.C + c), mgx = ld4(coef + 2 * g.C + c);
-                v.x = a.x * (gv.x - mg.x - (zv.x - mu.x) * rs.x * mgx.x);
-                v.y = a.y * (gv.y - mg.y - (zv.y - mu.y) * rs.y * mgx.y);
-                v.z = a.z * (gv.z - mg.z - (zv.z - mu.z) * rs.z * mgx.z);
-                v.w = a.w * (gv.w - mg.w - (zv.w - mu.w) * rs.w * mgx.w);
-            }
-            if (q >= 0 && q < g.Q) st4(dzpad + q * g.C + c, v);
-            sm[ql][cl + 4 * k] = v.x; sm[ql][cl + 4 * k + 1] = v.y;
-            sm[ql][cl + 4 * k + 2] = v.z; sm[ql][cl + 4 * k + 3] = v.w;
-        }
+    for (int h = 0; h < 2; ++h) {
+        ld8(gy + off + 8 * h, gv + 8 * h);
+        ld8(z + off + 8 * h, zv + 8 * h);
+        if (HAS_MY) ld8(my + off + 8 * h, mv + 8 * h);
+    }
+    if (t < TC) {
+        const int c = c0 + t;
+        cf[0][t] = coef[c]; cf[1][t] = coef[g.C + c]; cf[2][t] = coef[2 * g.C + c];
+        cf[3][t] = mean[c]; cf[4][t] = rstd[c];
+        if (!HAS_MY) { cf[5][t] = scale[c]; cf[6][t] = shift[c]; }
+    }
+    __syncthreads();
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int cc = cl + i;
+        const float m = HAS_MY ? mv[i] : fmaf(zv[i], cf[5][cc], cf[6][cc]);
+        const float gg = m > 0.f ? gv[i] : 0.f;
+        v[i] = p >= 0 ? cf[0][cc] * (gg - cf[1][cc] - (zv[i] - cf[3][cc]) * cf[4][cc] * cf[2][cc]) : 0.f;
+        sm[ql][cc] = v[i];
+    }
+    if (q >= 0 && q < g.Q) {
+        st8(dzpad + q * g.C + c0 + cl, v);
+        st8(dzpad + q * g.C + c0 + cl + 8, v + 8);
     }
     __syncthreads();
     {
         const int cr = t >> 2, jl = (t & 3) * 16;
         T* dst = dzT + (size_t)(c0 + cr) * g.Qs + j0 + jl;
+        float w[16];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            st4(dst + 4 * k, make_float4(sm[jl + 4 * k][cr], sm[jl + 4 * k + 1][cr], sm[jl + 4 * k + 2][cr],
-                                         sm[jl + 4 * k + 3][cr]));
+        for (int i = 0; i < 16; ++i) w[i] = sm[jl + i][cr];
+        st8(dst, w);
+        st8(dst + 8, w + 8);
     }
 }
 
@@ -349,10 +382,16 @@ __global__ __launch_bounds__(256) void transpose3_kernel(const T* __restrict__ x
     constexpr int NE = (TQ + 2) * (TC / 4), PER = (NE + 255) / 256;
     float4 v[PER];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {                // all loads in flight before the LDS writes
-        const int e = t + 256 * k, ql = e / (TC / 4), cl = (e % (TC / 4)) * 4;
+    for (int k = 0; k < PER; ++k) {                // all loads in flight before the LDS writes (clamped
+        const int e = min(t + 256 * k, NE - 1), ql = e / (TC / 4), cl = (e % (TC / 4)) * 4;   // addresses,
+        const long q = j0 - g.G + ql - 1;                                                       // no branch)
+        v[k] = ld4(xpad + std::min<long>(std::max<long>(q, 0), g.Q - 1) * g.C + c0 + cl);
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int e = min(t + 256 * k, NE - 1), ql = e / (TC / 4);
         const long q = j0 - g.G + ql - 1;
-        v[k] = (e < NE && q >= 0 && q < g.Q) ? ld4(xpad + q * g.C + c0 + cl) : f4(0.f);
+        if (q < 0 || q >= g.Q) v[k] = f4(0.f);
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -428,33 +467,48 @@ __global__ __launch_bounds__(256) void prep_weights_kernel(const float* __restri
         sm[ol][r] = v[k];
     }
     __syncthreads();
-    for (int e = t; e < 32 * 9 * 32; e += 256) {   // wk rows (o, tap): 32 contiguous c
-        const int cl = e & 31, r = e >> 5, ol = r / 9, tap = r - ol * 9;
-        if (o0 + ol < N && c0 + cl < C) wk[((size_t)(o0 + ol) * 9 + tap) * C + c0 + cl] = (T)sm[ol][cl * 9 + tap];
+    // 16-B stores of 8 consecutive elements (N, C multiples of 32: checked by the launcher)
+    for (int e = t; e < 32 * 9 * 4; e += 256) {    // wk rows (o, tap): 32 contiguous c
+        const int cv = (e & 3) * 8, r = e >> 2, ol = r / 9, tap = r - ol * 9;
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = sm[ol][(cv + i) * 9 + tap];
+        st8(wk + ((size_t)(o0 + ol) * 9 + tap) * C + c0 + cv, x);
     }
-    for (int e = t; e < 32 * 9 * 32; e += 256) {   // wf rows (c, tap): 32 contiguous o
-        const int ol = e & 31, r = e >> 5, cl = r / 9, tap = r - cl * 9;
-        if (o0 + ol < N && c0 + cl < C) wf[((size_t)(c0 + cl) * 9 + tap) * N + o0 + ol] = (T)sm[ol][cl * 9 + 8 - tap];
+    for (int e = t; e < 32 * 9 * 4; e += 256) {    // wf rows (c, tap): 32 contiguous o
+        const int ov = (e & 3) * 8, r = e >> 2, cl = r / 9, tap = r - cl * 9;
+        float x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = sm[ov + i][cl * 9 + 8 - tap];
+        st8(wf + ((size_t)(c0 + cl) * 9 + tap) * N + o0 + ov, x);
     }
 }
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
+// bn_bwd_partial rows per block: 8 rows per thread-row-lane (two 4-row load batches)
+inline int bn_partial_rows(int C) { return 8 * std::max(1, 512 / std::max(1, C / 8)); }
 
 template <class T>
 int bn_bwd_reduce_t(const void* gy, const void* my, const void* z, const float* mean, const float* rstd,
                     const float* scale, const float* shift, double* sums, void* ws, size_t wsb, long P, int C,
                     hipStream_t st)
 {
-    const int C4 = C / 4;
-    const int RL = std::max(1, 512 / C4);
-    const int threads = C4 * RL;
-    const int rpb = 64;
+    if (C % 8 || C / 8 > 512) return EBC_E_UNSUPPORTED;
+    const int C8 = C / 8;
+    const int RL = std::max(1, 512 / C8);
+    const int threads = C8 * RL;
+    const int rpb = bn_partial_rows(C);
     const long nb = (P + rpb - 1) / rpb;
     const size_t need = CONV_WS_STATS_OFFSET + (size_t)nb * 2 * C * 4;
-    if (!ws || wsb < need || threads > 1024) return EBC_E_ARG;
+    if (!ws || wsb < need) return EBC_E_ARG;
     float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + CONV_WS_STATS_OFFSET);
-    hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, dim3((unsigned)nb), dim3(threads), (size_t)RL * 2 * C * 4, st,
-                       (const T*)gy, (const T*)my, (const T*)z, mean, rstd, scale, shift, part, P, C, rpb);
+    const size_t lds = (size_t)RL * 2 * C * 4;
+    if (my)
+        hipLaunchKernelGGL((bn_bwd_partial_kernel<T, true, 4>), dim3((unsigned)nb), dim3(threads), lds, st,
+                           (const T*)gy, (const T*)my, (const T*)z, mean, rstd, scale, shift, part, P, C, rpb);
+    else
+        hipLaunchKernelGGL((bn_bwd_partial_kernel<T, false, 4>), dim3((unsigned)nb), dim3(threads), lds, st,
+                           (const T*)gy, (const T*)my, (const T*)z, mean, rstd, scale, shift, part, P, C, rpb);
     hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
                        2 * C, sums);
     EBC_CHECK_LAUNCH();
@@ -487,7 +541,8 @@ extern "C" size_t ebc_dec_workspace_bytes(int dtype, int B, int H, int W, int C,
     size_t need = ebc::conv_gemm_workspace_bytes(dtype, 1, M, N, 9 * C);
     need = std::max(need, ebc::conv_gemm_workspace_bytes(dtype, 1, M, C, 9 * N));
     need = std::max(need, ebc::conv_gemm_workspace_bytes(dtype, 2, N, 9 * C, B * g.kpi * g.bk));
-    const long nb = ((long)M + 63) / 64;
+    const int rpb = std::min(bn_partial_rows(C), bn_partial_rows(N));
+    const long nb = std::max(((long)M + 63) / 64, ((long)M + rpb - 1) / rpb);
     need = std::max(need, CONV_WS_STATS_OFFSET + (size_t)nb * 2 * std::max(C, N) * 4);
     return need;
 }
@@ -604,9 +659,15 @@ extern "C" int ebc_bn_bwd_apply(int dtype, const void* gy, const void* mask_y, c
     const Geo g = make_geo(dtype, B, H, W, C);
     const DGeo d = dgeo(g);
     const dim3 grid((unsigned)(g.Qs / TQ), (unsigned)(C / TC));
-    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream,
-                                               (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale, shift,
-                                               coef, (T*)dzpad, (T*)dzT, d));
+    if (mask_y) {
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), grid, dim3(256), 0, (hipStream_t)stream,
+                                                   (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale,
+                                                   shift, coef, (T*)dzpad, (T*)dzT, d));
+    } else {
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false>), grid, dim3(256), 0, (hipStream_t)stream,
+                                                   (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale,
+                                                   shift, coef, (T*)dzpad, (T*)dzT, d));
+    }
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -645,8 +706,8 @@ extern "C" int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int 
 
 extern "C" int ebc_dec_prep_weights(int dtype, const float* w, void* wk, void* wf, int N, int C, ebc_stream_t stream)
 {
-    if (!w || !wk || !wf || N <= 0 || C <= 0) return EBC_E_ARG;
-    const dim3 grid((unsigned)((N + 31) / 32), (unsigned)((C + 31) / 32));
+    if (!w || !wk || !wf || N <= 0 || C <= 0 || N % 32 || C % 32) return EBC_E_ARG;
+    const dim3 grid((unsigned)(N / 32), (unsigned)(C / 32));
     EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(prep_weights_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, w,
                                                (T*)wk, (T*)wf, N, C));
     EBC_CHECK_LAUNCH();

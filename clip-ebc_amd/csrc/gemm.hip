@@ -60,6 +60,18 @@ template <int ROWB> __device__ __forceinline__ int swz_row(int row) {
     else return (0x1320 >> (((row >> 2) & 3) * 4)) & 3;      // [0,2,3,1][(row >> 2) & 3]
 }
 
+// MODE 0 B-slab row -> output column within the tile.  The swapped MFMA leaves each lane 4
+// consecutive columns (4*fg .. 4*fg+3) of one row per 16-column sub-tile; loading the B rows of a
+// wave's WN columns in this order makes sub-tiles 2p and 2p+1 hold the 8 consecutive columns
+// p*32 + 8*fg .. +7 of the lane's row (an odd last sub-tile keeps its own 4), so the epilogue stores
+// straight from the accumulators in 16-B pieces (64 B per row per instruction), without staging the
+// tile through LDS.
+template <int WN, int TN> __device__ __forceinline__ int bcol(int s) {
+    const int w = s / WN, l = s - w * WN, b = l >> 4, j = l & 15, fg = j >> 2, i = j & 3;
+    const int c = ((TN & 1) && b == TN - 1) ? b * 16 + fg * 4 + i : (b >> 1) * 32 + fg * 8 + (b & 1) * 4 + i;
+    return w * WN + c;
+}
+
 // QuickGELU x*sigmoid(1.702x) (blocks.py:17-19) with the hardware exp2 / reciprocal (1-ulp each):
 // the IEEE expf + division forms cost ~25 VALU per element in the epilogue.
 __device__ __forceinline__ float sigmoid1702(float a) {
@@ -220,7 +232,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
                 base = A + (size_t)gr * K;
             }
         } else {
-            const int n = n0 + row - BM;
+            const int n = n0 + (MODE == 0 ? bcol<WN, TN>(row - BM) : row - BM);
             if constexpr (MODE == 2) {
                 const int cc = n / 9, t = n - 9 * cc, ky = t / 3, kx = t - 3 * ky;   // nn.Conv2d [o][c][ky][kx]
                 base = Bw + (size_t)(kx * g.cC + cc) * g.cQs + g.cG + (long)(ky - 1) * g.cWp;
@@ -404,6 +416,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     int kt0 = 0;
     for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
     for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
+#if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 4)
+    // experiment build: no epilogue (a never-taken store keeps the K loop alive)
+    if (g.K == 12345) {
+        float s = 0.f;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+        reinterpret_cast<float*>(g.C)[tid] = s;
+    }
+    return;
+#endif
 
     if (g.splits > 1) {
         // split-K: publish this split's f32 partial (lane-major: the reader has the same lane map,
@@ -430,18 +454,99 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         if (tid == 0) last = atomicAdd(&g.cnt[tile], 1) == g.splits - 1;
         __syncthreads();
         if (!last) return;
-        for (int sp = 0; sp < g.splits; ++sp) {
-            if (sp == split) continue;
+        // bit-reproducible sum whichever split arrives last: two splits add the other's partial (f32
+        // addition commutes); more splits re-read every partial, this one's too, in split order
+        auto add_partial = [&](int sp) {
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
                 for (int b = 0; b < TN; ++b)
                     acc[a][b] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                         rs, ((sp * PT) + ((wave * TM + a) * TN + b) * 64 + lane) * 16, 0, 16));
+        };
+        if (g.splits == 2) {
+            add_partial(1 - split);
+        } else {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int sp = 0; sp < g.splits; ++sp) add_partial(sp);
         }
         if (tid == 0) atomicExch(&g.cnt[tile], 0);   // re-armed for the next launch
     }
 
+    if constexpr (MODE == 0) {
+        // direct epilogue (bcol above): lane (fr, fg) holds rows m0 + wm*WM + a*16 + fr and, per column
+        // group q, 8 (a sub-tile pair) or 4 (odd last sub-tile) consecutive columns.  Operands
+        // (resid / aux) are loaded for the whole wave tile first (row-clamped, unconditional), then each
+        // group is finished and stored; rows >= M are never stored.
+        static_assert(EPI <= EPI_GELU_BWD, "MODE 0 epilogues");
+        TO* C = reinterpret_cast<TO*>(g.C);
+        constexpr int NP = TN / 2, ODD = TN & 1;
+        constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID;
+        using PA = typename std::conditional<EPI == EPI_RESID, float, T>::type;
+        typedef PA pa8 __attribute__((ext_vector_type(8)));
+        typedef PA pa4 __attribute__((ext_vector_type(4)));
+        const int mb = m0 + wm * WM + fr;
+        const int nb = n0 + wn * WN;
+        pa8 p8[PRE ? TM : 1][NP > 0 ? NP : 1];
+        pa4 p4[PRE && ODD ? TM : 1];
+        if constexpr (PRE) {
+            const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
+#pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) p8[a][q] = *reinterpret_cast<const pa8*>(src + ro + q * 32 + fg * 8);
+                if constexpr (ODD) p4[a] = *reinterpret_cast<const pa4*>(src + ro + NP * 32 + fg * 4);
+            }
+        }
+        float bv[NP > 0 ? NP : 1][8], bo[4];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            if (g.bias) load8f<float>(g.bias + nb + q * 32 + fg * 8, bv[q]);
+            else for (int i = 0; i < 8; ++i) bv[q][i] = 0.f;
+        }
+        if constexpr (ODD) {
+            if (g.bias) load4<float>(g.bias + nb + NP * 32 + fg * 4, bo);
+            else for (int i = 0; i < 4; ++i) bo[i] = 0.f;
+        }
+        auto finish = [&](float* v, int w, const float* bias, const auto& pre, size_t off) {
+            for (int i = 0; i < w; ++i) v[i] += bias[i];
+            if constexpr (EPI == EPI_GELU) {
+                if (g.aux) {
+                    if (w == 8) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
+                    else store4<T>(reinterpret_cast<T*>(g.aux) + off, v);
+                }
+                for (int i = 0; i < w; ++i) v[i] = quick_gelu(v[i]);
+            } else if constexpr (EPI == EPI_GELU_BWD) {
+                for (int i = 0; i < w; ++i) v[i] *= quick_gelu_grad((float)pre[i]);
+            } else if constexpr (EPI == EPI_RESID) {
+                for (int i = 0; i < w; ++i) v[i] += pre[i];
+            }
+            if (w == 8) store8<TO>(C + off, v);
+            else store4<TO>(C + off, v);
+        };
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+            const int m = mb + a * 16;
+            if (m >= g.M) break;                 // rows ascend with a
+            const size_t ro = (size_t)m * g.N + nb;
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                float v[8] = {acc[a][2 * q][0], acc[a][2 * q][1], acc[a][2 * q][2], acc[a][2 * q][3],
+                              acc[a][2 * q + 1][0], acc[a][2 * q + 1][1], acc[a][2 * q + 1][2], acc[a][2 * q + 1][3]};
+                if constexpr (PRE) finish(v, 8, bv[q], p8[a][q], ro + q * 32 + fg * 8);
+                else finish(v, 8, bv[q], 0, ro + q * 32 + fg * 8);
+            }
+            if constexpr (ODD) {
+                float v[4] = {acc[a][TN - 1][0], acc[a][TN - 1][1], acc[a][TN - 1][2], acc[a][TN - 1][3]};
+                if constexpr (PRE) finish(v, 4, bo, p4[a], ro + NP * 32 + fg * 4);
+                else finish(v, 4, bo, 0, ro + NP * 32 + fg * 4);
+            }
+        }
+    } else {
     // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i].
     // Staged through LDS in passes of EPR rows (row pitch BN+4 floats: conflict-free b128 writes),
     // then every thread finishes 8 consecutive columns of a row: coalesced 16-B loads of resid/aux
@@ -546,6 +651,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             g.stats[((size_t)tm * 2 + 1) * g.N + n0 + tid] = col_q;
         }
     }
+    }   // staged epilogue (MODE 1 / 2)
 }
 
 template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0>
@@ -582,7 +688,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 struct TileCfg { int id, bm, bn; };
 constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {6, 256, 128},
                             {7, 256, 256}, {8, 128, 64}, {9, 128, 128}, {10, 256, 128}, {11, 192, 128}, {12, 128, 64},
-                            {13, 128, 96}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128}};
+                            {13, 128, 96}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128},
+                            {32, 256, 96}};
 const TileCfg* find_cfg(int id) {
     for (const TileCfg& c : CFGS) if (c.id == id) return &c;
     return nullptr;
@@ -618,8 +725,9 @@ int pick_cfg(int M, int N, int K, bool wide) {
     if (N % 96 == 0 && N < 2048 && K >= 2048) return 13;
     return 2;
 }
+inline bool split_cfg(int id) { return id == 20 || id == 21 || id == 32; }
 int pick_splits(int M, int N, int K, const TileCfg& c, int bk) {
-    if (c.id != 20 && c.id != 21) return 1;
+    if (!split_cfg(c.id)) return 1;
     const long tiles = ntiles(M, N, c.bm, c.bn);
     int s = 1;
     // more splits while the grid stays within ~1.2 waves of CUs and each slice keeps >= 512 of K
@@ -636,8 +744,9 @@ int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
     if (!c || g.N % c->bn != 0 || (cfg >= 8 && !SIXTEEN)) cfg = 0;
     if (cfg == 0) cfg = pick_cfg(g.M, g.N, g.K, SIXTEEN);
     c = find_cfg(cfg);
-    const int bk = cfg >= 20 ? 32 : 128 / E::BYTES;
-    int splits = forced_splits() > 0 ? forced_splits() : (cfg >= 20 ? pick_splits(g.M, g.N, g.K, *c, bk) : 1);
+    const bool r64 = cfg >= 20 && cfg < 30;                   // 64-B K rows (4-stage rings)
+    const int bk = r64 ? 32 : 128 / E::BYTES;
+    int splits = forced_splits() > 0 ? forced_splits() : pick_splits(g.M, g.N, g.K, *c, bk);
     if (splits > 1) {
         const int tiles = ((g.M + c->bm - 1) / c->bm) * (g.N / c->bn);
         const size_t need = GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
@@ -671,6 +780,7 @@ int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
             case 21: return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64>(g, st);
             case 22: return launch_gemm<E, TO, EPI, 128, 256, 4, 2, 4, 64>(g, st);
             case 24: return launch_gemm<E, TO, EPI, 128, 128, 4, 2, 2, 64>(g, st);
+            case 32: return launch_gemm<E, TO, EPI, 256, 96, 3, 4, 2>(g, st);
         }
     }
     return EBC_E_UNSUPPORTED;
@@ -721,9 +831,11 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
     if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;
     return N % 96 == 0 ? 13 : 2;
 }
+int forced_conv_splits() { static const int v = env_int("EBC_CONV_SPLITS"); return v; }
 int conv_splits(int cfg, int mode, int M, int N, int nk)
 {
     if (mode != 2) return 1;
+    if (const int f = forced_conv_splits()) return (f >= 1 && nk % f == 0) ? f : 1;
     const TileCfg* c = find_cfg(cfg);
     const long tiles = ntiles(M, N, c->bm, c->bn);
     int s = 1;
@@ -810,7 +922,8 @@ size_t gemm_workspace_bytes(int dtype, int M, int N, int K)
     if (!c || N % c->bn != 0) cfg = pick_cfg(M, N, K, true);
     c = find_cfg(cfg);
     if (cfg < 20) return 0;
-    const int splits = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, 32);
+    const int bk = cfg < 30 ? 32 : (dtype == EBC_F32 ? 32 : 64);
+    const int splits = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, bk);
     if (splits <= 1) return 0;
     const size_t tiles = (size_t)((M + c->bm - 1) / c->bm) * (N / c->bn);
     return GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
@@ -831,6 +944,101 @@ int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void*
     return EBC_E_ARG;
 }
 }  // namespace ebc
+
+namespace {
+// weight-gradient GEMM: 128x64 tiles, K split so that the grid is about one wave of CUs
+int wgrad_splits(int M, int N, int K, int bk) {
+    const long tiles = ntiles(M, N, 128, 64);
+    const int nk = K / bk;
+    int s = 1;
+    for (int c = 2; c <= 16; ++c)
+        if (tiles * c <= NUM_CU * 6 / 5 && nk % c == 0 && nk / c >= 8) s = c;
+    return s;
+}
+size_t wgrad_ws(int M, int N, int K, int bk) {
+    const int s = wgrad_splits(M, N, K, bk);
+    return s > 1 ? GEMM_CNT_BYTES + (size_t)s * ntiles(M, N, 128, 64) * 128 * 64 * 4 : 0;
+}
+template <class E>
+int wgrad_launch(GemmArgs g, void* ws, size_t wsb, hipStream_t st) {
+    constexpr int bk = 128 / E::BYTES;
+    int s = wgrad_splits(g.M, g.N, g.K, bk);
+    if (s > 1 && (!ws || wsb < wgrad_ws(g.M, g.N, g.K, bk) || ntiles(g.M, g.N, 128, 64) > (long)(GEMM_CNT_BYTES / 4)))
+        return EBC_E_ARG;
+    if (s > 1) {
+        g.cnt = reinterpret_cast<int*>(ws);
+        g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
+    }
+    g.splits = s;
+    g.kslice = g.K / s;
+    return launch_gemm<E, float, EPI_STORE, 128, 64, 2>(g, st);
+}
+
+// out[c][r] = in[r][c]: 64x64 tiles through LDS, 8-element (16 B for 16-bit) vectors both ways
+template <class T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in, T* __restrict__ out, int R, int C, long ldo)
+{
+    __shared__ T sm[64][64 + 2];
+    const int t = threadIdx.x, r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    typedef T t8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = t + 256 * k, rl = e >> 3, cl = (e & 7) * 8;
+        if (r0 + rl < R && c0 + cl < C) {
+            const t8 v = *reinterpret_cast<const t8*>(in + (size_t)(r0 + rl) * C + c0 + cl);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sm[rl][cl + i] = v[i];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = t + 256 * k, cl = e >> 3, rl = (e & 7) * 8;
+        if (c0 + cl < C && r0 + rl < R) {
+            t8 v;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = sm[rl + i][cl];
+            *reinterpret_cast<t8*>(out + (size_t)(c0 + cl) * ldo + r0 + rl) = v;
+        }
+    }
+}
+}  // namespace
+
+extern "C" size_t ebc_gemm_wgrad_workspace_bytes(int dtype, int M, int N, int K)
+{
+    if (M <= 0 || N <= 0 || K <= 0) return 0;
+    return wgrad_ws(M, N, K, dtype == EBC_F32 ? 32 : 64);
+}
+
+extern "C" int ebc_gemm_wgrad(int dtype, const void* A, const void* B, float* C, int M, int N, int K,
+                              void* workspace, size_t workspace_bytes, ebc_stream_t stream)
+{
+    const int bk = dtype == EBC_F32 ? 32 : 64;
+    if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || K % bk || N % 64) return EBC_E_ARG;
+    GemmArgs g{A, B, C, nullptr, nullptr, nullptr, M, N, K};
+    const hipStream_t st = (hipStream_t)stream;
+    switch (dtype) {
+        case EBC_F32: return wgrad_launch<EF32>(g, workspace, workspace_bytes, st);
+        case EBC_F16: return wgrad_launch<EF16>(g, workspace, workspace_bytes, st);
+        case EBC_BF16: return wgrad_launch<EBF16>(g, workspace, workspace_bytes, st);
+    }
+    return EBC_E_ARG;
+}
+
+extern "C" int ebc_transpose(int dtype, const void* in, void* out, int R, int C, long ld_out, ebc_stream_t stream)
+{
+    if (!in || !out || R <= 0 || C <= 0 || R % 8 || C % 8 || ld_out < R || ld_out % 8) return EBC_E_ARG;
+    const dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
+    const hipStream_t st = (hipStream_t)stream;
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, st, (const float*)in, (float*)out, R, C, ld_out); break;
+        case EBC_F16: hipLaunchKernelGGL(transpose_kernel<_Float16>, grid, dim3(256), 0, st, (const _Float16*)in, (_Float16*)out, R, C, ld_out); break;
+        case EBC_BF16: hipLaunchKernelGGL(transpose_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)in, (__bf16*)out, R, C, ld_out); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
 
 extern "C" int ebc_gemm(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
                         const float* bias, const float* resid, void* aux, int M, int N, int K,

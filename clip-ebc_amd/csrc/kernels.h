@@ -33,6 +33,9 @@ int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg
 int im2col(int dtype, const float* x, void* out, int B, int H, int W, int P, hipStream_t st);
 int embed_tokens(const float* patch, const float* cls, const float* pos, const float* gamma, const float* beta,
                  const float* vpt, long vpt_bstride, float* X, int B, int L, int G, int NVPT, int D, hipStream_t st);
+// ln_1 with the deep-VPT rows taken from the prompt (and written into X): replaces insert_vpt + layernorm_fwd
+int layernorm_fwd_vpt(int dtype, float* X, const float* vpt, long vpt_bstride, int L, int NVPT, const float* gamma,
+                      const float* beta, void* out, float* mean, float* rstd, int M, int D, hipStream_t st);
 int insert_vpt(float* X, const float* vpt, long vpt_bstride, int B, int L, int NVPT, int D, hipStream_t st);
 int vpt_grad(int dtype, float* dX, void* dXt, float* dvpt, int B, int L, int NVPT, int D, int per_batch, int accumulate,
              hipStream_t st);

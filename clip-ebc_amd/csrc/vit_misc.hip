@@ -75,18 +75,36 @@ __device__ __forceinline__ void ln_row(float4 (&v)[NV], const float* gamma, cons
     }
 }
 
+// deep-VPT insert fused into ln_1 (model.py:131-140, 161-168): rows 1..NV of every crop are read from
+// the prompt (vpt + b * bstride + (l-1) * D) instead of X, and written into X for the residual path
+struct VptIns {
+    const float* vpt;       // null: plain LayerNorm
+    long bstride;
+    int L, NV;
+    float* X;
+};
+
 template <class T, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, RowMap map, const float* gamma,
                                                      const float* beta, T* out, float* outf, float* mean_out,
-                                                     float* rstd_out, int M)
+                                                     float* rstd_out, int M, VptIns vi)
 {
     constexpr int D = 256 * NV;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (r >= M) return;
     const float* xr = x + map(r) * D;
+    bool ins = false;
+    if (vi.vpt) {
+        const int b = r / vi.L, l = r - b * vi.L;
+        if (l >= 1 && l <= vi.NV) { xr = vi.vpt + b * vi.bstride + (size_t)(l - 1) * D; ins = true; }
+    }
     float4 v[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const float4*>(xr + 4 * lane + 256 * i);
+    if (ins) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) *reinterpret_cast<float4*>(vi.X + (size_t)r * D + 4 * lane + 256 * i) = v[i];
+    }
     float mean, rstd;
     ln_row<NV>(v, gamma, beta, mean, rstd);
 #pragma unroll
@@ -202,25 +220,53 @@ __global__ void insert_vpt_kernel(float* X, const float* vpt, long vpt_bstride, 
 }
 
 // dvpt[r, c] (+)= sum_b dX[b, 1+r, c]  (or per batch when per_batch), then zero those rows of dX / dXt.
+// Block = 64 column groups of 4 x 4 crop lanes for one 256-column chunk of prompt row r: crop lane bl sums
+// crops bl, bl+4, ... (all its loads in flight at once), the 4 lane sums meet in LDS in lane order.
 template <class T>
-__global__ void vpt_grad_kernel(float* dX, T* dXt, float* dvpt, int B, int L, int NVPT, int D, int per_batch, int accumulate)
+__global__ __launch_bounds__(256) void vpt_grad_kernel(float* __restrict__ dX, T* __restrict__ dXt,
+                                                       float* __restrict__ dvpt, int B, int L, int NVPT, int D,
+                                                       int per_batch, int accumulate)
 {
-    const int total = NVPT * D;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-        const int r = e / D, c = e % D;
-        float s = 0.f;
-        for (int b = 0; b < B; ++b) {
+    __shared__ float4 red[4][64];
+    const int cg = threadIdx.x & 63, bl = threadIdx.x >> 6;
+    const int chunks = D / 256, r = blockIdx.x / chunks, c = (blockIdx.x - r * chunks) * 256 + 4 * cg;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s = z;
+    constexpr int MAXB = 16;                      // crops per lane held in registers per pass
+    for (int b0 = bl; b0 < B; b0 += 4 * MAXB) {
+        float4 x[MAXB];
+#pragma unroll
+        for (int k = 0; k < MAXB; ++k) {
+            const int b = b0 + 4 * k;
+            x[k] = b < B ? *reinterpret_cast<const float4*>(dX + ((size_t)b * L + 1 + r) * D + c) : z;
+        }
+#pragma unroll
+        for (int k = 0; k < MAXB; ++k) {
+            const int b = b0 + 4 * k;
+            if (b >= B) continue;
             const size_t o = ((size_t)b * L + 1 + r) * D + c;
             if (per_batch) {
-                float* dst = dvpt + (size_t)b * total + e;
-                *dst = accumulate ? *dst + dX[o] : dX[o];
+                float4* dst = reinterpret_cast<float4*>(dvpt + ((size_t)b * NVPT + r) * D + c);
+                float4 y = x[k];
+                if (accumulate) { const float4 d = *dst; y.x += d.x; y.y += d.y; y.z += d.z; y.w += d.w; }
+                *dst = y;
             } else {
-                s += dX[o];
+                s.x += x[k].x; s.y += x[k].y; s.z += x[k].z; s.w += x[k].w;
             }
-            dX[o] = 0.f;
-            if (dXt) dXt[o] = (T)0.f;
+            *reinterpret_cast<float4*>(dX + o) = z;
+            if (dXt) st4<T>(dXt + o, z);
         }
-        if (!per_batch) dvpt[e] = accumulate ? dvpt[e] + s : s;
+    }
+    if (per_batch) return;
+    red[bl][cg] = s;
+    __syncthreads();
+    if (bl == 0) {
+        float4 t = red[0][cg];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) { const float4 u = red[k][cg]; t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w; }
+        float4* dst = reinterpret_cast<float4*>(dvpt + (size_t)r * D + c);
+        if (accumulate) { const float4 d = *dst; t.x += d.x; t.y += d.y; t.z += d.z; t.w += d.w; }
+        *dst = t;
     }
 }
 
@@ -404,20 +450,35 @@ inline int grid_for(size_t n, int block = 256) {
 // ------------------------------------------------------------------------------- launchers
 namespace ebc {
 
+static int ln_fwd_launch(int dtype, const float* x, RowMap map, const float* gamma, const float* beta, void* out,
+                         float* outf, float* mean, float* rstd, int M, VptIns vi, hipStream_t st)
+{
+    const dim3 grid((M + 3) / 4);
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL((ln_fwd_kernel<float, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (float*)out, outf, mean, rstd, M, vi); break;
+        case EBC_F16: hipLaunchKernelGGL((ln_fwd_kernel<_Float16, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (_Float16*)out, outf, mean, rstd, M, vi); break;
+        case EBC_BF16: hipLaunchKernelGGL((ln_fwd_kernel<__bf16, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (__bf16*)out, outf, mean, rstd, M, vi); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
 int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,
                   void* out, float* outf, float* mean, float* rstd, int M, int D, hipStream_t st)
 {
     if (D != 768 || M <= 0) return EBC_E_UNSUPPORTED;
     const RowMap map{rpg > 0 ? rpg : M, gstride, goff};
-    const dim3 grid((M + 3) / 4);
-    switch (dtype) {
-        case EBC_F32: hipLaunchKernelGGL((ln_fwd_kernel<float, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (float*)out, outf, mean, rstd, M); break;
-        case EBC_F16: hipLaunchKernelGGL((ln_fwd_kernel<_Float16, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (_Float16*)out, outf, mean, rstd, M); break;
-        case EBC_BF16: hipLaunchKernelGGL((ln_fwd_kernel<__bf16, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (__bf16*)out, outf, mean, rstd, M); break;
-        default: return EBC_E_ARG;
-    }
-    EBC_CHECK_LAUNCH();
-    return EBC_OK;
+    return ln_fwd_launch(dtype, x, map, gamma, beta, out, outf, mean, rstd, M, VptIns{nullptr, 0, 1, 0, nullptr}, st);
+}
+
+int layernorm_fwd_vpt(int dtype, float* X, const float* vpt, long vpt_bstride, int L, int NVPT, const float* gamma,
+                      const float* beta, void* out, float* mean, float* rstd, int M, int D, hipStream_t st)
+{
+    if (D != 768 || M <= 0 || L <= NVPT || M % L) return EBC_E_UNSUPPORTED;
+    const RowMap map{M, 0, 0};
+    return ln_fwd_launch(dtype, X, map, gamma, beta, out, nullptr, mean, rstd, M,
+                         VptIns{vpt, vpt_bstride, L, NVPT, X}, st);
 }
 
 template <class T>
@@ -481,11 +542,12 @@ int insert_vpt(float* X, const float* vpt, long vpt_bstride, int B, int L, int N
 
 int vpt_grad(int dtype, float* dX, void* dXt, float* dvpt, int B, int L, int NVPT, int D, int per_batch, int accumulate, hipStream_t st)
 {
-    const int n = NVPT * D;
+    if (D % 256 || NVPT <= 0 || B <= 0) return NVPT == 0 ? EBC_OK : EBC_E_UNSUPPORTED;
+    const dim3 grid((unsigned)(NVPT * (D / 256)));
     switch (dtype) {
-        case EBC_F32: hipLaunchKernelGGL(vpt_grad_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, dX, (float*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
-        case EBC_F16: hipLaunchKernelGGL(vpt_grad_kernel<_Float16>, dim3(grid_for(n)), dim3(256), 0, st, dX, (_Float16*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
-        case EBC_BF16: hipLaunchKernelGGL(vpt_grad_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, st, dX, (__bf16*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
+        case EBC_F32: hipLaunchKernelGGL(vpt_grad_kernel<float>, grid, dim3(256), 0, st, dX, (float*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
+        case EBC_F16: hipLaunchKernelGGL(vpt_grad_kernel<_Float16>, grid, dim3(256), 0, st, dX, (_Float16*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
+        case EBC_BF16: hipLaunchKernelGGL(vpt_grad_kernel<__bf16>, grid, dim3(256), 0, st, dX, (__bf16*)dXt, dvpt, B, L, NVPT, D, per_batch, accumulate); break;
         default: return EBC_E_ARG;
     }
     EBC_CHECK_LAUNCH();

@@ -37,6 +37,9 @@ SIGNATURES = {
     "ebc_gemm": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "ebc_gemm_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "ebc_gemm_ws": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _Z, _P]),
+    "ebc_gemm_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "ebc_gemm_wgrad": (_I, [_I, _P, _P, _P, _I, _I, _I, _P, _Z, _P]),
+    "ebc_transpose": (_I, [_I, _P, _P, _I, _I, _L, _P]),
     "ebc_vit_workspace_bytes": (_Z, [_I, _I, _I, _I, _I, _I, _I]),
     "ebc_vit_forward": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_long, _I, _I, _P, _Z, _P, _P]),
     "ebc_vit_backward": (_I, [_P, _I, _I, _I, _I, _P, _Z, _P, _P, ctypes.c_long, _P]),

@@ -260,7 +260,21 @@ class _HeadFn(torch.autograd.Function):
         dY = torch.empty(P, C, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dZ), _lib.ptr(Wt), _lib.ptr(dY), None, None, None,
                               P, C, EMBED, _lib.stream()), "ebc_gemm(projection dX)")
-        dW = torch.mm(dZ.t(), Y).float().reshape(wshape)         # dW = dZ^T Y (library GEMM, K = B*H*W)
+        # dW = dZ^T Y over K = B*H*W pixels: both operands transposed to K-contiguous, split-K MFMA GEMM
+        # (K padded with zero columns to the GEMM's K step when B*H*W is not a multiple of it)
+        kstep = 32 if cdtype == torch.float32 else 64
+        Pp = -(-P // kstep) * kstep
+        alloc = torch.empty if Pp == P else torch.zeros
+        dZT = alloc(EMBED, Pp, device=dev, dtype=cdtype)
+        YT = alloc(C, Pp, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_transpose(dt, _lib.ptr(dZ), _lib.ptr(dZT), P, EMBED, Pp, _lib.stream()), "ebc_transpose(dZ)")
+        _lib.check(L.ebc_transpose(dt, _lib.ptr(Y), _lib.ptr(YT), P, C, Pp, _lib.stream()), "ebc_transpose(Y)")
+        dW = torch.empty(EMBED, C, device=dev, dtype=torch.float32)
+        nb = L.ebc_gemm_wgrad_workspace_bytes(dt, EMBED, C, Pp)
+        ws = _dec_workspace(dev, nb, slot=2)
+        _lib.check(L.ebc_gemm_wgrad(dt, _lib.ptr(dZT), _lib.ptr(YT), _lib.ptr(dW), EMBED, C, Pp, _lib.ptr(ws), ws.numel(),
+                                    _lib.stream()), "ebc_gemm_wgrad(projection dW)")
+        dW = dW.reshape(wshape)
         dy = dY.view(B, Hh, Ww, C) if nhwc else dY.view(B, Hh, Ww, C).permute(0, 3, 1, 2).to(ydt)
         return dy, dW, dbias, dscale.reshape(()), None, None, None, None
 
@@ -276,7 +290,7 @@ _SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
 
 def _dec_workspace(dev: torch.device, nbytes: int, slot: int = 0) -> Tensor:
     """Stream-owned scratch of the decoder calls (slot 0: the caller's stream, slot 1: the side stream of the
-    weight-gradient GEMMs); its first 16 KiB (split-K counters) start zeroed."""
+    weight-gradient GEMMs, slot 2: the projection's dW GEMM); its first 16 KiB (split-K counters) start zeroed."""
     ws = _DEC_WS.get((dev, slot))
     if ws is None or ws.numel() < nbytes:
         ws = torch.zeros(max(nbytes, 1 << 20), device=dev, dtype=torch.uint8)

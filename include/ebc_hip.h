@@ -86,6 +86,16 @@ size_t ebc_gemm_workspace_bytes(int dtype, int M, int N, int K);
 int ebc_gemm_ws(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
                 const float* bias, const float* resid, void* aux, int M, int N, int K,
                 void* workspace, size_t workspace_bytes, ebc_stream_t stream);
+/* Weight-gradient GEMM for a long reduction (K = pixels), f32 output:  C[M,N] = A[M,K] . B[N,K]^T
+ * with A, B in `dtype` (K-contiguous: the transposed activations / output gradients).  Replaces the
+ * projection's dW = dZ^T Y of models/clip/model.py:91-95 (nn.Conv2d 1x1 backward).  Splits K over
+ * workgroups (deterministic last-arriver sum); `workspace` as for ebc_gemm_ws. */
+size_t ebc_gemm_wgrad_workspace_bytes(int dtype, int M, int N, int K);
+int ebc_gemm_wgrad(int dtype, const void* A, const void* B, float* C, int M, int N, int K,
+                   void* workspace, size_t workspace_bytes, ebc_stream_t stream);
+/* out[c][r] = in[r][c] for in [R][C] (16-bit or f32 elements; R, C and the output row stride ld_out >= R
+ * multiples of 8): the K-contiguous operand copies for ebc_gemm_wgrad. */
+int ebc_transpose(int dtype, const void* in, void* out, int R, int C, long ld_out, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * CLIP ViT-B/16 + deep VPT encoder: CLIP_EBC._forward_vpt (models/clip/model.py:142-189), whole

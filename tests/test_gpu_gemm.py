@@ -156,3 +156,40 @@ def test_gemm_split_k(dname, M, N, K, epi):
     torch.cuda.synchronize()
     if nbytes:
         assert int(ws[:16384].view(torch.int32).abs().sum()) == 0, "split-K counters not re-armed"
+
+
+@pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
+@pytest.mark.parametrize("R,C,ld", [(12544, 512, 12544), (1568, 768, 1600), (8, 64, 8)])
+def test_transpose_exact(dname, R, C, ld):
+    dt = DT[dname]
+    x = torch.randn(R, C, device="cuda").to(dt)
+    out = torch.full((C, ld), 7.0, device="cuda", dtype=dt)
+    _lib.check(_lib.lib().ebc_transpose(_lib.dtype_code(dt), _lib.ptr(x), _lib.ptr(out), R, C, ld, _lib.stream()),
+               "ebc_transpose")
+    assert torch.equal(out[:, :R], x.t())
+    assert bool((out[:, R:] == 7.0).all())                   # padding columns untouched
+
+
+@pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 12544), (512, 768, 1600), (128, 64, 64), (300, 192, 2048)])
+def test_gemm_wgrad(dname, M, N, K):
+    """Projection dW (split-K, deterministic last-arriver sum) vs fp64, and run-to-run bit equality."""
+    dt = DT[dname]
+    if K % (32 if dname == "f32" else 64):
+        pytest.skip()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + K)
+    A = torch.randn(M, K, device="cuda", generator=g).to(dt)
+    B = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(dt)
+    L = _lib.lib()
+    nb = L.ebc_gemm_wgrad_workspace_bytes(_lib.dtype_code(dt), M, N, K)
+    ws = torch.zeros(max(nb, 16), device="cuda", dtype=torch.uint8)
+    outs = []
+    for _ in range(2):
+        C = torch.empty(M, N, device="cuda")
+        _lib.check(L.ebc_gemm_wgrad(_lib.dtype_code(dt), _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), M, N, K, _lib.ptr(ws),
+                                    ws.numel(), _lib.stream()), "ebc_gemm_wgrad")
+        outs.append(C)
+    ref = A.double() @ B.double().t()
+    assert _rel(outs[0], ref) < TOL[dname]
+    assert torch.equal(outs[0], outs[1])
+    assert int(ws[:16 * 1024].count_nonzero()) == 0          # split-K counters re-armed

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Experiment builds of libebc_hip.so for GEMM bottleneck analysis (tools/gemm_bench.py with
-# EBC_LIB_PATH=clip-ebc_amd/lib/exp<m>/libebc_hip.so):  1 = no MFMA, 2 = no global->LDS loads, 3 = neither.
+# EBC_LIB_PATH=clip-ebc_amd/lib/exp<m>/libebc_hip.so):  1 = no MFMA, 2 = no global->LDS loads, 4 = no epilogue (bits combine).
 set -e
 cd "$(dirname "$0")/../clip-ebc_amd"
 for m in "$@"; do
