@@ -688,8 +688,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 struct TileCfg { int id, bm, bn; };
 constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {6, 256, 128},
                             {7, 256, 256}, {8, 128, 64}, {9, 128, 128}, {10, 256, 128}, {11, 192, 128}, {12, 128, 64},
-                            {13, 128, 96}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128},
-                            {32, 256, 96}};
+                            {13, 128, 96}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128}};
 const TileCfg* find_cfg(int id) {
     for (const TileCfg& c : CFGS) if (c.id == id) return &c;
     return nullptr;
@@ -725,7 +724,8 @@ int pick_cfg(int M, int N, int K, bool wide) {
     if (N % 96 == 0 && N < 2048 && K >= 2048) return 13;
     return 2;
 }
-inline bool split_cfg(int id) { return id == 20 || id == 21 || id == 32; }
+// r01: a split-K 256x96 tile (3-stage ring) for the N = 768 products measured 20-25 % slower than cfg 13
+inline bool split_cfg(int id) { return id == 20 || id == 21; }
 int pick_splits(int M, int N, int K, const TileCfg& c, int bk) {
     if (!split_cfg(c.id)) return 1;
     const long tiles = ntiles(M, N, c.bm, c.bn);
@@ -780,7 +780,6 @@ int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
             case 21: return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64>(g, st);
             case 22: return launch_gemm<E, TO, EPI, 128, 256, 4, 2, 4, 64>(g, st);
             case 24: return launch_gemm<E, TO, EPI, 128, 128, 4, 2, 2, 64>(g, st);
-            case 32: return launch_gemm<E, TO, EPI, 256, 96, 3, 4, 2>(g, st);
         }
     }
     return EBC_E_UNSUPPORTED;
@@ -828,6 +827,8 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
         const TileCfg* c = find_cfg(f);
         if (c && N % c->bn == 0 && (f == 2 || f == 3 || f == 13 || f == 20 || f == 21)) return f;
     }
+    // r01: 160x256 tiles (237 instead of 196 tiles at M = 16*784, N = 768) measured only 2-3 % faster on the
+    // forward convs (their 80x64 wave tiles lose per-CU throughput), not kept
     if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;
     return N % 96 == 0 ? 13 : 2;
 }
@@ -922,7 +923,7 @@ size_t gemm_workspace_bytes(int dtype, int M, int N, int K)
     if (!c || N % c->bn != 0) cfg = pick_cfg(M, N, K, true);
     c = find_cfg(cfg);
     if (cfg < 20) return 0;
-    const int bk = cfg < 30 ? 32 : (dtype == EBC_F32 ? 32 : 64);
+    const int bk = 32;
     const int splits = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, bk);
     if (splits <= 1) return 0;
     const size_t tiles = (size_t)((M + c->bm - 1) / c->bm) * (N / c->bn);
