@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crops", type=int, default=8, help="crops per CPU-baseline step")
     ap.add_argument("--cpu-steps", type=int, default=12)
+    ap.add_argument("--eval", action="store_true",
+                    help="SURVEY §8(d) config 5 instead: sliding-window eval of 2048x3072 images (window = stride = 224, "
+                         "140 tiles per image, tiles sharded over ranks); --steps images timed; --dtype fp32 is the "
+                         "reference's own eval precision")
     return ap.parse_args()
 
 
@@ -153,6 +157,55 @@ def setup(args, rank, world, local, device):
     return step
 
 
+def run_eval(args, rank, world, device):
+    """Config 5: images/s and tiles/s of ebc_amd.eval_utils.sliding_window_predict (utils/eval_utils.py:26-96) on
+    QNRF-shaped synthetic images; the timed region includes the tile gather, the forward, the cross-rank tile
+    gather and the overlap assembly + D2H copy the reference's API returns."""
+    from ebc_amd.eval_utils import sliding_window_predict, tile_grid
+    from ebc_amd.model import get_model
+    torch.manual_seed(42)
+    model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
+                      vpt_drop=0.0, deep_vpt=True).to(device).eval()
+    H, W = 2048, 3072
+    g = np.random.Generator(np.random.PCG64(7))                 # one image, its tiles sharded over the ranks
+    mean = np.array([0.485, 0.456, 0.406], np.float32).reshape(1, 3, 1, 1)
+    std = np.array([0.229, 0.224, 0.225], np.float32).reshape(1, 3, 1, 1)
+    img = torch.from_numpy(((g.random((1, 3, H, W), dtype=np.float32) - mean) / std).astype(np.float32)).to(device)
+    rows, cols = tile_grid(H, W, (224, 224), (224, 224))
+    amp_dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.dtype]
+
+    def one():
+        with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
+            return sliding_window_predict(model, img, 224, 224)
+
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    if rank == 0:
+        tiles = rows * cols
+        print(json.dumps({
+            "metric": "eval tiles/s clip_vit_b_16 sliding window 2048x3072 (window 224, stride 224)",
+            "value": round(tiles * args.steps / elapsed, 2), "unit": "tiles/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_image": round(elapsed / args.steps * 1e3, 3),
+            "images_per_s": round(args.steps / elapsed, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (uniform pixels, ImageNet-normalised)",
+            "config": {"workload": f"SURVEY §8(d) config 5: {tiles} tiles per image sharded over {world} rank(s)",
+                       "tiles_per_image": tiles, "density_map": list(out.shape)}}), flush=True)
+
+
 def committed_traffic(dtype):
     """HBM bytes per launch of the probe kernel from the committed PMC passes (FETCH_SIZE x2 gfx950
     correction + WRITE_SIZE, profiles/r01_gemm_fc_traffic.json); None when no profile matches."""
@@ -180,6 +233,11 @@ def main():
         dist.init_process_group(backend, device_id=torch.device(f"cuda:{dev_index}") if backend == "nccl" else None)
     torch.cuda.set_device(dev_index)
     device = torch.device(f"cuda:{dev_index}")
+    if args.eval:
+        run_eval(args, rank, world, device)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     step = setup(args, rank, world, local, device)
     B = args.crops_per_gpu
 
