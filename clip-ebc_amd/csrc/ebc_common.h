@@ -17,16 +17,38 @@
 
 namespace ebc {
 
+// Wave-wide reductions on DPP (VALU lane moves) instead of __shfl_xor, which hipcc lowers to six
+// ds_bpermute LDS round trips each followed by lgkmcnt(0): quad xor-1 / xor-2, row half-mirror and
+// row mirror leave every lane with its 16-lane row's total, row_bcast:15 / row_bcast:31 fold the
+// four rows into lane 63, and readlane broadcasts it (the result is wave-uniform).  Every lane of
+// the wave must be active.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_rows(float v, float old) {  // rows outside ROWS keep `old`
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                                 CTRL, ROWS, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
+    v += dpp_rows<0x142, 0xA>(v, 0.f);
+    v += dpp_rows<0x143, 0xC>(v, 0.f);
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, dpp_mov<0xB1>(v));
+    v = fmaxf(v, dpp_mov<0x4E>(v));
+    v = fmaxf(v, dpp_mov<0x141>(v));
+    v = fmaxf(v, dpp_mov<0x140>(v));
+    v = fmaxf(v, dpp_rows<0x142, 0xA>(v, -INFINITY));
+    v = fmaxf(v, dpp_rows<0x143, 0xC>(v, -INFINITY));
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 __device__ __forceinline__ int wave_or(int v) {
