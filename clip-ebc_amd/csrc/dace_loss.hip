@@ -30,7 +30,7 @@ using namespace ebc;
 
 namespace {
 
-constexpr int NT = 512;                  // threads per workgroup (8 waves, 2 per SIMD)
+constexpr int NT = 1024;                 // threads per workgroup (16 waves, 4 per SIMD)
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
@@ -41,7 +41,7 @@ template <int G> struct Cfg {
     // in LDS (KSPLIT x GG) and are summed by the consumer (no atomics: LDS float atomics run at
     // ~3 cycles per lane).
     static constexpr int NB = (G / 4) * (G / 4);
-    static constexpr int KSPLIT = NT / NB;
+    static constexpr int KSPLIT = 512 / NB;            // (sized for 512 threads: the dense fallback's LDS partials)
     // home buckets of the sorted Sinkhorn: one per BSxBS cell block; a <= 9-cell window starting in
     // block B reaches block B + HALO
     static constexpr int BS = 4, NB1 = G / BS, NBK = NB1 * NB1, HALO = 8 / BS;
