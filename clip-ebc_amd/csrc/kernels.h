@@ -36,6 +36,13 @@ int embed_tokens(const float* patch, const float* cls, const float* pos, const f
 // ln_1 with the deep-VPT rows taken from the prompt (and written into X): replaces insert_vpt + layernorm_fwd
 int layernorm_fwd_vpt(int dtype, float* X, const float* vpt, long vpt_bstride, int L, int NVPT, const float* gamma,
                       const float* beta, void* out, float* mean, float* rstd, int M, int D, hipStream_t st);
+// ln_1 backward that routes the prompt rows' gradient to vpt_rows [B][NVPT][D] (and zeroes them in dx_out /
+// dx_out_t): replaces layernorm_bwd + vpt_grad; vpt_sum then reduces the per-crop rows over the batch for
+// every layer in one launch
+int layernorm_bwd_vpt(int dtype, const void* dy, const float* x, const float* mean, const float* rstd,
+                      const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, int D, float* vpt_rows,
+                      int L, int NVPT, hipStream_t st);
+int vpt_sum(const float* rows, float* const* dst, int layers, int B, int NVPT, int D, hipStream_t st);
 int insert_vpt(float* X, const float* vpt, long vpt_bstride, int B, int L, int NVPT, int D, hipStream_t st);
 int vpt_grad(int dtype, float* dX, void* dXt, float* dvpt, int B, int L, int NVPT, int D, int per_batch, int accumulate,
              hipStream_t st);

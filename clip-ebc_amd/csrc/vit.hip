@@ -47,6 +47,7 @@ struct Layout {
     float *patch_f, *mpost, *rpost;
     // backward transients
     float *dXa, *dXb, *delta;
+    float* vpt_rows;                // [layers][B][NV][768] per-crop prompt gradients (summed over crops at the end)
     void *dXt, *dH, *dA, *dO, *dQKV;
     void* gws;                      // split-K GEMM workspace (leading counter block zeroed per call)
     size_t gws_bytes;
@@ -94,7 +95,10 @@ Layout carve(void* ws, int B, int L, int G, int layers, int dtype, int training)
         lay.dA = c.take<void>(M * MLP * es);
         lay.dO = c.take<void>(M * WIDTH * es);
         lay.dQKV = c.take<void>(M * QKVW * es);
+        const int NV = L - 1 - G;
+        lay.vpt_rows = NV > 0 ? c.take<float>((size_t)layers * B * NV * WIDTH * 4) : nullptr;
     } else {
+        lay.vpt_rows = nullptr;
         lay.dXa = lay.dXb = lay.delta = nullptr;
         lay.dXt = lay.dH = lay.dA = lay.dO = lay.dQKV = nullptr;
     }
@@ -263,14 +267,20 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dXt, p.wt_out, lay.dO, nullptr, M, WIDTH, WIDTH));
         EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st));
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dQKV, p.wt_qkv, lay.dH, nullptr, M, WIDTH, QKVW));
-        EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, lay.X[l], 0, 0, 0, s.m1, s.r1, p.ln1_g, dX, dXo, lay.dXt, M, WIDTH, st));
-        { float* t = dX; dX = dXo; dXo = t; }
-        // prompt rows: dvpt_l = sum_b dX[b, 1..NV]; they were replaced at this block's input, so the
-        // previous block's output gets zero gradient there (deep VPT).  Shallow VPT: only layer 0.
+        // prompt rows (deep VPT; shallow VPT: layer 0 only): ln_1's backward routes their gradient to the
+        // per-crop rows (straight into dvpt_l when it is per crop) and zeroes them in the token stream,
+        // since the prompt replaced them at this block's input
         if (NV > 0 && dvpt && dvpt[l]) {
-            EBC_TRY(ebc::vpt_grad(dtype, dX, lay.dXt, dvpt[l], B, L, NV, WIDTH, per_batch, 0, st));
+            float* rows = per_batch ? dvpt[l] : lay.vpt_rows + (size_t)l * B * NV * WIDTH;
+            EBC_TRY(ebc::layernorm_bwd_vpt(dtype, lay.dH, lay.X[l], s.m1, s.r1, p.ln1_g, dX, dXo, lay.dXt, M, WIDTH,
+                                           rows, L, NV, st));
+        } else {
+            EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, lay.X[l], 0, 0, 0, s.m1, s.r1, p.ln1_g, dX, dXo, lay.dXt, M, WIDTH, st));
         }
+        { float* t = dX; dX = dXo; dXo = t; }
     }
+    // dvpt_l = sum over crops of the prompt rows, every layer in one launch (shared prompts)
+    if (NV > 0 && dvpt && !per_batch) EBC_TRY(ebc::vpt_sum(lay.vpt_rows, dvpt, layers, B, NV, WIDTH, st));
     return EBC_OK;
 }
 

@@ -117,10 +117,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 }
 
 // dx_out = dx_in + LN'(dy):  rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
+// deep-VPT gradient fused into ln_1's backward (model.py:131-140): rows 1..NV of every crop are the
+// gradient of that layer's prompt tokens; they go to rows[(b*NV + l-1)*D] and the token-stream
+// gradient of those rows (dx_out, dx_out_t) becomes zero (the prompt replaced them at this layer's input)
+struct VptOut {
+    float* rows;            // null: plain LayerNorm backward
+    int L, NV;
+};
+
 template <class T, class DY, int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, const float* __restrict__ x, RowMap map,
                                                      const float* mean_in, const float* rstd_in, const float* gamma,
-                                                     const float* dx_in, float* dx_out, T* dx_out_t, int M)
+                                                     const float* dx_in, float* dx_out, T* dx_out_t, int M, VptOut vo)
 {
     constexpr int D = 256 * NV;
     constexpr float inv = 1.0f / (float)D;
@@ -152,9 +160,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
             const float4 a = *reinterpret_cast<const float4*>(dx_in + xr + c);
             o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
         }
+        if (vo.rows) {
+            const int b = r / vo.L, l = r - b * vo.L;
+            if (l >= 1 && l <= vo.NV) {
+                *reinterpret_cast<float4*>(vo.rows + ((size_t)b * vo.NV + l - 1) * D + c) = o;
+                o = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
         *reinterpret_cast<float4*>(dx_out + xr + c) = o;
         if (dx_out_t) st4<T>(dx_out_t + xr + c, o);
     }
+}
+
+// dvpt_l[r][c] = sum_b rows_l[b][r][c] for every layer l with a destination (crop order), one launch
+struct VptSum {
+    float* dst[64];
+};
+__global__ void vpt_sum_kernel(const float* __restrict__ rows, VptSum vs, int layers, int B, int n4)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;        // float4 index within one layer's [NV][D]
+    const int l = blockIdx.y;
+    if (e >= n4 || !vs.dst[l]) return;
+    const float4* src = reinterpret_cast<const float4*>(rows) + (size_t)l * B * n4 + e;
+    float4 acc = src[0];
+    for (int b = 1; b < B; ++b) {
+        const float4 v = src[(size_t)b * n4];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(vs.dst[l])[e] = acc;
 }
 
 // x [B,3,H,W] f32 -> patches [B*gh*gw, 3*P*P] (k = c*P*P + kh*P + kw, conv1 weight order)
@@ -483,13 +516,13 @@ int layernorm_fwd_vpt(int dtype, float* X, const float* vpt, long vpt_bstride, i
 
 template <class T>
 static int ln_bwd_t(int dy_f32, const void* dy, const float* x, RowMap map, const float* mean, const float* rstd,
-                    const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, hipStream_t st)
+                    const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, VptOut vo, hipStream_t st)
 {
     const dim3 grid((M + 3) / 4);
     if (dy_f32)
-        hipLaunchKernelGGL((ln_bwd_kernel<T, float, 3>), grid, dim3(256), 0, st, (const float*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M);
+        hipLaunchKernelGGL((ln_bwd_kernel<T, float, 3>), grid, dim3(256), 0, st, (const float*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M, vo);
     else
-        hipLaunchKernelGGL((ln_bwd_kernel<T, T, 3>), grid, dim3(256), 0, st, (const T*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M);
+        hipLaunchKernelGGL((ln_bwd_kernel<T, T, 3>), grid, dim3(256), 0, st, (const T*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M, vo);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -500,10 +533,11 @@ int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg
 {
     if (D != 768 || M <= 0) return EBC_E_UNSUPPORTED;
     const RowMap map{rpg > 0 ? rpg : M, gstride, goff};
+    const VptOut vo{nullptr, 1, 0};
     switch (dtype) {
-        case EBC_F32: return ln_bwd_t<float>(1, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, st);
-        case EBC_F16: return ln_bwd_t<_Float16>(dy_f32, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, st);
-        case EBC_BF16: return ln_bwd_t<__bf16>(dy_f32, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, st);
+        case EBC_F32: return ln_bwd_t<float>(1, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, vo, st);
+        case EBC_F16: return ln_bwd_t<_Float16>(dy_f32, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, vo, st);
+        case EBC_BF16: return ln_bwd_t<__bf16>(dy_f32, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, vo, st);
     }
     return EBC_E_ARG;
 }
@@ -528,6 +562,34 @@ int embed_tokens(const float* patch, const float* cls, const float* pos, const f
     if (D != 768 || L != 1 + NVPT + G) return EBC_E_ARG;
     hipLaunchKernelGGL(embed_kernel<3>, dim3((B * L + 3) / 4), dim3(256), 0, st, patch, cls, pos, gamma, beta, vpt,
                        vpt_bstride, X, B, L, G, NVPT);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+int layernorm_bwd_vpt(int dtype, const void* dy, const float* x, const float* mean, const float* rstd,
+                      const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, int D, float* vpt_rows,
+                      int L, int NVPT, hipStream_t st)
+{
+    if (D != 768 || M <= 0 || M % L || NVPT < 1 || NVPT >= L || !vpt_rows) return EBC_E_UNSUPPORTED;
+    const RowMap map{M, 0, 0};
+    const VptOut vo{vpt_rows, L, NVPT};
+    switch (dtype) {
+        case EBC_F32: return ln_bwd_t<float>(1, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, vo, st);
+        case EBC_F16: return ln_bwd_t<_Float16>(0, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, vo, st);
+        case EBC_BF16: return ln_bwd_t<__bf16>(0, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, vo, st);
+    }
+    return EBC_E_ARG;
+}
+
+int vpt_sum(const float* rows, float* const* dst, int layers, int B, int NVPT, int D, hipStream_t st)
+{
+    if (layers <= 0 || layers > 64 || B <= 0 || D % 4) return EBC_E_ARG;
+    VptSum vs{};
+    bool any = false;
+    for (int l = 0; l < layers; ++l) { vs.dst[l] = dst[l]; any |= dst[l] != nullptr; }
+    if (!any) return EBC_OK;
+    const int n4 = NVPT * D / 4;
+    hipLaunchKernelGGL(vpt_sum_kernel, dim3((n4 + 255) / 256, layers), dim3(256), 0, st, rows, vs, layers, B, n4);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

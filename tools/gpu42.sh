@@ -1,0 +1,7 @@
+# r01: VPT gradient fused into ln_1 backward + one batched crop sum
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_model.py tests/test_gpu_kernels.py tests/test_gpu_eval.py > gpurun_out/t42_tests.log 2>&1 || { tail -40 gpurun_out/t42_tests.log; exit 1; }
+tail -1 gpurun_out/t42_tests.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/t42_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/t42_prof.log 2>&1
