@@ -74,10 +74,11 @@ __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* bas
 }
 
 // ------------------------------------------------------------------------------ forward
-template <class E, int NWV>
+template <class E, int NWV, int LFIX>
 __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T* __restrict__ qkv, typename E::T* __restrict__ out,
-                                                       float* __restrict__ lse, int B, int L, int H, float scale)
+                                                       float* __restrict__ lse, int B, int L_, int H, float scale)
 {
+    const int L = LFIX > 0 ? LFIX : L_;                        // compile-time sequence: tile loops and masks fold
     using T = typename E::T;
     using C = AttnCfg<E>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -171,12 +172,13 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
 }
 
 // ------------------------------------------------------------------------------ backward dQ
-template <class E, int NWV>
+template <class E, int NWV, int LFIX>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                           const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                           float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                          int L, int H, float scale)
+                                                          int L_, int H, float scale)
 {
+    const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
     using C = AttnCfg<E>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -269,11 +271,12 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
 }
 
 // ------------------------------------------------------------------------------ backward dK, dV
-template <class E, int NWV>
+template <class E, int NWV, int LFIX>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                            const float* __restrict__ lse, const float* __restrict__ delta,
-                                                           typename E::T* __restrict__ dqkv, int B, int L, int H, float scale)
+                                                           typename E::T* __restrict__ dqkv, int B, int L_, int H, float scale)
 {
+    const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
     using C = AttnCfg<E>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -341,7 +344,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
             dv[dt] = mma(pf, load_colfrag<E>(Ds, C::LDR, 32 * st, 16 * dt), dv[dt]);
             dk[dt] = mma(dsf, load_colfrag<E>(Qs, C::LDR, 32 * st, 16 * dt), dk[dt]);
         }
-    }
+            }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int key = k0 + 4 * fg + i;
@@ -362,43 +365,48 @@ int attn_waves(int L) {
     return L > 128 ? 16 : 8;
 }
 
-template <class E, int NW> int attn_fwd_nw(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+// the CLIP ViT-B/16 + 32-prompt sequence (1 + 32 + 196 tokens) gets kernels compiled for it
+constexpr int L_VPT32 = 229;
+
+template <class E, int NW, int LFIX> int attn_fwd_nw(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
 {
     using C = AttnCfg<E>;
     const size_t lds = 2 * C::TILE_BYTES;
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)attn_fwd_kernel<E, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
+        if (hipFuncSetAttribute((const void*)attn_fwd_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
         attr = true;
     }
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
-    hipLaunchKernelGGL((attn_fwd_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
+    hipLaunchKernelGGL((attn_fwd_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
                        (typename E::T*)out, lse, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
 template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
 {
-    return attn_waves(L) == 16 ? attn_fwd_nw<E, 16>(qkv, out, lse, B, L, H, st) : attn_fwd_nw<E, 8>(qkv, out, lse, B, L, H, st);
+    if (attn_waves(L) == 16)
+        return L == L_VPT32 ? attn_fwd_nw<E, 16, L_VPT32>(qkv, out, lse, B, L, H, st) : attn_fwd_nw<E, 16, 0>(qkv, out, lse, B, L, H, st);
+    return attn_fwd_nw<E, 8, 0>(qkv, out, lse, B, L, H, st);
 }
 
-template <class E, int NW> int attn_bwd_nw(const void* qkv, const void* dout, const void* out, const float* lse,
-                                           float* delta, void* dqkv, int B, int L, int H, hipStream_t st)
+template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void* dout, const void* out, const float* lse,
+                                                     float* delta, void* dqkv, int B, int L, int H, hipStream_t st)
 {
     using C = AttnCfg<E>;
     const size_t lds_dq = 2 * C::TILE_BYTES, lds_kv = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<E, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dq) != hipSuccess) return EBC_E_LAUNCH;
-        if (hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<E, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv) != hipSuccess) return EBC_E_LAUNCH;
+        if (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dq) != hipSuccess) return EBC_E_LAUNCH;
+        if (hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv) != hipSuccess) return EBC_E_LAUNCH;
         attr = true;
     }
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds_dq, st, (const typename E::T*)qkv,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds_dq, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, (const typename E::T*)out, lse, delta, (typename E::T*)dqkv, B, L, H,
                        0.125f);
     EBC_CHECK_LAUNCH();
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, NW>), dim3(grid), dim3(64 * NW), lds_kv, st, (const typename E::T*)qkv,
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds_kv, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
@@ -406,8 +414,10 @@ template <class E, int NW> int attn_bwd_nw(const void* qkv, const void* dout, co
 template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
                                   void* dqkv, int B, int L, int H, hipStream_t st)
 {
-    return attn_waves(L) == 16 ? attn_bwd_nw<E, 16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st)
-                               : attn_bwd_nw<E, 8>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+    if (attn_waves(L) == 16)
+        return L == L_VPT32 ? attn_bwd_nw<E, 16, L_VPT32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st)
+                            : attn_bwd_nw<E, 16, 0>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+    return attn_bwd_nw<E, 8, 0>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
 }
 
 }  // namespace

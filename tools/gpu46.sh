@@ -1,0 +1,8 @@
+# r01: dK/dV loop fully unrolled for L = 229
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_kernels.py tests/test_gpu_model.py > gpurun_out/t46_tests.log 2>&1 || { tail -40 gpurun_out/t46_tests.log; exit 1; }
+tail -1 gpurun_out/t46_tests.log
+timeout -k 10 120 python tools/attn_bench.py 2>&1 | grep -v amdgpu.ids
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/t46_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/t46_prof.log 2>&1
