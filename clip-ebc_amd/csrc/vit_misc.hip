@@ -336,11 +336,15 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z,
     load_text(text, NB, tn, nullptr);
     const float s = expf(*logit_scale);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int pi = w; pi < PIX_PER_BLOCK; pi += 4) {
-        const int p = blockIdx.x * PIX_PER_BLOCK + pi;
+    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front
+    float vv[PPW][8];
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) load_pix<TZ>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        const int p = blockIdx.x * PIX_PER_BLOCK + w + 4 * j;
         if (p >= P) break;
-        float v[8];
-        load_pix<TZ>(Z + (size_t)p * CH, v);
+        float* v = vv[j];
         float ss = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
@@ -384,11 +388,15 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     float dsc = 0.f;
-    for (int pi = w; pi < PIX_PER_BLOCK; pi += 4) {
-        const int p = blockIdx.x * PIX_PER_BLOCK + pi;
+    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front
+    float vv[PPW][8];
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) load_pix<TZ>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+        const int p = blockIdx.x * PIX_PER_BLOCK + w + 4 * j;
         if (p >= P) break;
-        float v[8];
-        load_pix<TZ>(Z + (size_t)p * CH, v);
+        float* v = vv[j];
         float ss = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
