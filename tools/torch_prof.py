@@ -27,7 +27,7 @@ def main():
         step(i)
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True) as prof:
         for i in range(a.steps):
             step(10 + i)
         torch.cuda.synchronize()
@@ -38,6 +38,13 @@ def main():
     rows = [e for e in prof.key_averages(group_by_input_shape=True)
             if any(k in e.key for k in ("copy", "fill", "zero", "_to_copy", "clone", "cat", "stack", "flip", "Memcpy", "Memset"))]
     rows.sort(key=lambda e: -e.device_time_total)
+    print("\n== copy/fill ops by call stack")
+    for e in sorted(prof.key_averages(group_by_stack_n=6), key=lambda e: -e.device_time_total):
+        if not any(k in e.key for k in ("copy_", "fill_", "_to_copy", "clone", "cat")) or e.device_time_total <= 0:
+            continue
+        print(f"{e.device_time_total:10.1f} us  n={e.count:4d}  {e.key}")
+        for fr in (e.stack or [])[:6]:
+            print("        ", fr)
     print("\n== glue ops (per profiled window of %d steps)" % a.steps)
     for e in rows[:40]:
         print(f"{e.device_time_total:10.1f} us  n={e.count:4d}  {e.key[:40]:40s} {str(e.input_shapes)[:150]}")
