@@ -10,8 +10,9 @@
 // Design:
 //  * The DMCount cost is separable: C[i, iy*g+jx] = yd_i[iy] + xd_i[jx]
 //    (dm_loss.py:53-59), so K = exp(C/-reg) = Ey_i[iy] * Ex_i[jx] with Ey = exp(yd/-reg),
-//    Ex = exp(xd/-reg).  A crop's kernel matrix shrinks from n*g^2 to 2*n*g floats, which fits
-//    the 160 KiB LDS for n <= ~470 (g = 28) and streams from L2 above that.
+//    Ex = exp(xd/-reg).  A crop's kernel matrix shrinks from n*g^2 to 2*n*g floats; the bucketed
+//    path keeps only each point's 12-cell aligned window of Ey and Ex (2*n*12 floats), so a crop
+//    stays LDS-resident up to ~1200 points (g = 28); wide windows or more points stream from L2.
 //  * K^T u = (u*Ey)^T Ex is a dense [G x n] x [n x G] product, run as 4x4 register blocks over
 //    b128 LDS reads with the points split across thread groups (partials summed by the v pass).
 //  * exp(C/-reg) underflows to exactly 0 beyond ~32 px (reg = 10), so each point's factors are
@@ -45,11 +46,26 @@ template <int G> struct Cfg {
     // home buckets of the sorted Sinkhorn: one per BSxBS cell block; a <= 9-cell window starting in
     // block B reaches block B + HALO
     static constexpr int BS = 4, NB1 = G / BS, NBK = NB1 * NB1, HALO = 8 / BS;
-    // fixed LDS (floats): pd, td, b, v0, v1, partial[KSPLIT][GG], misc[64], bucket counts/starts
-    static constexpr int FIXED = 5 * GG + KSPLIT * GG + 64 + ((2 * NBK + 4 + 3) & ~3);
+    // fixed LDS (floats): pd, td, b, v0, v1, misc[64], bucket counts/starts, partial[KSPLIT][GG]
+    static constexpr int BKT = (2 * NBK + 4 + 3) & ~3;
+    static constexpr int FIXED = 5 * GG + 64 + BKT + KSPLIT * GG;
     static constexpr size_t FIXED_BYTES = (size_t)FIXED * 4;
     static constexpr int PER_POINT = 2 * G + 6;          // Ey, Ex (16-B aligned rows), u0, u1, window, key, x, y
+    // bucketed path: factor rows cut to the 12 cells from the window's 4-aligned start (clamped to
+    // G - 12): a <= 9-cell window starting at offset <= 3 fits, and a 4x4 block of any bucket that
+    // gathers the point lies at offset 0, 4 or 8.  It needs only GG of the partials, so its factors
+    // start at part + GG.
+    static constexpr int CW = 12;
+    static constexpr int PER_POINT_C = 2 * CW + 6;
+    static constexpr size_t FIXED_BYTES_C = (size_t)(5 * GG + 64 + BKT + GG) * 4;
 };
+
+// first cell of a point's compact factor row (window start lo, length len; 0 for an empty window)
+template <int G, int CW>
+__device__ __forceinline__ int row_base(int lo, int len) {
+    if constexpr (CW == G) return 0;
+    else return len ? min(lo & ~3, G - CW) : 0;
+}
 
 struct Params {
     const float* pred_class; const float* pred_density; const float* target_density;
@@ -61,7 +77,9 @@ struct Params {
     int max_iter, eval_freq;
     float* grad_class; float* grad_density; float* crop_stats; float* beta_out; int* status;
     float* ws_factors;     // global factor storage for crops that do not fit LDS
-    int lds_cap;           // max points kept in LDS
+    int lds_cap;           // max points kept in LDS with full factor rows (dense path)
+    int lds_cap_s;         // max points kept in LDS with full factor rows (bucketed path)
+    int lds_cap_c;         // max points kept in LDS with compact factor rows (bucketed path)
     unsigned long long* prof;   // diagnostics (EBC_DACE_PROF=1): per crop 16 counters, else null
 };
 
@@ -291,9 +309,10 @@ __device__ __forceinline__ float sum4_dpp(float x) {
 //    v = b / (K^T u + eps) for it (no LDS partials), so an iteration is two phases and two barriers:
 //    [K^T u, v] then [K v, u];
 //  * K v: 4 lanes per point, each lane <= 3 window rows read as three aligned 16-B chunks of v.
+// Factor rows are CW wide: G (full rows) or Cfg::CW (the 12 cells from row_base: compact).
 // Returns false (nothing iterated) when a window is wider than 9 cells; the caller then runs
 // sinkhorn_crop.  On return the factors, u (u0), windows and point coordinates (spts) are sorted.
-template <int G>
+template <int G, int CW>
 __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                                 const float* __restrict__ pts, float* Ey, float* Ex, float* u0, float* u1, int* win,
                                 int* key, float* spts, int* bk, const float* b, float* v0, float* v1, float* part,
@@ -346,12 +365,14 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
         const int slot = start[kk] + r;
         const float px = pts[2 * i], py = pts[2 * i + 1];
         const float x = pcoord(px, size, norm), y = pcoord(py, size, norm);
-        for (int k = 0; k < G; ++k) {
-            const float c = cood(k, size, norm);
-            const float yd = (-2.0f * (y * c) + y * y) + c * c;
-            const float xd = (-2.0f * (x * c) + x * x) + c * c;
-            Ey[slot * G + k] = expf(yd / -reg);
-            Ex[slot * G + k] = expf(xd / -reg);
+        const int w = tmpwin[i];
+        const int yb = row_base<G, CW>(w & 255, (w >> 8) & 255), xb = row_base<G, CW>((w >> 16) & 255, (w >> 24) & 255);
+        for (int k = 0; k < CW; ++k) {
+            const float cy = cood(yb + k, size, norm), cx = cood(xb + k, size, norm);
+            const float yd = (-2.0f * (y * cy) + y * y) + cy * cy;
+            const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
+            Ey[slot * CW + k] = expf(yd / -reg);
+            Ex[slot * CW + k] = expf(xd / -reg);
         }
         spts[2 * slot] = px;
         spts[2 * slot + 1] = py;
@@ -363,19 +384,25 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
     const float a = 1.0f / (float)n;
 
     // candidate ranges of block blk: home rows BY-HALO..BY, columns BX-HALO..BX (contiguous per row)
-    struct Ranges { int s[HALO + 1], pre[HALO + 2]; };
+    // (compact rows: bd[d][k] = first sorted index of home column hx0 + 1 + k in row d, so a
+    // candidate's home column -- hence its row base -- follows from its index without a load)
+    struct Ranges { int s[HALO + 1], pre[HALO + 2], bd[HALO + 1][HALO]; };
     auto ranges = [&](int blk, Ranges& R) {
-        const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1;
+        const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1, hx0 = max(BX - HALO, 0);
         R.pre[0] = 0;
 #pragma unroll
         for (int d = 0; d <= HALO; ++d) {
             const int hy = BY - HALO + d;
             int s0 = 0, e0 = 0;
-            if (hy >= 0) { s0 = start[hy * NB1 + max(BX - HALO, 0)]; e0 = start[hy * NB1 + BX + 1]; }
+            if (hy >= 0) { s0 = start[hy * NB1 + hx0]; e0 = start[hy * NB1 + BX + 1]; }
             R.s[d] = s0;
             R.pre[d + 1] = R.pre[d] + (e0 - s0);
+#pragma unroll
+            for (int k = 0; k < HALO; ++k) R.bd[d][k] = hy >= 0 ? start[hy * NB1 + min(hx0 + 1 + k, BX + 1)] : 0;
         }
     };
+    // row base of a home bucket coordinate (compact rows; the 4x4 block at 4*B reads offset 4*B - base)
+    auto hbase = [&](int h) { return CW == G ? 0 : min(C::BS * h, G - CW); };
     // 8 adjacent lanes per 4x4 block: lane kg takes candidates kg, kg+8, ... four at a time (all LDS
     // reads before the FMAs); the 16 block sums meet by DPP and lane kg keeps cells 2kg, 2kg+1
     constexpr int LPB = 8;
@@ -384,19 +411,30 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
         const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1, by = BY * 4, bx = BX * 4;
         float4 acc[4] = {};
         const int nc = R.pre[HALO + 1];
+        const int hx0 = max(BX - HALO, 0);
         for (int c0 = kg; c0 < nc; c0 += 4 * LPB) {
             float ui[4];
             float4 ey[4], ex[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int c = c0 + k * LPB;
-                int i = 0;
+                int i = 0, oy = by, ox = bx;
 #pragma unroll
                 for (int d = 0; d <= HALO; ++d)
-                    if (c >= R.pre[d] && c < R.pre[d + 1]) i = R.s[d] + c - R.pre[d];
+                    if (c >= R.pre[d] && c < R.pre[d + 1]) {
+                        i = R.s[d] + c - R.pre[d];
+                        if constexpr (CW != G) {
+                            int hx = hx0;
+#pragma unroll
+                            for (int q2 = 0; q2 < HALO; ++q2) hx += i >= R.bd[d][q2];
+                            oy = by - hbase(BY - HALO + d);
+                            ox = bx - hbase(hx);
+                        }
+                    }
+                if constexpr (CW != G) { if (c >= nc) { oy = 0; ox = 0; } }
                 ui[k] = c < nc ? uu[i] : 0.f;
-                ey[k] = *reinterpret_cast<const float4*>(&Ey[i * G + by]);
-                ex[k] = *reinterpret_cast<const float4*>(&Ex[i * G + bx]);
+                ey[k] = *reinterpret_cast<const float4*>(&Ey[i * CW + oy]);
+                ex[k] = *reinterpret_cast<const float4*>(&Ex[i * CW + ox]);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -491,7 +529,8 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
                 const int ylo = w & 255, ylen = (w >> 8) & 255, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
                 if (xlen) {
                     const int x4 = min(xlo & ~3, G - 12);
-                    const float* exr = Ex + i * G + x4;
+                    const float* exr = Ex + i * CW + x4 - row_base<G, CW>(xlo, xlen);
+                    const float* eyr = Ey + i * CW + ylo - row_base<G, CW>(ylo, ylen);
                     const float4 e0 = *reinterpret_cast<const float4*>(exr);
                     const float4 e1 = *reinterpret_cast<const float4*>(exr + 4);
                     const float4 e2 = *reinterpret_cast<const float4*>(exr + 8);
@@ -505,7 +544,7 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
                         sum = fmaf(e1.x, a1.x, sum); sum = fmaf(e1.y, a1.y, sum); sum = fmaf(e1.z, a1.z, sum);
                         sum = fmaf(e1.w, a1.w, sum); sum = fmaf(e2.x, a2.x, sum); sum = fmaf(e2.y, a2.y, sum);
                         sum = fmaf(e2.z, a2.z, sum); sum = fmaf(e2.w, a2.w, sum);
-                        acc = fmaf(Ey[i * G + ylo + r], sum, acc);
+                        acc = fmaf(eyr[r], sum, acc);
                     }
                 }
             }
@@ -553,7 +592,7 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
 }
 
 // Wasserstein distance sum(C * P) over the windows (dm_loss.py:77; reported, unused by training)
-template <int G, typename FP, typename IP>
+template <int G, int CW, typename FP, typename IP>
 __device__ float transport_cost(int n, int size, int norm, const float* pts, FP Ey, FP Ex, FP u, IP win,
                                 const float* v, int WY, float* misc)
 {
@@ -563,6 +602,7 @@ __device__ float transport_cost(int n, int size, int norm, const float* pts, FP 
         const int wi = win[i];
         if (r >= ((wi >> 8) & 255)) continue;
         const int iy = (wi & 255) + r, xlo = (wi >> 16) & 255, xlen = (wi >> 24) & 255;
+        const int yb = row_base<G, CW>(wi & 255, (wi >> 8) & 255), xb = row_base<G, CW>(xlo, xlen);
         const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
         const float c = cood(iy, size, norm);
         const float yd = (-2.0f * (y * c) + y * y) + c * c;
@@ -571,11 +611,11 @@ __device__ float transport_cost(int n, int size, int norm, const float* pts, FP 
             const int jx = xlo + k;
             const float cx = cood(jx, size, norm);
             const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
-            const float kv = Ex[i * G + jx] * v[iy * G + jx];
+            const float kv = Ex[i * CW + jx - xb] * v[iy * G + jx];
             t1 += kv;
             t2 = fmaf(kv, xd, t2);
         }
-        w += u[i] * Ey[i * G + iy] * (yd * t1 + t2);
+        w += u[i] * Ey[i * CW + iy - yb] * (yd * t1 + t2);
     }
     return block_sum(w, misc);
 }
@@ -591,10 +631,11 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     float* bb = td + GG;        // normed pred density (Sinkhorn b)
     float* v0 = bb + GG;
     float* v1 = v0 + GG;
-    float* part = v1 + GG;      // K^T u partials [KSPLIT][GG]
-    float* misc = part + C::KSPLIT * GG;
+    float* misc = v1 + GG;
     int* bkt = reinterpret_cast<int*>(misc + 64);             // sorted-Sinkhorn bucket counts / starts
-    float* fac = misc + 64 + ((2 * C::NBK + 4 + 3) & ~3);     // LDS factors (if they fit)
+    float* part = misc + 64 + C::BKT;                         // K^T u partials [KSPLIT][GG]
+    float* fac = part + C::KSPLIT * GG;                       // LDS factors, full rows (if they fit)
+    float* facc = part + GG;                                  // LDS factors, compact rows (bucketed path)
 
     const int p0 = P.offsets[b], n = P.offsets[b + 1] - p0;
     if (P.prof && t == 0) { for (int k = 0; k < 16; ++k) P.prof[b * 16 + k] = 0; P.prof[b * 16 + 6] = clock64(); P.prof[b * 16 + 5] = n; }
@@ -670,23 +711,9 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         // 4. Sinkhorn OT (dm_loss.py:49-77)
         if (n > 0) {
             const float* pts = P.points + 2 * (size_t)p0;
-            // Two inlined copies so each sees one address space for the factors: LDS-resident
-            // crops get ds_* accesses (a select between LDS and global would make them flat_*).
-            auto ot = [&](float* base, auto in_lds) {
-                float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
-                int* win = reinterpret_cast<int*>(u1 + n);
-                int* key = win + n;
-                float* spts = reinterpret_cast<float*>(key + n);
-                bool sorted = false;
-                if constexpr (decltype(in_lds)::value)
-                    sorted = sinkhorn_sorted<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
-                                                Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc, &iters,
-                                                &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr);
-                if (!sorted)
-                    sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
-                                     u1, win, bb, v0, v1, part, misc, &iters, &rolled, &err_last,
-                                     P.prof ? P.prof + b * 16 : nullptr);
-                const float* cpts = sorted ? spts : pts;
+            // Inlined copies so each sees one address space for the factors: LDS-resident crops get
+            // ds_* accesses (a select between LDS and global would make them flat_*).
+            auto post = [&](auto cw, auto Ey, auto Ex, auto u0, auto win, const float* cpts) {
                 if (P.prof && t == 0) P.prof[b * 16 + 8] = clock64();
                 const int WY = __float_as_int(misc[1]);
                 __syncthreads();
@@ -708,10 +735,39 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                     v1[j] = og;
                 }
                 ot_b = block_sum(ol, misc);
-                wd_b = transport_cost<G>(n, S, P.norm_cood, cpts, Ey, Ex, u0, win, v0, WY, misc);
+                wd_b = transport_cost<G, decltype(cw)::value>(n, S, P.norm_cood, cpts, Ey, Ex, u0, win, v0, WY, misc);
             };
-            if (n <= P.lds_cap) ot(fac, std::true_type{});
-            else ot(P.ws_factors + (size_t)C::PER_POINT * p0, std::false_type{});
+            // dense path (full rows; wide windows or too many points for the compact rows)
+            auto dense = [&](float* base, auto /*in_lds: one instantiation per address space*/) {
+                float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
+                int* win = reinterpret_cast<int*>(u1 + n);
+                sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
+                                 u1, win, bb, v0, v1, part, misc, &iters, &rolled, &err_last,
+                                 P.prof ? P.prof + b * 16 : nullptr);
+                post(std::integral_constant<int, G>{}, Ey, Ex, u0, win, pts);
+            };
+            // bucketed path in LDS: full factor rows while they fit (fewest VALU per candidate), else
+            // the compact 12-cell rows (a per-candidate row base, computed from its home bucket)
+            auto bucketed = [&](auto cw) {
+                constexpr int CW = decltype(cw)::value;
+                float* Ey = facc; float* Ex = Ey + n * CW; float* u0 = Ex + n * CW; float* u1 = u0 + n;
+                int* win = reinterpret_cast<int*>(u1 + n);
+                int* key = win + n;
+                float* spts = reinterpret_cast<float*>(key + n);
+                if (!sinkhorn_sorted<G, CW>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
+                                            Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc, &iters,
+                                            &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr))
+                    return false;
+                post(cw, Ey, Ex, u0, win, spts);
+                return true;
+            };
+            bool done = false;
+            if (n <= P.lds_cap_s) done = bucketed(std::integral_constant<int, G>{});
+            else if (n <= P.lds_cap_c) done = bucketed(std::integral_constant<int, C::CW>{});
+            if (!done) {
+                if (n <= P.lds_cap) dense(fac, std::true_type{});
+                else dense(P.ws_factors + (size_t)C::PER_POINT * p0, std::false_type{});
+            }
         } else {
             for (int j = t; j < GG; j += NT) v1[j] = 0.f;
             __syncthreads();
@@ -772,6 +828,8 @@ template <int G> int launch(const Params& P0, hipStream_t st)
     using C = Cfg<G>;
     Params P = P0;
     P.lds_cap = (int)((LDS_MAX - C::FIXED_BYTES) / (sizeof(float) * C::PER_POINT));
+    P.lds_cap_s = (int)((LDS_MAX - C::FIXED_BYTES_C) / (sizeof(float) * C::PER_POINT));
+    P.lds_cap_c = (int)((LDS_MAX - C::FIXED_BYTES_C) / (sizeof(float) * C::PER_POINT_C));
     static bool attr = false;
     if (!attr) {
         if (hipFuncSetAttribute((const void*)dace_loss_kernel<G>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX) != hipSuccess)

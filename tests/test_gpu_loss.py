@@ -72,8 +72,10 @@ def _oracle(pcl, pde, dens, pts, size, count_loss="dmcount"):
 @pytest.mark.parametrize("size,counts", [
     (224, None),                                  # lognormal ragged batch, 16 crops
     (224, [0, 0, 0, 0]),                          # empty crops: OT skipped (dm_loss.py:49)
-    (224, [600, 1, 2048, 473, 474, 475, 3]),      # around / above the LDS capacity (global factors)
+    (224, [600, 1, 2048, 473, 474, 475, 3]),      # above the full-row LDS capacity (468 points)
+    (224, [1202, 1203, 582, 583, 5]),             # g = 28 LDS capacities: compact rows 1202, full rows 582
     (448, [0, 130, 127, 129, 900, 2]),            # g = 56
+    (448, [722, 723, 183, 184]),                  # g = 56 LDS capacities: compact rows 722, full rows 183
 ])
 def test_dace_kernel_matches_oracle(size, counts):
     B = 16 if counts is None else len(counts)
