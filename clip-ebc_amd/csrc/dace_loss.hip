@@ -31,7 +31,10 @@ using namespace ebc;
 
 namespace {
 
-constexpr int NT = 1024;                 // threads per workgroup (16 waves, 4 per SIMD)
+#ifndef EBC_DACE_NT
+#define EBC_DACE_NT 1024
+#endif
+constexpr int NT = EBC_DACE_NT;          // threads per workgroup (16 waves, 4 per SIMD)
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
