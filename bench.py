@@ -47,6 +47,9 @@ def parse():
                     help="SURVEY §8(d) config 5 instead: sliding-window eval of 2048x3072 images (window = stride = 224, "
                          "140 tiles per image, tiles sharded over ranks); --steps images timed; --dtype fp32 is the "
                          "reference's own eval precision")
+    ap.add_argument("--augment", action="store_true",
+                    help="SURVEY §8f row f2 instead: the reference's training augmentation on device (RandomResizedCrop + "
+                         "flip + RandomApply(jitter, blur, noise) + normalise + dot maps), 16 images x 2 crops per step")
     return ap.parse_args()
 
 
@@ -157,6 +160,55 @@ def setup(args, rank, world, local, device):
     return step
 
 
+def run_augment(args, rank, device):
+    """Row f2: crops/s of ebc_amd.transforms.CropAugment (host parameter draws + label arithmetic + the
+    three augmentation launches + dot maps) for 16 NWPU-sized 1536x2048 images x num_crops 2 per step,
+    images pre-staged in HBM; the CPU baseline runs the oracle (torch CPU: the reference's own ops) on the
+    same crop plans."""
+    from ebc_amd.transforms import CropAugment
+    from oracle import augment_ref
+    H, W, NI, NC = 1536, 2048, 16, 2
+    g = torch.Generator().manual_seed(5 + rank)
+    imgs = [torch.rand(3, H, W, generator=g).to(device) for _ in range(NI)]
+    labels = [torch.rand(200, 2, generator=g) * torch.tensor([W, H], dtype=torch.float32) for _ in range(NI)]
+    aug = CropAugment()                                     # trainer.py:40-52 defaults
+    torch.manual_seed(rank)
+    for _ in range(args.warmup):
+        aug(imgs, labels, NC)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        aug(imgs, labels, NC)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # device-only share: the launches of one step between events
+    plans = [aug.plan_crop(i, H, W, labels[i].clone())[0] for i in range(NI) for _ in range(NC)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        aug.apply(imgs, plans)
+    e1.record()
+    torch.cuda.synchronize()
+    dev_ms = e0.elapsed_time(e1) / 10
+    if rank == 0:
+        cpu_imgs = [x.cpu() for x in imgs[:2]]
+        sample = [p for p in plans if p.image < 2]
+        t1 = time.perf_counter()
+        augment_ref.apply_plans(cpu_imgs, sample, (224, 224))
+        cpu_el = time.perf_counter() - t1
+        crops = NI * NC * args.steps
+        print(json.dumps({
+            "metric": "train-augment crops/s (RandomResizedCrop+flip+jitter+blur+noise+normalise+dot maps, trainer defaults)",
+            "value": round(crops / el, 2), "unit": "crops/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic 1536x2048 images in HBM, 200 points each",
+            "config": {"workload": f"{NI} images x {NC} crops -> 224x224 (SURVEY §8f f2)"},
+            "device_ms_per_step": round(dev_ms, 4),
+            "cpu_baseline": {"value": round(len(sample) / cpu_el, 2), "unit": "crops/s", "cores": torch.get_num_threads(),
+                             "kind": "port", "sample": f"{len(sample)} crops of the same plans through oracle/augment_ref.py "
+                                                       f"(torch CPU ops the reference's workers run); {cpu_el:.2f}s"}}), flush=True)
+
+
 def run_eval(args, rank, world, device):
     """Config 5: images/s and tiles/s of ebc_amd.eval_utils.sliding_window_predict (utils/eval_utils.py:26-96) on
     QNRF-shaped synthetic images; the timed region includes the tile gather, the forward, the cross-rank tile
@@ -233,6 +285,11 @@ def main():
         dist.init_process_group(backend, device_id=torch.device(f"cuda:{dev_index}") if backend == "nccl" else None)
     torch.cuda.set_device(dev_index)
     device = torch.device(f"cuda:{dev_index}")
+    if args.augment:
+        run_augment(args, rank, device)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.eval:
         run_eval(args, rank, world, device)
         if world > 1:

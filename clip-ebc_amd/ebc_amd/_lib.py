@@ -25,8 +25,25 @@ _F = ctypes.c_float
 _Z = ctypes.c_size_t
 _D = ctypes.c_double
 _L = ctypes.c_long
-_D = ctypes.c_double
-_L = ctypes.c_long
+
+
+class EbcCropDesc(ctypes.Structure):
+    """include/ebc_hip.h EbcCropDesc (one augmented training crop)."""
+    _fields_ = [("src_off", ctypes.c_int64), ("out_off", ctypes.c_int64), ("tmp_off", ctypes.c_int64),
+                ("src_h", ctypes.c_int32), ("src_w", ctypes.c_int32), ("top", ctypes.c_int32), ("left", ctypes.c_int32),
+                ("crop_h", ctypes.c_int32), ("crop_w", ctypes.c_int32), ("out_h", ctypes.c_int32), ("out_w", ctypes.c_int32),
+                ("flip", ctypes.c_int32), ("jitter_ops", ctypes.c_int32),
+                ("brightness", ctypes.c_float), ("contrast", ctypes.c_float), ("saturation", ctypes.c_float),
+                ("blur", ctypes.c_int32), ("noise", ctypes.c_int32),
+                ("saltiness", ctypes.c_float), ("spiciness", ctypes.c_float),
+                ("seed", ctypes.c_uint32), ("normalize", ctypes.c_int32)]
+
+
+class EbcAugConst(ctypes.Structure):
+    """include/ebc_hip.h EbcAugConst (passed by value)."""
+    _fields_ = [("mean", ctypes.c_float * 3), ("std", ctypes.c_float * 3), ("blur_k", ctypes.c_int32),
+                ("sigma_x", ctypes.c_float), ("sigma_y", ctypes.c_float)]
+
 
 # name -> (restype, argtypes); must mirror include/ebc_hip.h
 SIGNATURES = {
@@ -66,6 +83,8 @@ SIGNATURES = {
     "ebc_dec_transpose3": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_dec_prep_weights": (_I, [_I, _P, _P, _P, _I, _I, _P]),
     "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, EbcAugConst, _P]),
+    "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
 }
 
 

@@ -171,6 +171,43 @@ int ebc_tile_gather(const float* image, float* tiles, int C, int H, int W, int w
 int ebc_tile_assemble(const float* preds, float* out, int Cp, int H, int W, int wh, int ww, int sh, int sw,
                       int reduction, ebc_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Training-crop augmentation on device (the reference runs it on CPU in
+ * DataLoader workers, utils/data_utils.py:14-26).  One descriptor per output crop (device array);
+ * the host samples the random parameters with the reference's RNG calls:
+ *   crop window + resize  RandomResizedCrop / _crop / _resize (datasets/transforms.py:9-43,133-171):
+ *                         torch F.interpolate(bicubic, antialias=True) taps; src == NULL skips it
+ *   flip                  RandomHorizontalFlip (transforms.py:174-187), on the resize store
+ *   jitter_ops            ColorJitter order (transforms.py:190-201 -> torchvision ColorJitter):
+ *                         3 bits per slot, 1 brightness, 2 contrast, 3 saturation (hue unsupported)
+ *   blur                  GaussianBlur(kernel_size, sigma=(sx, sy)) (transforms.py:217-223), reflect pad
+ *   noise                 PepperSaltNoise (transforms.py:242-255), counter-based uniforms from `seed`
+ *   normalize             Normalize(ImageNet mean/std) (datasets/crowd.py:64,162)
+ * workspace: per crop tmp_off .. + max(3*crop_h*out_w, 3*out_h*out_w) floats (caller-assigned). */
+#define EBC_AUG_MAX_BLUR 31
+typedef struct {
+    int64_t src_off, out_off, tmp_off;   /* element offsets: source image [3][src_h][src_w], output [3][out_h][out_w], scratch */
+    int32_t src_h, src_w, top, left, crop_h, crop_w, out_h, out_w;
+    int32_t flip, jitter_ops;
+    float brightness, contrast, saturation;
+    int32_t blur, noise;
+    float saltiness, spiciness;
+    uint32_t seed;
+    int32_t normalize;
+} EbcCropDesc;
+typedef struct {
+    float mean[3], std[3];
+    int32_t blur_k;                      /* odd, <= EBC_AUG_MAX_BLUR */
+    float sigma_x, sigma_y;
+} EbcAugConst;
+/* max_crop_h / max_out_h: maxima over the descriptors (grid sizing) */
+int ebc_augment_crops(const float* src, const EbcCropDesc* desc, int n, int max_crop_h, int max_out_h, float* out,
+                      float* workspace, EbcAugConst k, ebc_stream_t stream);
+/* generate_density_map(label, H, W, sigma=None) (datasets/utils.py:11-28) for B crops: out [B][1][H][W]
+ * = 1 at (clamp(int y), clamp(int x)) of points [sum n, 2] (x, y), offsets [B+1] (device) */
+int ebc_point_map(const float* points, const int* offsets, int B, int H, int W, int max_points, float* out,
+                  ebc_stream_t stream);
+
 
 /* ------------------------------------------------------------------------------------------
  * Decoder BasicBlock (models/utils.py:254-303, cfg [768] for vit_b_16, models/clip/model.py:250-251)

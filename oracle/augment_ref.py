@@ -1,0 +1,113 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+CPU restatement of the reference's training-crop pixel pipeline, applied to the per-crop parameters
+that `ebc_amd.transforms.CropAugment.plan_crop` drew.  Pinning:
+  * crop + resize: `TF.resize(..., BICUBIC, antialias=True)` on a float tensor is torch's
+    `F.interpolate(mode="bicubic", antialias=True)` (the reference's dependency, called here directly),
+    `_crop` is a slice (datasets/transforms.py:9-43,133-171) -- pinned by torch itself;
+  * flip, normalise: exact (transforms.py:174-187, datasets/crowd.py:64,162);
+  * ColorJitter / GaussianBlur: torchvision's functional algorithms restated (adjust_brightness /
+    adjust_contrast / adjust_saturation / rgb_to_grayscale / _blend, gaussian_blur with reflect padding
+    and the outer-product kernel); torchvision is not importable here, so these two are
+    "parity unpinned" against the library itself (the restatement follows its published code);
+  * PepperSaltNoise: the reference's two `torch.where`s (transforms.py:242-255) over the same
+    counter-based uniforms the device draws (`hash_uniform`).
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+MEAN = (0.485, 0.456, 0.406)
+STD = (0.229, 0.224, 0.225)
+
+
+def hash_uniform(seed: int, n: int) -> np.ndarray:
+    """murmur3-finalised (seed ^ idx * 0x9E3779B9) -> 24-bit uniforms, as the device kernel."""
+    idx = np.arange(n, dtype=np.uint64)
+    h = (np.uint64(seed) ^ ((idx * np.uint64(0x9E3779B9)) & np.uint64(0xFFFFFFFF))) & np.uint64(0xFFFFFFFF)
+    m = np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & m
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & m
+    h ^= h >> np.uint64(16)
+    return ((h >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)).astype(np.float32)
+
+
+def resize(img: torch.Tensor, h: int, w: int) -> torch.Tensor:
+    """datasets/transforms.py:_resize pixels (TF.resize bicubic, antialias) for [3, H, W]."""
+    if img.shape[-2:] == (h, w):
+        return img
+    return F.interpolate(img[None], size=(h, w), mode="bicubic", align_corners=False, antialias=True)[0]
+
+
+def _gray(img):
+    r, g, b = img.unbind(dim=-3)
+    return (0.2989 * r + 0.587 * g + 0.114 * b).unsqueeze(dim=-3)
+
+
+def _blend(a, b, ratio):
+    return (ratio * a + (1.0 - ratio) * b).clamp(0, 1.0)
+
+
+def jitter(img, op, f):
+    """torchvision adjust_brightness (1) / adjust_contrast (2) / adjust_saturation (3) on float images."""
+    if op == 1:
+        return _blend(img, torch.zeros_like(img), f)
+    if op == 2:
+        mean = torch.mean(_gray(img), dim=(-3, -2, -1), keepdim=True)
+        return _blend(img, mean, f)
+    return _blend(img, _gray(img), f)
+
+
+def gaussian_blur(img, k: int, sx: float, sy: float):
+    """torchvision gaussian_blur(img, [k, k], [sx, sy]) for a float [3, H, W] tensor."""
+    def k1(s):
+        half = (k - 1) * 0.5
+        x = torch.linspace(-half, half, steps=k)
+        pdf = torch.exp(-0.5 * (x / s).pow(2))
+        return pdf / pdf.sum()
+    kern = k1(sy)[:, None] * k1(sx)[None, :]
+    kern = kern.expand(3, 1, k, k)
+    x = F.pad(img[None], [k // 2, k // 2, k // 2, k // 2], mode="reflect")
+    return F.conv2d(x, kern, groups=3)[0]
+
+
+def apply_plans(images: Sequence[torch.Tensor], plans, size, saltiness=1e-3, spiciness=1e-3, kernel_size=5,
+                sigma=(0.1, 5.0), normalize=True) -> torch.Tensor:
+    out = []
+    for p in plans:
+        img = images[p.image].float()
+        if p.pre_resize is not None:
+            img = resize(img, *p.pre_resize)
+        img = img[:, p.top:p.top + p.crop_h, p.left:p.left + p.crop_w]
+        img = resize(img, size[0], size[1])
+        if p.flip:
+            img = img.flip(-1)
+        for op, f in p.jitter:
+            img = jitter(img, op, f)
+        if p.blur:
+            img = gaussian_blur(img, kernel_size, sigma[0], sigma[1])
+        if p.noise:
+            u = torch.from_numpy(hash_uniform(p.seed, img.numel())).reshape(img.shape)
+            img = torch.where(u < saltiness, 1.0, img)
+            img = torch.where(u > 1 - spiciness, 0.0, img)
+        if normalize:
+            img = (img - torch.tensor(MEAN)[:, None, None]) / torch.tensor(STD)[:, None, None]
+        out.append(img)
+    return torch.stack(out)
+
+
+def density_map(label: torch.Tensor, h: int, w: int) -> torch.Tensor:
+    """datasets/utils.py:generate_density_map (:11-28), sigma = None."""
+    d = torch.zeros((1, h, w), dtype=torch.float32)
+    if len(label) > 0:
+        lab = label.long()
+        lab[:, 0] = lab[:, 0].clamp(min=0, max=w - 1)
+        lab[:, 1] = lab[:, 1].clamp(min=0, max=h - 1)
+        d[0, lab[:, 1], lab[:, 0]] = 1.0
+    return d
