@@ -1,4 +1,4 @@
-// Fused DACE / DMCount loss for gfx950: one 512-thread workgroup per crop, every Sinkhorn
+// Fused DACE / DMCount loss for gfx950: one 1024-thread workgroup per crop, every Sinkhorn
 // iteration on device, no host synchronisation.
 //
 // Reference: DACELoss.forward        losses/dace_loss.py:49-70  (+ _bin_count :42-47)
