@@ -718,10 +718,16 @@ int pick_cfg(int M, int N, int K, bool wide) {
     // r01 sweep: MLP c_fc / GELU' (N = 3072, K = 768): 256x192 27.6 / 31.9 us vs 34.3 / 37.0 (128x64);
     // QKV (N = 2304): 192x192 20.1 us vs 23.3 (256x192)
     if (N % 192 == 0 && N >= 3072 && K <= 1024 && ntiles(M, N, 256, 192) >= 160) return 3;
-    if (N % 192 == 0 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
+    // (not for N <= 768: the projection's dX, N = 768 / K = 512 over 16*784 rows, is 17.4 us on 128x64
+    // vs 24.3 us on 192x192, s5 sweep tools/gpu65.sh)
+    if (N % 192 == 0 && N > 768 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
+    // the 1x1 projection conv 768 -> 512 (f32 out, 16*784 rows): 128x128 18.9 us vs 23.3 us on 128x64
+    if (N % 128 == 0 && N <= 512 && K <= 1024 && ntiles(M, N, 128, 128) >= 256) return 1;
     // decoder 3x3 convs as implicit GEMM (M = B*784, K = 9*768): one wave of 256x192 tiles
     if (N % 192 == 0 && K >= 4096 && ntiles(M, N, 256, 192) >= 160) return 3;
-    if (N % 96 == 0 && N < 2048 && K >= 2048) return 13;
+    // s5 re-sweep (tools/gpu63.sh): the N = 768, K = 768 products (out-proj + residual, its dX) are also
+    // faster on 128x96 S3 than on 128x64: 13.6 -> 12.1 us / 9.1 -> 8.9 us
+    if (N % 96 == 0 && N < 2048 && K >= 768) return 13;
     return 2;
 }
 // r01: a split-K 256x96 tile (3-stage ring) for the N = 768 products measured 20-25 % slower than cfg 13

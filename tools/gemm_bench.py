@@ -13,6 +13,9 @@ SHAPES = [  # (name, N, K, epilogue)
     ("qkv", 2304, 768, 0), ("out+res", 768, 768, 2), ("fc+gelu", 3072, 768, 1), ("proj+res", 768, 3072, 2),
     ("bwd gelu'", 3072, 768, 3), ("bwd dH2", 768, 3072, 0), ("bwd dO", 768, 768, 0), ("bwd dH", 768, 2304, 0),
 ]
+if os.environ.get("GB_SET") == "proj":   # the 1x1 projection conv 768 -> 512 over B*784 pixels and its dX
+    M = int(os.environ.get("GB_M", 16 * 784))
+    SHAPES = [("proj", 512, 768, 0, 1), ("proj dX", 768, 512, 0, 0)]     # (.., f32 output)
 
 
 def timeit(fn, reps=50):
@@ -31,19 +34,20 @@ def main():
     L = _lib.lib()
     dt = torch.float16
     tot_e = tot_t = 0.0
-    for name, N, K, epi in SHAPES:
+    for name, N, K, epi, *of in SHAPES:
+        OUT_F32 = of[0] if of else 0
         A = torch.randn(M, K, device="cuda").to(dt)
         B = (torch.randn(N, K, device="cuda") / K ** 0.5).to(dt)
         bias = torch.randn(N, device="cuda")
         aux = torch.randn(M, N, device="cuda").to(dt)
-        C = torch.empty(M, N, device="cuda", dtype=torch.float32 if epi == 2 else dt)
+        C = torch.empty(M, N, device="cuda", dtype=torch.float32 if epi == 2 or OUT_F32 else dt)
         R = torch.randn(M, N, device="cuda")
 
         nb = L.ebc_gemm_workspace_bytes(1, M, N, K)
         ws = torch.zeros(max(nb, 16), device="cuda", dtype=torch.uint8)
 
         def ours():
-            _lib.check(L.ebc_gemm_ws(1, epi, 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), _lib.ptr(bias), _lib.ptr(R),
+            _lib.check(L.ebc_gemm_ws(1, epi, OUT_F32, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), _lib.ptr(bias), _lib.ptr(R),
                                      _lib.ptr(aux), M, N, K, _lib.ptr(ws), ws.numel(), _lib.stream()), "gemm")
 
         def theirs():
