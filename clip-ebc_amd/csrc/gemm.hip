@@ -714,6 +714,11 @@ int pick_cfg(int M, int N, int K, bool wide) {
     // (cfg 20-24) are correct but slower here (their epilogue and split fix-up dominate) and are
     // kept for forced runs only.
     if (!wide) return 2;
+    // many-tile shapes (the sliding-window eval batch: M = 140 tiles x 229 tokens = 32060 rows; s5 sweep
+    // tools/gpu72.sh): the 256-wide tiles win once they fill >= 1.5 waves of CUs -- qkv 161.6 -> 149.0 us,
+    // out-proj 88.1 -> 66.4, c_fc 236.0 -> 205.7 (256x256), c_proj 250.8 -> 173.4
+    if (N % 256 == 0 && N >= 3072 && K <= 1024 && ntiles(M, N, 256, 256) >= 384) return 7;
+    if (N % 192 == 0 && ntiles(M, N, 256, 192) >= 384) return 3;
     if (N % 192 == 0 && N % 256 != 0 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
     // r01 sweep: MLP c_fc / GELU' (N = 3072, K = 768): 256x192 27.6 / 31.9 us vs 34.3 / 37.0 (128x64);
     // QKV (N = 2304): 192x192 20.1 us vs 23.3 (256x192)
