@@ -14,6 +14,7 @@
 // The MFMA is issued "swapped" (weights as the A operand) so each lane ends with 4 consecutive
 // output columns of one row: vector epilogue loads/stores.
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "ebc_common.h"
@@ -48,6 +49,7 @@ struct GemmArgs {
     int cH = 0, cW = 0, cC = 0, cHp = 0, cWp = 0, kpi = 0;
     long cQs = 0, cG = 0;
     float* stats = nullptr;  // EPI_STATS: [ceil(M/BM)][2][N] per-tile column sums / sums of squares
+    int group_m = 0;         // > 1: tiles ordered in groups of group_m tile rows, column-major inside a group
     const void* aux2 = nullptr;   // EPI_ADD_RELU_GRAD: ReLU output y (mask y > 0): C = acc + gy * (y > 0)
 };
 
@@ -198,7 +200,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
     const int wg = xcd_remap(blockIdx.x, ntm * ntn * g.splits);
     const int tile = wg / g.splits, split = wg - tile * g.splits;   // a tile's splits are adjacent
-    const int tm = tile / ntn, tn = tile % ntn;
+    int tm = tile / ntn, tn = tile % ntn;
+    if (g.group_m > 1) {
+        // each XCD's contiguous run of tiles (xcd_remap) then covers a group_m-tall block of tile rows and a
+        // few tile columns instead of one or two whole tile rows: the B (weight) panels are fetched into
+        // fewer XCD L2s (the wide-N products re-fetched B once per XCD)
+        const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
+        const int gm = min(ntm - first, g.group_m), r = tile - grp * per;
+        tm = first + r % gm;
+        tn = r / gm;
+    }
     const int m0 = tm * BM, n0 = tn * BN;
 
     const T* A = reinterpret_cast<const T*>(g.A);
@@ -735,6 +746,19 @@ int pick_cfg(int M, int N, int K, bool wide) {
     if (N % 96 == 0 && N < 2048 && K >= 768) return 13;
     return 2;
 }
+// Tile order for the wide-N products (>= 12 tile columns): with the row-major order each XCD's 1/8 of the
+// tiles spans one or two whole tile rows, so every XCD fetches all of B (c_fc: 46 MB fetched for 10.4 MB
+// of operands, PMC).  Grouping tile rows makes the XCD blocks squarer: the L2-miss bytes
+// A*ntn*GM/C + B*ntm/GM (C = tiles per XCD) are minimal at GM = sqrt(C * BN / BM).
+int group_rows(int M, int N, int bm, int bn, int splits) {
+    static const int forced = env_int("EBC_GEMM_GROUP_M");      // tuning override (-1: row-major)
+    if (forced) return forced > 0 ? forced : 0;
+    const long ntm = (M + bm - 1) / bm, ntn = N / bn;
+    if (ntn < 12 || splits > 1) return 0;
+    const double C = (double)(ntm * ntn) / 8.0;
+    const int gm = (int)(sqrt(C * bn / bm) + 0.5);
+    return gm > 1 && gm < ntm ? gm : 0;
+}
 // r01: a split-K 256x96 tile (3-stage ring) for the N = 768 products measured 20-25 % slower than cfg 13
 inline bool split_cfg(int id) { return id == 20 || id == 21; }
 int pick_splits(int M, int N, int K, const TileCfg& c, int bk) {
@@ -770,6 +794,7 @@ int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
     }
     g.splits = splits;
     g.kslice = g.K / splits;
+    g.group_m = group_rows(g.M, g.N, c->bm, c->bn, splits);
     switch (cfg) {
         case 1: return launch_gemm<E, TO, EPI, 128, 128, 2>(g, st);
         case 2: return launch_gemm<E, TO, EPI, 128, 64, 2>(g, st);
