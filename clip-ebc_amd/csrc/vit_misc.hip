@@ -333,13 +333,13 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z,
                                                        const float* anchors, float* logits, float* expo, int P, int HW, int NB)
 {
     extern __shared__ __attribute__((aligned(16))) float tn[];
-    load_text(text, NB, tn, nullptr);
-    const float s = expf(*logit_scale);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front
-    float vv[PPW][8];
+    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front,
+    float vv[PPW][8];                                 // before the text normalisation (latencies overlap)
 #pragma unroll
     for (int j = 0; j < PPW; ++j) load_pix<TZ>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+    const float s = expf(*logit_scale);
+    load_text(text, NB, tn, nullptr);
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
         const int p = blockIdx.x * PIX_PER_BLOCK + w + 4 * j;
@@ -382,16 +382,16 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
     extern __shared__ __attribute__((aligned(16))) float tn[];
     float* dbias_l = tn + NB * CH;       // [4 waves][CH]
     float* dsc_l = dbias_l + 4 * CH;     // [4]
-    load_text(text, NB, tn, nullptr);
-    const float ls = *logit_scale, s = expf(ls);
-    const float gs = gscale ? *gscale : 1.0f;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float dsc = 0.f;
-    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front
-    float vv[PPW][8];
+    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front,
+    float vv[PPW][8];                                 // before the text normalisation (latencies overlap)
 #pragma unroll
     for (int j = 0; j < PPW; ++j) load_pix<TZ>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+    const float ls = *logit_scale, s = expf(ls);
+    const float gs = gscale ? *gscale : 1.0f;
+    load_text(text, NB, tn, nullptr);
+    float db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float dsc = 0.f;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
         const int p = blockIdx.x * PIX_PER_BLOCK + w + 4 * j;
