@@ -743,7 +743,10 @@ int pick_cfg(int M, int N, int K, bool wide) {
     if (N % 192 == 0 && K >= 4096 && ntiles(M, N, 256, 192) >= 160) return 3;
     // s5 re-sweep (tools/gpu63.sh): the N = 768, K = 768 products (out-proj + residual, its dX) are also
     // faster on 128x96 S3 than on 128x64: 13.6 -> 12.1 us / 9.1 -> 8.9 us
-    if (N % 96 == 0 && N < 2048 && K >= 768) return 13;
+    // with more than one wave of 128x96 tiles (32 crops per GPU, SURVEY config 4: M = 7328) the 2-stage ring
+    // wins: two workgroups fit a CU (56 KB of LDS instead of 84), s5 sweep tools/gpu78.sh: c_proj + residual
+    // 51.5 -> 44.2 us, out-proj 21.9 -> 18.9, dH2 44.2 -> 37.8, dH 33.2 -> 29.5
+    if (N % 96 == 0 && N < 2048 && K >= 768) return ntiles(M, N, 128, 96) > NUM_CU ? 5 : 13;
     return 2;
 }
 // Tile order for the wide-N products (>= 12 tile columns): with the row-major order each XCD's 1/8 of the
