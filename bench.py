@@ -3,17 +3,29 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--crops-per-gpu B] [--dtype fp16|bf16|fp32]
 
 One step = forward (autocast, like the reference train.py:36-40) + DACE/DMCount loss (on-device
-Sinkhorn) + backward + GradScaler/Adam step over the 11.3 M trainable parameters, on synthetic
-crops pre-staged in HBM (BASELINE.md "Synthetic inputs").  N > 1: one process per GPU under
-torch.distributed.run, DDP over RCCL with SyncBatchNorm as trainer.py:147; weak scaling (fixed
-crops per GPU).  Rank 0 prints ONE JSON line (see README / DESIGN.md §Measurement).
+Sinkhorn) + backward + GradScaler/Adam step over the 11.3 M trainable parameters, on synthetic crops
+pre-staged in HBM (BASELINE.md "Synthetic inputs": a distinct batch per step, seed 1000 + rank*100003 +
+step).  N = 1: BASELINE configs[2] (16 crops).  N > 1: one process per GPU, DDP over RCCL with
+SyncBatchNorm as trainer.py:147, BASELINE configs[3] (32 crops per GPU, weak scaling); `--gpus N`
+without a launcher starts `torch.distributed.run` itself (before this process touches the GPU).
+Rank 0 prints ONE JSON line:
+  value        crops/s over all ranks, K timed steps between barriers + device syncs, max over ranks
+  median_ms    median per-step time (HIP events on the step stream; BASELINE.md "Timing")
+  roofline     the step's dominant kernel by in-step time (every instrumented launch of a few extra steps
+               bracketed by HIP events on its own stream, ebc_probe_*): algorithmic FLOP per launch /
+               its average duration vs the dense fp16 MFMA peak; `kernels` lists the top classes, and
+               `sinkhorn` the loss kernel's algorithmic bytes / duration vs HBM peak
+  cpu_baseline the oracle's fp32 CPU step (oracle/ref.py) on the host cores, rank 0 at N = 1 only
+The timed region is bracketed by `ebc_marker` kernels, so a rocprofv3 trace of this command can be cut
+to exactly the timed steps (tools/kstats.py --window).
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -30,19 +42,22 @@ ANCHORS_NWPU = [0.0, 1.0, 2.0, 3.0, 4.21931]     # configs/reduction_8.json ["4"
 FLOP_PER_CROP = 135.63e9                          # 58.33 fwd + 77.30 bwd GFLOP
 MFMA_PEAK_TF = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.3}   # MI355X dense (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+METRIC = "train crops/sec clip_vit_b_16 224px @1/2/4/8 MI355X; MAE parity"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--crops-per-gpu", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--crops-per-gpu", type=int, default=None,
+                    help="default 16 at N = 1 (BASELINE configs[2]), 32 at N > 1 (configs[3]: 128 images x 2 crops / 8)")
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
-    ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled through")
+    ap.add_argument("--pool", type=int, default=64, help="distinct synthetic batches (cycled beyond that)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-crops", type=int, default=8, help="crops per CPU-baseline step")
-    ap.add_argument("--cpu-steps", type=int, default=12)
+    ap.add_argument("--cpu-crops", type=int, default=16, help="crops per CPU-baseline step (BASELINE.md: 16)")
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps after 3 warm-up (BASELINE.md)")
+    ap.add_argument("--no-probe", action="store_true", help="skip the instrumented in-step kernel timing pass")
     ap.add_argument("--eval", action="store_true",
                     help="SURVEY §8(d) config 5 instead: sliding-window eval of 2048x3072 images (window = stride = 224, "
                          "140 tiles per image, tiles sharded over ranks); --steps images timed; --dtype fp32 is the "
@@ -50,7 +65,23 @@ def parse():
     ap.add_argument("--augment", action="store_true",
                     help="SURVEY §8f row f2 instead: the reference's training augmentation on device (RandomResizedCrop + "
                          "flip + RandomApply(jitter, blur, noise) + normalise + dot maps), 16 images x 2 crops per step")
-    return ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.crops_per_gpu is None:
+        a.crops_per_gpu = 16 if a.gpus == 1 else 32
+    return a
+
+
+def relaunch(args) -> int:
+    """`--gpus N` outside a launcher: one rank per GPU under torch.distributed.run, started as a CHILD
+    process before this one has touched the GPU (trainer.py:237-242 spawns one process per GPU too)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def make_batch(B, rank, step, device):
@@ -62,10 +93,12 @@ def make_batch(B, rank, step, device):
 
 
 def cpu_baseline(args, crops, steps):
-    """The oracle (oracle/ref.py: torch-fp32 CPU restatement of the reference step) on host cores."""
+    """The oracle (oracle/ref.py: torch-fp32 CPU restatement of the reference step, pinned by the golden
+    fixtures) on the host cores: B = 16, 3 warm-up + 5 timed steps (BASELINE.md "CPU baseline")."""
     from oracle import ref
     from ebc_amd import synthetic as syn
     nthreads = torch.get_num_threads()
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     sd = syn.full_state(0, layers=12, include_text=False)
     p = ref.params_from_state(sd)
     train = [v for k, v in p.items() if v.requires_grad]
@@ -80,45 +113,16 @@ def cpu_baseline(args, crops, steps):
         loss.backward()
         opt.step()
 
-    step(0)                                                  # warm-up
+    for s in range(3):                                       # warm-up
+        step(s)
     t0 = time.perf_counter()
     for s in range(steps):
-        step(s + 1)
+        step(3 + s)
     dt = time.perf_counter() - t0
     return {"value": round(crops * steps / dt, 4), "unit": "crops/s", "cores": nthreads, "kind": "port",
-            "sample": f"{steps} steps x {crops} crops (fwd+DACE/DMCount+bwd+Adam, fp32, 12 layers) of the oracle "
-                      f"oracle/ref.py on {nthreads} host threads; {dt:.1f}s"}
-
-
-def probe_kernels(dtype, device, reps=50):
-    """Time the dominant encoder GEMM (MLP c_fc, M = 16*229) and the Sinkhorn loss kernel alone with
-    HIP events on the current stream; returns roofline entries."""
-    from ebc_amd import _lib
-    L = _lib.lib()
-    tdt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}[dtype]
-    M, N, K = 16 * 229, 3072, 768
-    A = torch.randn(M, K, device=device).to(tdt)
-    Bw = (torch.randn(N, K, device=device) / 28).to(tdt)
-    C = torch.empty(M, N, device=device, dtype=tdt)
-    aux = torch.empty(M, N, device=device, dtype=tdt)
-    bias = torch.zeros(N, device=device)
-    code = _lib.dtype_code(tdt)
-
-    def launch():
-        _lib.check(L.ebc_gemm(code, 1, 0, _lib.ptr(A), _lib.ptr(Bw), _lib.ptr(C), _lib.ptr(bias), None,
-                              _lib.ptr(aux), M, N, K, _lib.stream()), "probe gemm")
-    for _ in range(5):
-        launch()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        launch()
-    e1.record()
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / reps * 1e-3
-    flops = 2.0 * M * N * K
-    return {"kernel": "gemm_nt_kernel<f16,GELU> (MLP c_fc 3664x3072x768, aux store)", "avg_us": t * 1e6,
-            "achieved": flops / t / 1e12, "flops_per_launch": flops}
+            "sample": f"{steps} timed steps (after 3 warm-up) x {crops} crops of the oracle oracle/ref.py "
+                      f"(fwd + DACE/DMCount + bwd + Adam, fp32, 12 layers) on {nthreads} torch threads "
+                      f"({affinity} CPUs in the affinity mask); {dt:.1f}s"}
 
 
 def setup(args, rank, world, local, device):
@@ -127,21 +131,19 @@ def setup(args, rank, world, local, device):
     from ebc_amd.model import get_model
     from ebc_amd.losses import DACELoss
     model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
-                      vpt_drop=0.0, deep_vpt=True).to(device)
+                      vpt_drop=0.0, deep_vpt=True, weights_seed=0).to(device)
     model.train()
     if world > 1:
         from ebc_amd.distributed import wrap_ddp       # SyncBatchNorm + DDP, as trainer.py:147
         model = wrap_ddp(model, device.index)
     loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=224).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
-    try:
-        opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
-    except Exception:
-        opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4)
+    opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
     amp_dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.dtype]
     scaler = torch.amp.GradScaler("cuda", enabled=args.dtype == "fp16")
     B = args.crops_per_gpu
-    pool = [make_batch(B, rank, s, device) for s in range(args.pool)]
+    npool = min(args.pool, args.warmup + args.steps)
+    pool = [make_batch(B, rank, s, device) for s in range(npool)]
     info_buf = torch.zeros(5, device=device)
 
     def step(i):
@@ -157,9 +159,92 @@ def setup(args, rank, world, local, device):
         torch.stack([info[k] for k in ("loss", "ot_loss", "tv_loss", "count_loss", "ce_loss")], out=info_buf)
         if world > 1:
             dist.all_reduce(info_buf)
+    step.pool = pool
     return step
 
 
+# ----------------------------------------------------------------------------- in-step kernel timing
+def _attn_flops(B, L, H, d=64):
+    # algorithmic products per launch: fwd QK^T + PV; bwd dQ kernel dP + dQ, dK/dV kernel dK + dV
+    return 4.0 * B * H * L * L * d
+
+
+def probe_steps(step, first, n, device, counts_of):
+    """Run n extra steps with every instrumented launch bracketed by HIP events (ebc_probe_*); returns the
+    per-step kernel classes sorted by time, and the Sinkhorn roofline entry."""
+    from ebc_amd import _lib
+    L = _lib.lib()
+    cap = 8192
+    torch.cuda.synchronize()
+    _lib.check(L.ebc_probe_begin(cap), "ebc_probe_begin")
+    for i in range(n):
+        step(first + i)
+    torch.cuda.synchronize()
+    recs = (_lib.EbcProbeRecord * cap)()
+    got = L.ebc_probe_end(recs, cap)
+    if got < 0:
+        raise RuntimeError("ebc_probe_end failed")
+    classes = {}
+    dace = []
+    for r in recs[:min(got, cap)]:
+        kind = _lib.PROBE_KINDS.get(r.kind, str(r.kind))
+        if kind == "gemm":
+            mode = {0: "", 1: " conv3x3", 2: " conv3x3-wgrad"}[r.mode]
+            epi = {0: "store", 1: "gelu", 2: "resid", 3: "gelu_bwd", 4: "bn_stats", 5: "add_relu_grad"}.get(r.epi, r.epi)
+            key = f"gemm_nt {r.bm}x{r.bn}{mode} {epi} M={r.m} N={r.n} K={r.k}"
+            flops = 2.0 * r.m * r.n * r.k
+        elif kind == "dace_loss":
+            key, flops = f"dace_loss_kernel B={r.m} g={r.k}", 0.0
+            dace.append(r.ms)
+        elif kind.startswith("attn"):
+            key, flops = f"{kind} B={r.m} L={r.n} heads={r.k}", _attn_flops(r.m, r.n, r.k)
+        else:
+            key, flops = f"{kind} rows={r.m}", 0.0
+        c = classes.setdefault(key, {"kernel": key, "launches": 0, "ms": 0.0, "flop_per_launch": flops})
+        c["launches"] += 1
+        c["ms"] += r.ms
+    out = []
+    for c in classes.values():
+        avg_us = c["ms"] / c["launches"] * 1e3
+        rec = {"kernel": c["kernel"], "per_step_us": round(c["ms"] / n * 1e3, 1), "launches_per_step": c["launches"] / n,
+               "avg_us": round(avg_us, 2)}
+        if c["flop_per_launch"]:
+            rec["tflops"] = round(c["flop_per_launch"] / (avg_us * 1e-6) / 1e12, 1)
+            rec["flop_per_launch"] = c["flop_per_launch"]
+        out.append(rec)
+    out.sort(key=lambda r: -r["per_step_us"])
+    sink = None
+    if dace:
+        # BASELINE.md: 4 n 784 (2 I + I/10) + 3*4*784 + 8 n bytes per crop, I = 100 iterations executed
+        byts = []
+        for i in range(n):
+            cnt = counts_of(first + i)
+            byts.append(sum(4 * c * 784 * (2 * 100 + 10) + 3 * 4 * 784 + 8 * c for c in cnt if c > 0))
+        avg_b, avg_s = sum(byts) / len(byts), sum(dace) / len(dace) * 1e-3
+        sink = {"bound": "hbm", "achieved": round(avg_b / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(avg_b / avg_s / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": int(avg_b),
+                "avg_us": round(avg_s * 1e6, 1), "kernel": "dace_loss_kernel<28> (fused DACE + DMCount + Sinkhorn, 100 its)",
+                "note": "reference-algorithm bytes (materialised K); the kernel keeps K factored in LDS, so this "
+                        "is an equivalent rate, not HBM traffic"}
+    return out, sink
+
+
+def committed_traffic(kernel_key):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE), profiles/r02_pmc_traffic.json; None when no pass covers that kernel."""
+    path = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            recs = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for r in recs if isinstance(recs, list) else []:
+        if r.get("kernel") == kernel_key:
+            return r.get("traffic_bytes_per_launch")
+    return None
+
+
+# ----------------------------------------------------------------------------- other workloads
 def run_augment(args, rank, device):
     """Row f2: crops/s of ebc_amd.transforms.CropAugment (host parameter draws + label arithmetic + the
     three augmentation launches + dot maps) for 16 NWPU-sized 1536x2048 images x num_crops 2 per step,
@@ -181,7 +266,6 @@ def run_augment(args, rank, device):
         aug(imgs, labels, NC)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    # device-only share: the launches of one step between events
     plans = [aug.plan_crop(i, H, W, labels[i].clone())[0] for i in range(NI) for _ in range(NC)]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -217,7 +301,7 @@ def run_eval(args, rank, world, device):
     from ebc_amd.model import get_model
     torch.manual_seed(42)
     model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
-                      vpt_drop=0.0, deep_vpt=True).to(device).eval()
+                      vpt_drop=0.0, deep_vpt=True, weights_seed=0).to(device).eval()
     H, W = 2048, 3072
     g = np.random.Generator(np.random.PCG64(7))                 # one image, its tiles sharded over the ranks
     mean = np.array([0.485, 0.456, 0.406], np.float32).reshape(1, 3, 1, 1)
@@ -228,7 +312,7 @@ def run_eval(args, rank, world, device):
 
     def one():
         with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
-            return sliding_window_predict(model, img, 224, 224)
+            return sliding_window_predict(model, img, 224, 224, shard=world > 1)
 
     for _ in range(args.warmup):
         one()
@@ -258,25 +342,17 @@ def run_eval(args, rank, world, device):
                        "tiles_per_image": tiles, "density_map": list(out.shape)}}), flush=True)
 
 
-def committed_traffic(dtype):
-    """HBM bytes per launch of the probe kernel from the committed PMC passes (FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE, profiles/r01_gemm_fc_traffic.json); None when no profile matches."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_gemm_fc_traffic.json")
-    try:
-        with open(path) as f:
-            rec = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if dtype != "fp16" or "EF16" not in rec.get("kernel", ""):
-        return None
-    return rec["traffic_bytes_per_launch"]
-
-
+# ----------------------------------------------------------------------------- main
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {world} rank(s) launched", file=sys.stderr)
+        sys.exit(2)
     # EBC_BENCH_ONE_DEVICE=1 EBC_BENCH_BACKEND=gloo: rehearse the N-rank path with every rank on cuda:0
     # (a 1-GPU box); the measured numbers of such a run are not a scaling result
     dev_index = 0 if os.environ.get("EBC_BENCH_ONE_DEVICE") == "1" else local
@@ -285,60 +361,79 @@ def main():
         dist.init_process_group(backend, device_id=torch.device(f"cuda:{dev_index}") if backend == "nccl" else None)
     torch.cuda.set_device(dev_index)
     device = torch.device(f"cuda:{dev_index}")
-    if args.augment:
-        run_augment(args, rank, device)
+    if args.augment or args.eval:
+        if args.augment:
+            run_augment(args, rank, device)
+        else:
+            run_eval(args, rank, world, device)
         if world > 1:
             dist.destroy_process_group()
         return
-    if args.eval:
-        run_eval(args, rank, world, device)
-        if world > 1:
-            dist.destroy_process_group()
-        return
+    from ebc_amd import _lib
     step = setup(args, rank, world, local, device)
     B = args.crops_per_gpu
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    st = torch.cuda.current_stream(device)
+    _lib.check(_lib.lib().ebc_marker(1, _lib.stream(device)), "ebc_marker")      # profile window: begin
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     for i in range(args.steps):
+        ev[i].record(st)
         step(args.warmup + i)
+    ev[-1].record(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    _lib.check(_lib.lib().ebc_marker(2, _lib.stream(device)), "ebc_marker")      # profile window: end
+    step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
+    per_rank = [elapsed]
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per_rank = [float(x) for x in allt]
+        elapsed = max(per_rank)
     crops = B * world * args.steps
     value = crops / elapsed
     ms = elapsed / args.steps * 1e3
 
+    kernels, sink = None, None
+    if not args.no_probe:
+        first = args.warmup + args.steps
+        kernels, sink = probe_steps(step, first, 3, device, lambda i: step.pool[i % len(step.pool)][3])
     if rank == 0:
-        probe = probe_kernels(args.dtype, device)
         peak = MFMA_PEAK_TF[args.dtype]
+        cfgname = "configs[2]" if (world == 1 and B == 16) else ("configs[3] per-rank shape" if B == 32 else "custom")
         out = {
-            "metric": "train crops/sec clip_vit_b_16 224px @1/2/4/8 MI355X; MAE parity",
-            "value": round(value, 3), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (BASELINE.md crops, pre-staged in HBM; synthetic random-init weights)",
-            "config": {"workload": f"clip_vit_b_16 224x224 deep-VPT(32) + DACE/DMCount train step, "
-                                   f"{B} crops/GPU, AMP {args.dtype} (BASELINE configs[2]" + (", DDP configs[3] shape" if world > 1 else "") + ")",
+            "metric": METRIC, "value": round(value, 3), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "median_ms_per_step": round(statistics.median(step_ms), 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (BASELINE.md crops, a distinct batch per step, pre-staged in HBM; synthetic random-init weights)",
+            "config": {"workload": f"clip_vit_b_16 224x224 deep-VPT(32) + DACE/DMCount train step, {B} crops/GPU, "
+                                   f"AMP {args.dtype}, NWPU anchors (BASELINE {cfgname})",
                        "global_batch": B * world, "seq_len": 229, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": round(probe["achieved"], 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(probe["achieved"] / peak, 4), "traffic": committed_traffic(args.dtype),
-                         "traffic_unit": "bytes/launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_gemm_fc_traffic.json)",
-                         "algorithmic_bytes": 55369728,
-                         "kernel": probe["kernel"], "avg_us": round(probe["avg_us"], 2)},
             "step_roofline": {"flop_per_crop": FLOP_PER_CROP, "achieved_tflops": round(value / world * FLOP_PER_CROP / 1e12, 2),
                               "frac": round(value / world * FLOP_PER_CROP / 1e12 / peak, 4)},
         }
+        if world > 1:
+            out["per_rank_crops_s"] = [round(B * args.steps / t, 2) for t in per_rank]
+        if kernels:
+            top = next(k for k in kernels if "tflops" in k)
+            out["roofline"] = {"bound": "mfma", "achieved": top["tflops"], "peak": peak, "unit": "TFLOP/s",
+                               "frac": round(top["tflops"] / peak, 4), "traffic": committed_traffic(top["kernel"]),
+                               "kernel": top["kernel"], "avg_us": top["avg_us"], "flop_per_launch": top["flop_per_launch"],
+                               "per_step_us": top["per_step_us"],
+                               "method": "in-step HIP events on the launch stream (ebc_probe), 3 instrumented steps"}
+            out["kernels"] = kernels[:12]
+            out["sinkhorn"] = sink
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, args.cpu_crops, args.cpu_steps)
         print(json.dumps(out), flush=True)

@@ -16,6 +16,7 @@
 #include <cstdlib>
 
 #include "ebc_common.h"
+#include "kernels.h"
 #include "mfma.h"
 
 using namespace ebc;
@@ -378,8 +379,10 @@ template <class E, int NW, int LFIX> int attn_fwd_nw(const void* qkv, void* out,
         attr = true;
     }
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
+    const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_FWD, 0, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_fwd_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
                        (typename E::T*)out, lse, B, L, H, 0.125f);
+    probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -402,12 +405,16 @@ template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void
         attr = true;
     }
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
+    int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 0, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_bwd_dq_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds_dq, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, (const typename E::T*)out, lse, delta, (typename E::T*)dqkv, B, L, H,
                        0.125f);
+    probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
+    pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DKV, 0, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds_kv, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, lse, delta, (typename E::T*)dqkv, B, L, H, 0.125f);
+    probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "ebc_common.h"
+#include "kernels.h"
 
 using namespace ebc;
 
@@ -83,6 +84,7 @@ struct Params {
     int lds_cap;           // max points kept in LDS with full factor rows (dense path)
     int lds_cap_s;         // max points kept in LDS with full factor rows (bucketed path)
     int lds_cap_c;         // max points kept in LDS with compact factor rows (bucketed path)
+    int total_points;      // sum of n over the crops (probe records only)
     unsigned long long* prof;   // diagnostics (EBC_DACE_PROF=1): per crop 16 counters, else null
 };
 
@@ -90,8 +92,8 @@ struct Params {
 // Sinkhorn-Knopp on the separable DMCount kernel.  `Ey`, `Ex` ([n][G]), `u0/u1` ([n]) live in
 // LDS or global memory (FP = float* into either); everything else in LDS.
 // cood of grid cell k (dm_loss.py:31-34): pixel centre, or normalised to [-1, 1] when norm_cood
-__device__ __forceinline__ float cood(int k, int size, int norm) {
-    const float c = (float)(k * 8) + 4.0f;
+__device__ __forceinline__ float cood(int k, int size, int red, int norm) {
+    const float c = (float)(k * red) + 0.5f * (float)red;    // arange(0, size, red) + red / 2
     return norm ? c / (float)size * 2.0f - 1.0f : c;
 }
 __device__ __forceinline__ float pcoord(float p, int size, int norm) {
@@ -125,7 +127,7 @@ __device__ __forceinline__ float sum8_dpp(float x) {
 }
 
 template <int G, typename FP, typename IP>
-__device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
+__device__ void sinkhorn_crop(int n, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                               const float* __restrict__ pts, FP Ey, FP Ex, FP u0, FP u1, IP win,
                               const float* b, float* v0, float* v1, float* part, float* misc,
                               int* iters_out, int* rolled_out, float* err_last_out, unsigned long long* pr)
@@ -141,7 +143,7 @@ __device__ void sinkhorn_crop(int n, int size, int norm, float reg, int max_iter
     // factors: Ey[i][iy] = exp(yd/-reg), Ex[i][jx] = exp(xd/-reg)
     for (int e = t; e < n * G; e += NT) {
         const int i = e / G, k = e - i * G;
-        const float c = cood(k, size, norm);                  // dm_loss.py:31-34 (reduction 8)
+        const float c = cood(k, size, red, norm);             // dm_loss.py:31-34
         const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
         const float yd = (-2.0f * (y * c) + y * y) + c * c;
         const float xd = (-2.0f * (x * c) + x * x) + c * c;
@@ -316,7 +318,7 @@ __device__ __forceinline__ float sum4_dpp(float x) {
 // Returns false (nothing iterated) when a window is wider than 9 cells; the caller then runs
 // sinkhorn_crop.  On return the factors, u (u0), windows and point coordinates (spts) are sorted.
 template <int G, int CW>
-__device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
+__device__ bool sinkhorn_sorted(int n, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                                 const float* __restrict__ pts, float* Ey, float* Ex, float* u0, float* u1, int* win,
                                 int* key, float* spts, int* bk, const float* b, float* v0, float* v1, float* part,
                                 float* misc, int* iters_out, int* rolled_out, float* err_last_out,
@@ -340,7 +342,7 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
         const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
         int ylo = G, yhi = -1, xlo = G, xhi = -1;
         for (int k = 0; k < G; ++k) {
-            const float c = cood(k, size, norm);
+            const float c = cood(k, size, red, norm);
             const float yd = (-2.0f * (y * c) + y * y) + c * c;
             const float xd = (-2.0f * (x * c) + x * x) + c * c;
             if (expf(yd / -reg) != 0.f) { ylo = min(ylo, k); yhi = k; }
@@ -371,7 +373,7 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
         const int w = tmpwin[i];
         const int yb = row_base<G, CW>(w & 255, (w >> 8) & 255), xb = row_base<G, CW>((w >> 16) & 255, (w >> 24) & 255);
         for (int k = 0; k < CW; ++k) {
-            const float cy = cood(yb + k, size, norm), cx = cood(xb + k, size, norm);
+            const float cy = cood(yb + k, size, red, norm), cx = cood(xb + k, size, red, norm);
             const float yd = (-2.0f * (y * cy) + y * y) + cy * cy;
             const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
             Ey[slot * CW + k] = expf(yd / -reg);
@@ -596,7 +598,7 @@ __device__ bool sinkhorn_sorted(int n, int size, int norm, float reg, int max_it
 
 // Wasserstein distance sum(C * P) over the windows (dm_loss.py:77; reported, unused by training)
 template <int G, int CW, typename FP, typename IP>
-__device__ float transport_cost(int n, int size, int norm, const float* pts, FP Ey, FP Ex, FP u, IP win,
+__device__ float transport_cost(int n, int size, int red, int norm, const float* pts, FP Ey, FP Ex, FP u, IP win,
                                 const float* v, int WY, float* misc)
 {
     float w = 0.f;
@@ -607,12 +609,12 @@ __device__ float transport_cost(int n, int size, int norm, const float* pts, FP 
         const int iy = (wi & 255) + r, xlo = (wi >> 16) & 255, xlen = (wi >> 24) & 255;
         const int yb = row_base<G, CW>(wi & 255, (wi >> 8) & 255), xb = row_base<G, CW>(xlo, xlen);
         const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
-        const float c = cood(iy, size, norm);
+        const float c = cood(iy, size, red, norm);
         const float yd = (-2.0f * (y * c) + y * y) + c * c;
         float t1 = 0.f, t2 = 0.f;
         for (int k = 0; k < xlen; ++k) {
             const int jx = xlo + k;
-            const float cx = cood(jx, size, norm);
+            const float cx = cood(jx, size, red, norm);
             const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
             const float kv = Ex[i * CW + jx - xb] * v[iy * G + jx];
             t1 += kv;
@@ -685,7 +687,8 @@ __device__ void crop_body(const Params& P, int b, float* lds)
 
     float cnt_b = 0.f, tv_b = 0.f, ot_b = 0.f, wd_b = 0.f, err_last = -1.f;
     int iters = 0, rolled = 0;
-    if (P.count_mode != EBC_COUNT_DMCOUNT) {
+    const bool dm = P.count_mode == EBC_COUNT_DMCOUNT;           // EBC_COUNT_OT_ONLY: the OT term alone
+    if (P.count_mode == EBC_COUNT_MAE || P.count_mode == EBC_COUNT_MSE) {
         // count_loss "mae" / "mse": per-pixel, summed over HW, mean over B (dace_loss.py:57-62)
         float s = 0.f;
         for (int j = t; j < GG; j += NT) {
@@ -710,7 +713,8 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         tvk = block_sum(tvk, misc);
         tv_b = tvs * tc;
         cnt_b = fabsf(pc - tc);
-        const float gcount = sgnf(pc - tc) * invB;
+        const float gcount = dm ? sgnf(pc - tc) * invB : 0.f;
+        const float wtv = dm ? P.w_tv : 0.f;
         // 4. Sinkhorn OT (dm_loss.py:49-77)
         if (n > 0) {
             const float* pts = P.points + 2 * (size_t)p0;
@@ -738,13 +742,13 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                     v1[j] = og;
                 }
                 ot_b = block_sum(ol, misc);
-                wd_b = transport_cost<G, decltype(cw)::value>(n, S, P.norm_cood, cpts, Ey, Ex, u0, win, v0, WY, misc);
+                wd_b = transport_cost<G, decltype(cw)::value>(n, S, P.red, P.norm_cood, cpts, Ey, Ex, u0, win, v0, WY, misc);
             };
             // dense path (full rows; wide windows or too many points for the compact rows)
             auto dense = [&](float* base, auto /*in_lds: one instantiation per address space*/) {
                 float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
                 int* win = reinterpret_cast<int*>(u1 + n);
-                sinkhorn_crop<G>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
+                sinkhorn_crop<G>(n, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
                                  u1, win, bb, v0, v1, part, misc, &iters, &rolled, &err_last,
                                  P.prof ? P.prof + b * 16 : nullptr);
                 post(std::integral_constant<int, G>{}, Ey, Ex, u0, win, pts);
@@ -757,7 +761,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                 int* win = reinterpret_cast<int*>(u1 + n);
                 int* key = win + n;
                 float* spts = reinterpret_cast<float*>(key + n);
-                if (!sinkhorn_sorted<G, CW>(n, P.size, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
+                if (!sinkhorn_sorted<G, CW>(n, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
                                             Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc, &iters,
                                             &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr))
                     return false;
@@ -772,7 +776,10 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                 else dense(P.ws_factors + (size_t)C::PER_POINT * p0, std::false_type{});
             }
         } else {
-            for (int j = t; j < GG; j += NT) v1[j] = 0.f;
+            for (int j = t; j < GG; j += NT) {
+                v1[j] = 0.f;
+                if (P.beta_out) P.beta_out[(size_t)b * GG + j] = 0.f;   // no OT for an empty crop (dm_loss.py:49)
+            }
             __syncthreads();
         }
         // 5. d loss / d pred_density = w_count * (w_ot * ot_grad + w_tv * tv_grad + count_grad)
@@ -780,7 +787,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         for (int j = t; j < GG; j += NT) {
             const float d = pd[j] * inv_pc - td[j] * inv_tc;
             const float gtv = ktv * (sgnf(d) * inv_pc - tvk * inv_pc * inv_pc);
-            P.grad_density[(size_t)b * GG + j] = P.w_count * (P.w_ot * v1[j] + P.w_tv * gtv + gcount);
+            P.grad_density[(size_t)b * GG + j] = P.w_count * (P.w_ot * v1[j] + wtv * gtv + gcount);
         }
     }
     if (P.prof && t == 0) { P.prof[b * 16 + 7] = clock64(); P.prof[b * 16 + 4] = iters; }
@@ -819,6 +826,9 @@ __global__ void dace_finalize_kernel(const float* stats, int B, int count_mode, 
             const float tv = r[1] * invB, cnt = r[2] * invB, ot = r[3];
             const float dm = ot * w_ot + tv * w_tv + cnt;
             losses[0] = ce + w_count * dm; losses[1] = ot; losses[2] = tv; losses[3] = cnt; losses[4] = ce;
+        } else if (count_mode == EBC_COUNT_OT_ONLY) {
+            const float ot = r[3];
+            losses[0] = w_count * w_ot * ot; losses[1] = ot; losses[2] = 0.f; losses[3] = 0.f; losses[4] = ce;
         } else {
             const float cnt = r[2] * invB;
             losses[0] = ce + w_count * cnt; losses[1] = 0.f; losses[2] = 0.f; losses[3] = cnt; losses[4] = ce;
@@ -843,7 +853,9 @@ template <int G> int launch(const Params& P0, hipStream_t st)
     static const bool want_prof = getenv("EBC_DACE_PROF") != nullptr;
     if (want_prof && !dprof && P.B <= 1024) (void)hipMalloc(&dprof, 1024 * 16 * sizeof(unsigned long long));
     if (want_prof) P.prof = dprof;
+    const int pi = probe_on() ? probe_start(EBC_PROBE_DACE, P.count_mode, 0, 0, 0, P.B, P.total_points, G, st) : -1;
     hipLaunchKernelGGL(dace_loss_kernel<G>, dim3(P.B), dim3(NT), LDS_MAX, st, P);
+    probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     if (P.prof) {   // diagnostics only: synchronous read-back and a line per crop on stderr
         unsigned long long h[1024 * 16];
@@ -875,8 +887,10 @@ extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density,
                              float* beta_out, int* status, void* workspace, size_t workspace_bytes,
                              ebc_stream_t stream)
 {
-    if (B <= 0 || N <= 0 || reduction != 8 || size % reduction != 0 || eval_freq <= 0 || reg <= 0.f)
+    if (B <= 0 || N <= 0 || reduction <= 0 || size % reduction != 0 || eval_freq <= 0 || reg <= 0.f)
         return EBC_E_ARG;
+    if (count_mode < EBC_COUNT_DMCOUNT || count_mode > EBC_COUNT_OT_ONLY) return EBC_E_ARG;
+    if (!target_is_reduced && reduction % 4 != 0) return EBC_E_UNSUPPORTED;   // float4 row pieces per cell
     if (!pred_class || !pred_density || !target_density || !offsets || !bins_lo || !bins_hi ||
         !grad_class || !grad_density || !losses || !crop_stats)
         return EBC_E_ARG;
@@ -891,6 +905,7 @@ extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density,
     P.reg = reg; P.stop_thr = stop_thr; P.max_iter = max_iter; P.eval_freq = eval_freq;
     P.grad_class = grad_class; P.grad_density = grad_density; P.crop_stats = crop_stats;
     P.beta_out = beta_out; P.status = status; P.ws_factors = (float*)workspace;
+    P.total_points = (int)((workspace_bytes - 256) / (sizeof(float) * (2 * (size_t)g + 6)));
     int rc;
     if (g == 28) rc = launch<28>(P, st);
     else if (g == 56) rc = launch<56>(P, st);

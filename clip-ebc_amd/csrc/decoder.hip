@@ -205,7 +205,10 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __re
 
 // BatchNorm2d (training: batch mean / biased variance, running stats with momentum and the unbiased
 // variance; eval: running stats), folded into a per-channel scale/shift
-__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __restrict__ sums, double count, float eps,
+// count_dev != NULL: the element count is a device value (SyncBatchNorm: the ranks' counts all-reduced
+// together with the sums, so ranks may hold different batch sizes)
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __restrict__ sums, double count,
+                                                              const double* __restrict__ count_dev, float eps,
                                                               float momentum, const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* mean, float* rstd,
                                                               float* scale, float* shift, float* rmean, float* rvar, int C)
@@ -213,6 +216,7 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __re
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= C) return;
     double m, var;
+    if (count_dev) count = *count_dev;
     if (sums) {
         m = sums[c] / count;
         var = sums[C + c] / count - m * m;
@@ -293,6 +297,7 @@ __global__ __launch_bounds__(512) void bn_bwd_partial_kernel(const T* __restrict
 
 // dgamma = sum(g*xhat), dbeta = sum(g); coef = [gamma*rstd, sum(g)/count, sum(g*xhat)/count]
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ sums, double count,
+                                                              const double* __restrict__ count_dev,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ rstd, float* dgamma,
                                                               float* dbeta, float* coef, int C)
@@ -300,6 +305,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= C) return;
     const double sg = sums[c], sgx = sums[C + c];
+    if (count_dev) count = *count_dev;
     if (dgamma) dgamma[c] = (float)sgx;
     if (dbeta) dbeta[c] = (float)sg;
     coef[c] = gamma[c] * rstd[c];
@@ -595,8 +601,9 @@ extern "C" int ebc_bn_finalize(const double* colsum, double count, float eps, fl
 {
     if (!gamma || !beta || !mean || !rstd || !scale || !shift) return EBC_E_ARG;
     if (!colsum && (!running_mean || !running_var)) return EBC_E_ARG;
-    if (colsum && count <= 1.0) return EBC_E_ARG;
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nblk(C)), dim3(256), 0, (hipStream_t)stream, colsum, count, eps,
+    if (colsum && count >= 0.0 && count <= 1.0) return EBC_E_ARG;
+    const double* cdev = colsum && count < 0.0 ? colsum + 2 * C : nullptr;     // device count at colsum[2C]
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nblk(C)), dim3(256), 0, (hipStream_t)stream, colsum, count, cdev, eps,
                        momentum, gamma, beta, mean, rstd, scale, shift, running_mean, running_var, C);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
@@ -643,8 +650,9 @@ extern "C" int ebc_bn_bwd_reduce(int dtype, const void* gy, const void* mask_y, 
 extern "C" int ebc_bn_bwd_finalize(const double* sums, double count, const float* gamma, const float* rstd,
                                    float* dgamma, float* dbeta, float* coef, int C, ebc_stream_t stream)
 {
-    if (!sums || !gamma || !rstd || !coef || count <= 0.0) return EBC_E_ARG;
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nblk(C)), dim3(256), 0, (hipStream_t)stream, sums, count, gamma,
+    if (!sums || !gamma || !rstd || !coef || count == 0.0) return EBC_E_ARG;
+    const double* cdev = count < 0.0 ? sums + 2 * C : nullptr;                 // device count at sums[2C]
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nblk(C)), dim3(256), 0, (hipStream_t)stream, sums, count, cdev, gamma,
                        rstd, dgamma, dbeta, coef, C);
     EBC_CHECK_LAUNCH();
     return EBC_OK;

@@ -681,7 +681,9 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
     }
     if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
     const int nwg = ((g.M + BM - 1) / BM) * (g.N / BN) * g.splits;
+    const int pi = probe_on() ? probe_start(EBC_PROBE_GEMM, EPI, BM, BN, MODE, g.M, g.N, g.K, st) : -1;
     hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
+    probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -773,15 +775,21 @@ int pick_splits(int M, int N, int K, const TileCfg& c, int bk) {
     return s;
 }
 
+// the tile configuration a MODE 0 product runs (EBC_GEMM_CFG override when it fits, else the heuristic)
+int select_cfg(bool sixteen, int M, int N, int K)
+{
+    int cfg = forced_cfg();
+    const TileCfg* c = find_cfg(cfg);
+    if (!c || N % c->bn != 0 || (cfg >= 8 && !sixteen)) cfg = 0;
+    return cfg ? cfg : pick_cfg(M, N, K, sixteen);
+}
+
 template <class E, class TO, int EPI>
 int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
 {
     constexpr bool SIXTEEN = E::BYTES == 2;
-    int cfg = forced_cfg();
+    const int cfg = select_cfg(SIXTEEN, g.M, g.N, g.K);
     const TileCfg* c = find_cfg(cfg);
-    if (!c || g.N % c->bn != 0 || (cfg >= 8 && !SIXTEEN)) cfg = 0;
-    if (cfg == 0) cfg = pick_cfg(g.M, g.N, g.K, SIXTEEN);
-    c = find_cfg(cfg);
     const bool r64 = cfg >= 20 && cfg < 30;                   // 64-B K rows (4-stage rings)
     const int bk = r64 ? 32 : 128 / E::BYTES;
     int splits = forced_splits() > 0 ? forced_splits() : pick_splits(g.M, g.N, g.K, *c, bk);
@@ -1100,4 +1108,34 @@ extern "C" int ebc_gemm_ws(int dtype, int epilogue, int out_f32, const void* A, 
     // caller's stream; the kernels leave its counter block zero again after every call
     return ebc::gemm_nt(dtype, epilogue, out_f32, A, B, C, bias, resid, aux, M, N, K, (hipStream_t)stream,
                         workspace, workspace_bytes);
+}
+
+extern "C" int ebc_gemm_tile_config(int dtype, int M, int N, int K, int* out)
+{
+    if (M <= 0 || N <= 0 || K <= 0 || (dtype != EBC_F32 && dtype != EBC_F16 && dtype != EBC_BF16)) return EBC_E_ARG;
+    const bool sixteen = dtype != EBC_F32;
+    const int cfg = select_cfg(sixteen, M, N, K);
+    const TileCfg* c = find_cfg(cfg);
+    if (out) {
+        const int bk = (cfg >= 20 && cfg < 30) ? 32 : (sixteen ? 64 : 32);
+        out[0] = c->bm;
+        out[1] = c->bn;
+        out[2] = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, bk);
+    }
+    return cfg;
+}
+
+extern "C" int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, int* out)
+{
+    if (M <= 0 || N <= 0 || K <= 0 || (mode != 1 && mode != 2)) return EBC_E_ARG;
+    const bool sixteen = dtype != EBC_F32;
+    const int cfg = conv_cfg(sixteen, mode, M, N);
+    const TileCfg* c = find_cfg(cfg);
+    if (out) {
+        const int bk = !sixteen ? 32 : (cfg >= 20 ? 32 : 64);
+        out[0] = c->bm;
+        out[1] = c->bn;
+        out[2] = conv_splits(cfg, mode, M, N, K / bk);
+    }
+    return cfg;
 }

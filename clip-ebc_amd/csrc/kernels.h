@@ -4,6 +4,10 @@
 #include <stddef.h>
 
 namespace ebc {
+// in-step launch timing (probe.hip): probe_start returns a record index (or -1 when not armed)
+bool probe_on();
+int probe_start(int kind, int epi, int bm, int bn, int mode, int m, int n, int k, hipStream_t st);
+void probe_stop(int idx, hipStream_t st);
 int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
             const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws = nullptr,
             size_t ws_bytes = 0);

@@ -9,6 +9,7 @@
 //            similarity head              models/clip/model.py:198-217
 // Every kernel is one wave per row (D = 256*NV), 16-B vector accesses, fp32 statistics.
 #include "ebc_common.h"
+#include "kernels.h"
 #include "mfma.h"
 
 using namespace ebc;
@@ -495,6 +496,8 @@ static int ln_fwd_launch(int dtype, const float* x, RowMap map, const float* gam
                          float* outf, float* mean, float* rstd, int M, VptIns vi, hipStream_t st)
 {
     const dim3 grid((M + 3) / 4);
+    const int pi = probe_on() ? probe_start(EBC_PROBE_LN_FWD, 0, 0, 0, 0, M, 768, 0, st) : -1;
+    struct Stop { int i; hipStream_t s; ~Stop() { probe_stop(i, s); } } stop{pi, st};
     switch (dtype) {
         case EBC_F32: hipLaunchKernelGGL((ln_fwd_kernel<float, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (float*)out, outf, mean, rstd, M, vi); break;
         case EBC_F16: hipLaunchKernelGGL((ln_fwd_kernel<_Float16, 3>), grid, dim3(256), 0, st, x, map, gamma, beta, (_Float16*)out, outf, mean, rstd, M, vi); break;
@@ -527,6 +530,8 @@ static int ln_bwd_t(int dy_f32, const void* dy, const float* x, RowMap map, cons
                     const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, VptOut vo, hipStream_t st)
 {
     const dim3 grid((M + 3) / 4);
+    const int pi = probe_on() ? probe_start(EBC_PROBE_LN_BWD, 0, 0, 0, 0, M, 768, 0, st) : -1;
+    struct Stop { int i; hipStream_t s; ~Stop() { probe_stop(i, s); } } stop{pi, st};
     if (dy_f32)
         hipLaunchKernelGGL((ln_bwd_kernel<T, float, 3>), grid, dim3(256), 0, st, (const float*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M, vo);
     else

@@ -14,7 +14,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("EBC_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libebc_hip.so")   # override: tuning builds
 
 EBC_F32, EBC_F16, EBC_BF16 = 0, 1, 2
-EBC_COUNT_DMCOUNT, EBC_COUNT_MAE, EBC_COUNT_MSE = 0, 1, 2
+EBC_COUNT_DMCOUNT, EBC_COUNT_MAE, EBC_COUNT_MSE, EBC_COUNT_OT_ONLY = 0, 1, 2, 3
 _ERR = {-1: "EBC_E_ARG", -2: "EBC_E_LAUNCH", -3: "EBC_E_UNSUPPORTED"}
 
 _lib: Optional[ctypes.CDLL] = None
@@ -39,6 +39,14 @@ class EbcCropDesc(ctypes.Structure):
                 ("seed", ctypes.c_uint32), ("normalize", ctypes.c_int32)]
 
 
+class EbcProbeRecord(ctypes.Structure):
+    """include/ebc_hip.h EbcProbeRecord (one instrumented launch)."""
+    _fields_ = [(n, ctypes.c_int) for n in ("kind", "epi", "bm", "bn", "mode", "m", "n", "k")] + [("ms", ctypes.c_float)]
+
+
+PROBE_KINDS = {1: "gemm", 2: "dace_loss", 3: "attn_fwd", 4: "attn_bwd_dq", 5: "attn_bwd_dkv", 6: "ln_fwd", 7: "ln_bwd"}
+
+
 class EbcAugConst(ctypes.Structure):
     """include/ebc_hip.h EbcAugConst (passed by value)."""
     _fields_ = [("mean", ctypes.c_float * 3), ("std", ctypes.c_float * 3), ("blur_k", ctypes.c_int32),
@@ -51,8 +59,12 @@ SIGNATURES = {
     "ebc_dace_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "ebc_dace_loss": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _I, _F, _I,
                            _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
+    "ebc_sinkhorn_workspace_bytes": (_Z, [_I, _I]),
+    "ebc_sinkhorn": (_I, [_P, _P, _P, _I, _I, _F, _I, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "ebc_gemm": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "ebc_gemm_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "ebc_gemm_tile_config": (_I, [_I, _I, _I, _I, _P]),
+    "ebc_conv_tile_config": (_I, [_I, _I, _I, _I, _I, _P]),
     "ebc_gemm_ws": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _Z, _P]),
     "ebc_gemm_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "ebc_gemm_wgrad": (_I, [_I, _P, _P, _P, _I, _I, _I, _P, _Z, _P]),
@@ -85,6 +97,9 @@ SIGNATURES = {
     "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, EbcAugConst, _P]),
     "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "ebc_probe_begin": (_I, [_I]),
+    "ebc_probe_end": (_I, [_P, _I]),
+    "ebc_marker": (_I, [_I, _P]),
 }
 
 
@@ -115,15 +130,37 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what} failed: {_ERR.get(rc, rc)}")
 
 
-def ptr(t: Optional[torch.Tensor]):
+def ptr(t: Optional[torch.Tensor], device: Optional[torch.device] = None):
+    """Raw device pointer of a contiguous HIP tensor; with `device`, the tensor must live there (every
+    operand of a launch is on the launch stream's device)."""
     if t is None:
         return None
     assert t.is_cuda and t.is_contiguous(), "ebc_amd kernels take contiguous device tensors"
+    if device is not None and t.device != device:
+        raise RuntimeError(f"ebc_amd: operand on {t.device}, launch stream on {device}")
     return ctypes.c_void_p(t.data_ptr())
 
 
-def stream() -> ctypes.c_void_p:
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+def _as_device(where) -> Optional[torch.device]:
+    if where is None:
+        return None
+    if isinstance(where, torch.Tensor):
+        return where.device
+    return torch.device(where)
+
+
+def stream(where=None) -> ctypes.c_void_p:
+    """The current torch stream of the device `where` (a tensor or a device) lives on -- NOT the current
+    device's: the reference trainer builds its model on f"cuda:{local_rank}" without set_device
+    (trainer.py:93, utils/ddp_utils.py:16-22), so the two can differ on ranks > 0."""
+    dev = _as_device(where)
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def on(where):
+    """Context manager making `where`'s device current for a block of library calls: the library's own
+    device queries (hipGetDevice, hipFuncSetAttribute) and its memsets then target the operands' GPU."""
+    return torch.cuda.device(_as_device(where))
 
 
 def dtype_code(dt: torch.dtype) -> int:

@@ -2,8 +2,10 @@
 
 `sliding_window_predict(model, image, window_size, stride)` keeps the reference signature and
 result (a CPU tensor [1, 1, H/r, W/r], overlaps averaged); tiles are gathered and the map assembled
-by HIP kernels (`ebc_tile_gather` / `ebc_tile_assemble`), the model runs once per tile batch, and
-under torch.distributed the tiles are sharded across ranks and all-gathered (BASELINE config 5).
+by HIP kernels (`ebc_tile_gather` / `ebc_tile_assemble`) and the model runs once per tile batch.
+Sharding the tiles of one image across ranks (BASELINE config 5) is OPT-IN (`shard=True`, every rank
+of `group` must call): the reference trainer evaluates on rank 0 alone while the other ranks wait in
+`dist.barrier()` (trainer.py:161-177,194), so a collective inside the default call would hang there.
 """
 from __future__ import annotations
 
@@ -38,8 +40,11 @@ def tile_grid(H: int, W: int, window: Tuple[int, int], stride: Tuple[int, int]) 
 
 def sliding_window_predict(model: nn.Module, image: Tensor, window_size: Union[int, Tuple[int, int]],
                            stride: Union[int, Tuple[int, int]], max_tiles_per_batch: int = 256,
-                           group: Optional[object] = None) -> Tensor:
-    """utils/eval_utils.py:26-96.  image [1, C, H, W] -> [1, Cp, H/r, W/r] (CPU tensor)."""
+                           shard: bool = False, group: Optional[object] = None) -> Tensor:
+    """utils/eval_utils.py:26-96.  image [1, C, H, W] -> [1, Cp, H/r, W/r] (CPU tensor).
+
+    shard=True (collective: every rank of `group` calls with the same image): each rank runs its
+    contiguous share of the tiles and the predictions are all-gathered before the assembly."""
     assert len(image.shape) == 4, f"Image must be a 4D tensor (1, c, h, w), got {image.shape}"
     window, strd = _pair(window_size), _pair(stride)
     assert window[0] > 0 and window[1] > 0, f"Window size must be a positive integer tuple (h, w), got {window}"
@@ -51,20 +56,20 @@ def sliding_window_predict(model: nn.Module, image: Tensor, window_size: Union[i
     rows, cols = tile_grid(H, W, window, strd)
     T = rows * cols
     reduction = getattr(model, "reduction", 1)
-    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    world = dist.get_world_size(group) if shard and dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if world > 1 else 0
     t0, t1, per = shard_range(T, world, rank)
     L = _lib.lib()
-    st = _lib.stream()
+    st = _lib.stream(dev)
     preds = None
     model.eval()
-    with torch.no_grad():
+    with torch.no_grad(), _lib.on(dev):
         outs = []
         for b0 in range(t0, t1, max_tiles_per_batch):
             n = min(max_tiles_per_batch, t1 - b0)
             tiles = torch.empty(n, C, window[0], window[1], device=dev, dtype=torch.float32)
-            _lib.check(L.ebc_tile_gather(_lib.ptr(img), _lib.ptr(tiles), C, H, W, window[0], window[1], strd[0], strd[1],
-                                         b0, n, st), "ebc_tile_gather")
+            _lib.check(L.ebc_tile_gather(_lib.ptr(img, dev), _lib.ptr(tiles), C, H, W, window[0], window[1], strd[0],
+                                         strd[1], b0, n, st), "ebc_tile_gather")
             outs.append(model(tiles).float())
         if outs:
             preds = torch.cat(outs, 0)
@@ -74,8 +79,8 @@ def sliding_window_predict(model: nn.Module, image: Tensor, window_size: Union[i
             preds = gather_shards(preds, T, per, (Cp, ph, pw), dev, group)
         preds = preds.contiguous()
         out = torch.empty(Cp, H // reduction, W // reduction, device=dev)
-        _lib.check(L.ebc_tile_assemble(_lib.ptr(preds), _lib.ptr(out), Cp, H, W, window[0], window[1], strd[0], strd[1],
-                                       reduction, st), "ebc_tile_assemble")
+        _lib.check(L.ebc_tile_assemble(_lib.ptr(preds, dev), _lib.ptr(out), Cp, H, W, window[0], window[1], strd[0],
+                                       strd[1], reduction, st), "ebc_tile_assemble")
     return out.unsqueeze(0).cpu()
 
 

@@ -1,4 +1,4 @@
-"""Drop-in DACE / DMCount losses backed by the fused gfx950 kernel (`ebc_dace_loss`).
+"""Drop-in DACE / DMCount / OT losses and `sinkhorn`, backed by gfx950 kernels.
 
 Mirrors the reference surface:
   * `DACELoss(bins, reduction, weight_count_loss=1.0, count_loss="mae", **kwargs)`
@@ -6,15 +6,24 @@ Mirrors the reference surface:
     -> (loss, loss_info)` with keys `loss, ot_loss, tv_loss, count_loss, ce_loss` (dmcount) or
     `ce_loss, {mae,mse}_loss, loss`;
   * `DMLoss(input_size, reduction, norm_cood=False, weight_ot=0.1, weight_tv=0.01, ...)`
-    (losses/dm_loss.py:82-124), `forward(pred_density, target_density, target_points)`.
+    (losses/dm_loss.py:82-124), `forward(pred_density, target_density, target_points)`;
+  * `OTLoss(input_size, reduction, norm_cood, num_of_iter_in_ot=100, reg=10.0)` (losses/dm_loss.py:12-79),
+    `forward(pred_density, normed_pred_density, target_points) -> (loss, wd, ot_obj_values)`;
+  * `sinkhorn(a, b, C, reg=1e-1, maxIter=1000, stopThr=1e-9, verbose=False, log=True, eval_freq=10,
+    print_freq=200) -> P | (P, log)` (losses/bregman_pytorch.py:11-144), log keys err/u/v/alpha/beta.
 
-Forward AND backward run in one kernel launch (+ a 1-block finalize): the loss is the last node of
-the graph, so its gradients are produced with the value and replayed (times the upstream scalar)
-in `backward`.
+DACE/DMCount forward AND backward run in one kernel launch (+ a 1-block finalize): the loss is the last
+node of the graph, so its gradients are produced with the value and replayed (times the upstream
+scalar) in `backward`.  The Sinkhorn internals of the last call (beta [B, g*g], status [B]: iterations,
+negative = NaN/Inf rollback, and the per-crop err of the last check) are kept on the DMLoss / OTLoss
+module when it is built with `keep_internals=True` (off by default: an extra [B, g*g] write).
+
+Geometry: the fused kernel is built for density grids g = input_size / reduction of 28 and 56 (224 or
+448 crops at reduction 8, 448 at 16); other sizes raise NotImplementedError at construction.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -22,31 +31,71 @@ from torch import Tensor, nn
 from . import _lib
 
 _INFO_DM = ("loss", "ot_loss", "tv_loss", "count_loss", "ce_loss")
+_GRIDS = (28, 56)
+M_EPS = 1e-16      # bregman_pytorch.py:8
+
+
+def _check_geometry(input_size: int, reduction: int) -> None:
+    assert input_size % reduction == 0, f"input_size {input_size} is not a multiple of reduction {reduction}"
+    g = input_size // reduction
+    if g not in _GRIDS or reduction % 4:
+        raise NotImplementedError(
+            f"ebc_amd DMCount kernel: density grid input_size/reduction = {g} (reduction {reduction}); "
+            f"built for grids {_GRIDS} with reduction % 4 == 0 (224/448 crops at reduction 8, 448 at 16)")
+
+
+class _Internals:
+    """Per-crop Sinkhorn results of one fused call (device tensors)."""
+
+    def __init__(self, beta: Tensor, status: Tensor, stats: Tensor):
+        self.beta = beta                 # [B, g*g]  reg * log(v + 1e-16)   (bregman_pytorch.py:137)
+        self.status = status             # [B] int32 iterations run, negative = rolled back at that iteration
+        self.crop_stats = stats          # [B, 8] ce, tv*n, count, ot, wd, iters, rolled, err of the last check
+
+    @property
+    def err_last(self) -> Tensor:
+        return self.crop_stats[:, 7]
+
+    @property
+    def wd(self) -> Tensor:
+        return self.crop_stats[:, 4]
+
+
+def _run_dace(pred_class, pred_density, target_density, points, offsets, order, bins_lo, bins_hi, cfg,
+              keep: bool):
+    (B, N, size, red, mode, norm, wc, wot, wtv, reg, iters, thr, freq, total, reduced) = cfg
+    dev = pred_density.device
+    g = size // red
+    pc = pred_class.detach().float().contiguous()
+    pd = pred_density.detach().float().contiguous()
+    td = target_density.detach().float().contiguous()
+    grad_c = torch.empty_like(pc)
+    grad_d = torch.empty_like(pd)
+    losses = torch.empty(5, device=dev, dtype=torch.float32)
+    stats = torch.empty(B, 8, device=dev, dtype=torch.float32)
+    beta = torch.empty(B, g * g, device=dev, dtype=torch.float32) if keep else None
+    status = torch.empty(B, device=dev, dtype=torch.int32) if keep else None
+    L = _lib.lib()
+    with _lib.on(dev):
+        ws_bytes = L.ebc_dace_workspace_bytes(B, total, size, red)
+        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+        rc = L.ebc_dace_loss(_lib.ptr(pc), _lib.ptr(pd, dev), _lib.ptr(td, dev), int(reduced), _lib.ptr(points, dev),
+                             _lib.ptr(offsets, dev), _lib.ptr(order, dev), _lib.ptr(bins_lo, dev), _lib.ptr(bins_hi, dev),
+                             B, N, size, red, mode, int(norm), wc, wot, wtv, reg, iters, thr, freq,
+                             _lib.ptr(grad_c), _lib.ptr(grad_d), _lib.ptr(losses), _lib.ptr(stats),
+                             _lib.ptr(beta), _lib.ptr(status), _lib.ptr(ws), ws_bytes, _lib.stream(dev))
+    _lib.check(rc, "ebc_dace_loss")
+    return losses, stats, grad_c, grad_d, (_Internals(beta, status, stats) if keep else None)
 
 
 class _DaceFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pred_class, pred_density, target_density, points, offsets, order, bins_lo, bins_hi,
-                cfg):
-        (B, N, size, red, mode, norm, wc, wot, wtv, reg, iters, thr, freq, total, reduced) = cfg
-        dev = pred_density.device
-        g = size // red
-        pc = pred_class.detach().float().contiguous()
-        pd = pred_density.detach().float().contiguous()
-        td = target_density.detach().float().contiguous()
-        grad_c = torch.empty_like(pc)
-        grad_d = torch.empty_like(pd)
-        losses = torch.empty(5, device=dev, dtype=torch.float32)
-        stats = torch.empty(B, 8, device=dev, dtype=torch.float32)
-        L = _lib.lib()
-        ws_bytes = L.ebc_dace_workspace_bytes(B, total, size, red)
-        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
-        rc = L.ebc_dace_loss(_lib.ptr(pc), _lib.ptr(pd), _lib.ptr(td), int(reduced), _lib.ptr(points),
-                             _lib.ptr(offsets), _lib.ptr(order), _lib.ptr(bins_lo), _lib.ptr(bins_hi),
-                             B, N, size, red, mode, int(norm), wc, wot, wtv, reg, iters, thr, freq,
-                             _lib.ptr(grad_c), _lib.ptr(grad_d), _lib.ptr(losses), _lib.ptr(stats),
-                             None, None, _lib.ptr(ws), ws_bytes, _lib.stream())
-        _lib.check(rc, "ebc_dace_loss")
+                cfg, sink):
+        losses, stats, grad_c, grad_d, internals = _run_dace(pred_class, pred_density, target_density, points,
+                                                             offsets, order, bins_lo, bins_hi, cfg, sink is not None)
+        if sink is not None:
+            sink.append(internals)
         ctx.save_for_backward(grad_c, grad_d)
         ctx.dtypes = (pred_class.dtype, pred_density.dtype)
         ctx.mark_non_differentiable(stats)
@@ -57,10 +106,11 @@ class _DaceFn(torch.autograd.Function):
         grad_c, grad_d = ctx.saved_tensors
         s = g_losses[0]
         return ((grad_c * s).to(ctx.dtypes[0]), (grad_d * s).to(ctx.dtypes[1]),
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def _pack_points(target_points: Sequence[Tensor], device) -> Tuple[Tensor, Tensor, Tensor, int]:
+    """The ragged label list -> packed [sum n, 2] f32 + offsets [B+1] + heaviest-first crop order (one H2D)."""
     counts = [int(p.shape[0]) for p in target_points]
     total = sum(counts)
     if total:
@@ -71,9 +121,21 @@ def _pack_points(target_points: Sequence[Tensor], device) -> Tuple[Tensor, Tenso
     for c in counts:
         offs.append(offs[-1] + c)
     order = sorted(range(len(counts)), key=lambda i: -counts[i])        # heaviest crops first
-    meta = torch.tensor(offs + order, dtype=torch.int32).pin_memory() if torch.cuda.is_available() else torch.tensor(offs + order, dtype=torch.int32)
+    meta = torch.tensor(offs + order, dtype=torch.int32)
+    if torch.cuda.is_available():
+        meta = meta.pin_memory()
     meta = meta.to(device, non_blocking=True)
     return pts, meta[: len(offs)], meta[len(offs):], total
+
+
+class _OTParams:
+    """OTLoss's configuration (losses/dm_loss.py:12-35)."""
+
+    def __init__(self, input_size, reduction, norm_cood, num_of_iter_in_ot=100, reg=10.0):
+        _check_geometry(input_size, reduction)
+        self.input_size, self.reduction, self.norm_cood = input_size, reduction, norm_cood
+        self.num_of_iter_in_ot, self.reg = num_of_iter_in_ot, reg
+        self.output_size = input_size // reduction
 
 
 class DACELoss(nn.Module):
@@ -94,6 +156,8 @@ class DACELoss(nn.Module):
         if self.use_dm_loss:
             assert "input_size" in kwargs, f"Expected input_size to be in kwargs when count_loss='dmcount', got {kwargs}"
             self.count_loss_fn = DMLoss(reduction=reduction, **kwargs)
+        elif reduction % 4:
+            raise NotImplementedError(f"ebc_amd DACE kernel: reduction {reduction} (needs reduction % 4 == 0)")
         self.weight_count_loss = weight_count_loss
         self.register_buffer("bins_lo", torch.tensor([float(b[0]) for b in bins], dtype=torch.float32), persistent=False)
         self.register_buffer("bins_hi", torch.tensor([float(b[1]) for b in bins], dtype=torch.float32), persistent=False)
@@ -104,6 +168,9 @@ class DACELoss(nn.Module):
         assert N == len(self.bins), f"pred_class has {N} channels, expected {len(self.bins)} bins"
         assert pred_density.shape == (B, 1, h, w), f"Expected pred_density [B,1,H,W], got {pred_density.shape}"
         assert h == w, "square crops only"
+        assert len(target_points) == B, f"Expected target_points to have length {B}, but got {len(target_points)}"
+        if h not in _GRIDS:
+            raise NotImplementedError(f"ebc_amd DACE kernel: density grid {h}x{w}; built for {_GRIDS}")
         reduced = tuple(target_density.shape[-2:]) == (h, w)
         size = h * self.reduction
         if not reduced:
@@ -122,7 +189,10 @@ class DACELoss(nn.Module):
                float(dm.weight_ot) if dm else 0.0, float(dm.weight_tv) if dm else 0.0,
                float(dm.ot_loss.reg) if dm else 10.0, int(dm.ot_loss.num_of_iter_in_ot) if dm else 0,
                1e-9, 10, total, reduced)
-        losses, _ = _DaceFn.apply(pred_class, pred_density, target_density, pts, offs, order, lo, hi, cfg)
+        sink = [] if (dm is not None and dm.keep_internals) else None
+        losses, _ = _DaceFn.apply(pred_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
+        if sink:
+            dm.internals = sink[0]
         d = losses.detach()
         if self.use_dm_loss:
             info = {k: d[i] for i, k in enumerate(_INFO_DM)}
@@ -131,37 +201,125 @@ class DACELoss(nn.Module):
         return losses[0], info
 
 
-class _OTParams:
-    def __init__(self, input_size, reduction, norm_cood, num_of_iter_in_ot=100, reg=10.0):
-        assert input_size % reduction == 0
-        self.input_size, self.reduction, self.norm_cood = input_size, reduction, norm_cood
-        self.num_of_iter_in_ot, self.reg = num_of_iter_in_ot, reg
+def _dummy_class(B: int, h: int, w: int, dev) -> Tuple[Tensor, Tensor, Tensor]:
+    """One bin covering every count: the fused kernel's CE part is log-softmax of a single logit = 0."""
+    return (torch.zeros(B, 1, h, w, device=dev, dtype=torch.float32), torch.zeros(1, device=dev),
+            torch.full((1,), float("inf"), device=dev))
 
 
 class DMLoss(nn.Module):
     """losses/dm_loss.py:82-124 (OT + TV + count) on the fused HIP kernel."""
 
     def __init__(self, input_size: int, reduction: int, norm_cood: bool = False, weight_ot: float = 0.1,
-                 weight_tv: float = 0.01, **kwargs: Any) -> None:
+                 weight_tv: float = 0.01, keep_internals: bool = False, **kwargs: Any) -> None:
         super().__init__()
         self.ot_loss = _OTParams(input_size, reduction, norm_cood, **kwargs)
         self.weight_ot = weight_ot
         self.weight_tv = weight_tv
+        self.keep_internals = keep_internals
+        self.internals: Optional[_Internals] = None
 
     def forward(self, pred_density: Tensor, target_density: Tensor, target_points: List[Tensor]):
         B, _, h, w = pred_density.shape
+        assert len(target_points) == B, f"Expected target_points to have length {B}, but got {len(target_points)}"
         dev = pred_density.device
         size = self.ot_loss.input_size
         reduced = tuple(target_density.shape[-2:]) == (h, w)
         pts, offs, order, total = _pack_points(target_points, dev)
-        # one dummy bin: the CE part of the fused kernel is computed on zero logits and discarded
-        zero_class = torch.zeros(B, 1, h, w, device=dev, dtype=torch.float32)
-        lo = torch.zeros(1, device=dev); hi = torch.full((1,), float("inf"), device=dev)
+        zero_class, lo, hi = _dummy_class(B, h, w, dev)
         cfg = (B, 1, size, self.ot_loss.reduction, _lib.EBC_COUNT_DMCOUNT, self.ot_loss.norm_cood, 1.0,
                float(self.weight_ot), float(self.weight_tv), float(self.ot_loss.reg),
                int(self.ot_loss.num_of_iter_in_ot), 1e-9, 10, total, reduced)
-        losses, _ = _DaceFn.apply(zero_class, pred_density, target_density, pts, offs, order, lo, hi, cfg)
+        sink = [] if self.keep_internals else None
+        losses, _ = _DaceFn.apply(zero_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
+        if sink:
+            self.internals = sink[0]
         d = losses.detach()
         loss = losses[0] - losses[4]   # remove the dummy CE (log 1 = 0 anyway)
         info = {"loss": d[0] - d[4], "ot_loss": d[1], "tv_loss": d[2], "count_loss": d[3]}
         return loss, info
+
+
+class OTLoss(nn.Module):
+    """losses/dm_loss.py:12-79: per crop, the entropic OT between the normalised predicted density and
+    the crop's points (uniform weights), returned as the surrogate loss sum(pred_density * gradient) whose
+    gradient w.r.t. pred_density is beta/count - <beta, density>/count^2 (dm_loss.py:65-76).
+
+    `normed_pred_density` must be pred_density / (count + 1e-8), which is what the reference's only
+    caller passes (dm_loss.py:106-108); the kernel forms it from `pred_density` itself.  `wd` (the
+    Wasserstein distance sum(C * P), dm_loss.py:77) is a host float as in the reference (one sync)."""
+
+    def __init__(self, input_size: int, reduction: int, norm_cood: bool, num_of_iter_in_ot: int = 100,
+                 reg: float = 10.0, keep_internals: bool = False) -> None:
+        super().__init__()
+        p = _OTParams(input_size, reduction, norm_cood, num_of_iter_in_ot, reg)
+        self.input_size, self.reduction, self.norm_cood = p.input_size, p.reduction, p.norm_cood
+        self.num_of_iter_in_ot, self.reg, self.output_size = p.num_of_iter_in_ot, p.reg, p.output_size
+        self.keep_internals = keep_internals
+        self.internals: Optional[_Internals] = None
+
+    def forward(self, pred_density: Tensor, normed_pred_density: Tensor,
+                target_points: List[Tensor]) -> Tuple[Tensor, float, Tensor]:
+        B = normed_pred_density.size(0)
+        assert len(target_points) == B, f"Expected target_points to have length {B}, but got {len(target_points)}"
+        assert self.output_size == normed_pred_density.size(2)
+        _, _, h, w = pred_density.shape
+        dev = pred_density.device
+        pts, offs, order, total = _pack_points(target_points, dev)
+        zero_class, lo, hi = _dummy_class(B, h, w, dev)
+        dummy_target = torch.zeros(B, 1, h, w, device=dev, dtype=torch.float32)
+        cfg = (B, 1, self.input_size, self.reduction, _lib.EBC_COUNT_OT_ONLY, self.norm_cood, 1.0, 1.0, 0.0,
+               float(self.reg), int(self.num_of_iter_in_ot), 1e-9, 10, total, True)
+        sink = []
+        losses, stats = _DaceFn.apply(zero_class, pred_density, dummy_target, pts, offs, order, lo, hi, cfg, sink)
+        it = sink[0]
+        if self.keep_internals:
+            self.internals = it
+        # ot_obj_values = sum over crops with points of <normed_pred_density, beta> (dm_loss.py:66)
+        has = torch.tensor([float(len(p) > 0) for p in target_points], device=dev).view(B, 1)
+        ot_obj = (normed_pred_density.detach().float().reshape(B, -1) * it.beta * has).sum().reshape(1)
+        wd = float(stats[:, 4].sum())
+        return losses[1].reshape(1), wd, ot_obj
+
+
+def sinkhorn(a: Tensor, b: Tensor, C: Tensor, reg: float = 1e-1, maxIter: int = 1000, stopThr: float = 1e-9,
+             verbose: bool = False, log: bool = True, eval_freq: int = 10, print_freq: int = 200):
+    """losses/bregman_pytorch.py:11-144 on one device launch (`ebc_sinkhorn`): every iteration, the
+    NaN/Inf rollback and the err checks stay on the GPU; the host reads the iteration count and the err
+    list once at the end (the reference syncs ~4 times per iteration).  Returns P, or (P, log) with log
+    keys err (list of floats), u, v, alpha, beta."""
+    if not (a.is_cuda and b.is_cuda and C.is_cuda):
+        raise RuntimeError("ebc_amd.sinkhorn runs on the MI355X HIP path only (inputs on the CPU)")
+    dev = a.device
+    na, nb = C.shape
+    assert na >= 1 and nb >= 1, f"C needs to be 2d. Found C.shape = {C.shape}"
+    assert na == a.shape[0] and nb == b.shape[0], f"Shape of a ({a.shape}) or b ({b.shape}) does not match that of C ({C.shape})"
+    assert reg > 0, f"reg should be greater than 0. Found reg = {reg}"
+    assert bool((a.min() >= 0.) & (b.min() >= 0.)), f"Elements in a and b should be nonnegative. Found a.min() = {a.min()}, b.min() = {b.min()}"
+    a32, b32, C32 = (t.detach().float().contiguous() for t in (a, b, C))
+    f32 = dict(device=dev, dtype=torch.float32)
+    P = torch.empty(na, nb, **f32)
+    u, v, alpha, beta = torch.empty(na, **f32), torch.empty(nb, **f32), torch.empty(na, **f32), torch.empty(nb, **f32)
+    nerr_max = max(1, -(-int(maxIter) // int(eval_freq)))
+    err = torch.empty(nerr_max, **f32)
+    info = torch.zeros(2, device=dev, dtype=torch.int32)
+    L = _lib.lib()
+    with _lib.on(dev):
+        wsb = L.ebc_sinkhorn_workspace_bytes(na, nb)
+        ws = torch.empty(max(wsb, 1), device=dev, dtype=torch.uint8)
+        rc = L.ebc_sinkhorn(_lib.ptr(a32), _lib.ptr(b32, dev), _lib.ptr(C32, dev), na, nb, float(reg), int(maxIter),
+                            float(stopThr), int(eval_freq), int(bool(log)), _lib.ptr(P), _lib.ptr(u), _lib.ptr(v),
+                            _lib.ptr(alpha), _lib.ptr(beta), _lib.ptr(err), _lib.ptr(info), _lib.ptr(ws), wsb,
+                            _lib.stream(dev))
+    _lib.check(rc, "ebc_sinkhorn")
+    iters, nerr = (int(x) for x in info.cpu())
+    if iters < 0:
+        print("Warning: numerical errors at iteration", -iters)          # bregman_pytorch.py:113
+    errs = [float(e) for e in err[:nerr].cpu()] if log else []
+    if verbose:
+        for k, e in enumerate(errs):
+            if ((k + 1) * eval_freq) % print_freq == 0:
+                print("iteration {:5d}, constraint error {:5e}".format((k + 1) * eval_freq, e))
+    if log:
+        return P, {"err": errs, "u": u, "v": v, "alpha": alpha, "beta": beta}
+    return P

@@ -172,6 +172,11 @@ class _VitFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cache, image, vpt_bstride, training, *vpts):
+        with _lib.on(image):
+            return _VitFn._forward(ctx, cache, image, vpt_bstride, training, *vpts)
+
+    @staticmethod
+    def _forward(ctx, cache, image, vpt_bstride, training, *vpts):
         L = _lib.lib()
         B, _, H, W = image.shape
         gh, gw = H // PATCH, W // PATCH
@@ -185,7 +190,7 @@ class _VitFn(torch.autograd.Function):
         arr = (_VP * cache.layers)(*([_p(v) for v in vp] + [None] * (cache.layers - len(vp))))
         w = cache.weights(gh, gw)
         rc = L.ebc_vit_forward(ctypes.byref(w), _lib.ptr(image), B, H, W, arr, vpt_bstride, dt, int(training),
-                               _lib.ptr(ws), nbytes, _lib.ptr(feat), _lib.stream())
+                               _lib.ptr(ws), nbytes, _lib.ptr(feat), _lib.stream(dev))
         _lib.check(rc, "ebc_vit_forward")
         ctx.cache, ctx.ws, ctx.shape, ctx.bstride = cache, ws, (B, H, W), vpt_bstride
         ctx.vpt_shapes = [v.shape for v in vpts]
@@ -194,6 +199,11 @@ class _VitFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dfeat):
+        with _lib.on(dfeat):
+            return _VitFn._backward(ctx, dfeat)
+
+    @staticmethod
+    def _backward(ctx, dfeat):
         L = _lib.lib()
         cache = ctx.cache
         B, H, W = ctx.shape
@@ -201,7 +211,7 @@ class _VitFn(torch.autograd.Function):
         arr = (_VP * cache.layers)(*([_p(v) for v in dvpt] + [None] * (cache.layers - len(dvpt))))
         w = cache.weights(H // PATCH, W // PATCH)
         rc = L.ebc_vit_backward(ctypes.byref(w), B, H, W, _lib.dtype_code(cache.dtype), _lib.ptr(ctx.ws), ctx.ws.numel(),
-                                _lib.ptr(dfeat.float().contiguous()), arr, ctx.bstride, _lib.stream())
+                                _lib.ptr(dfeat.float().contiguous()), arr, ctx.bstride, _lib.stream(dfeat))
         _lib.check(rc, "ebc_vit_backward")
         ctx.ws = None
         return (None, None, None, None) + tuple(dvpt)
@@ -215,7 +225,13 @@ class _HeadFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, weight, bias, logit_scale, text, anchors, cdtype, nhwc=False):
+        with _lib.on(y):
+            return _HeadFn._forward(ctx, y, weight, bias, logit_scale, text, anchors, cdtype, nhwc)
+
+    @staticmethod
+    def _forward(ctx, y, weight, bias, logit_scale, text, anchors, cdtype, nhwc):
         L = _lib.lib()
+        st = _lib.stream(y)
         if nhwc:
             B, Hh, Ww, C = y.shape
         else:
@@ -230,20 +246,26 @@ class _HeadFn(torch.autograd.Function):
         bf = bias.detach().float().contiguous()
         Z = torch.empty(P, EMBED, device=y.device, dtype=torch.float32)
         _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(Y), _lib.ptr(Wc), _lib.ptr(Z), _lib.ptr(bf), None, None,
-                              P, EMBED, C, _lib.stream()), "ebc_gemm(projection)")
+                              P, EMBED, C, st), "ebc_gemm(projection)")
         ls = logit_scale.detach().float().reshape(1).contiguous()
         logits = torch.empty(B, NB, Hh, Ww, device=y.device, dtype=torch.float32)
         expo = torch.empty(B, 1, Hh, Ww, device=y.device, dtype=torch.float32)
         _lib.check(L.ebc_head_fwd(_lib.EBC_F32, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
-                                  _lib.ptr(logits), _lib.ptr(expo), P, HW, NB, _lib.stream()), "ebc_head_fwd")
+                                  _lib.ptr(logits), _lib.ptr(expo), P, HW, NB, st), "ebc_head_fwd")
         ctx.save_for_backward(Y, Wc, Z, ls, text, anchors)
         ctx.meta = (B, C, Hh, Ww, cdtype, y.dtype, weight.shape, nhwc)
         return logits, expo
 
     @staticmethod
     def backward(ctx, dlogits, dexp):
+        with _lib.on(ctx.saved_tensors[2]):
+            return _HeadFn._backward(ctx, dlogits, dexp)
+
+    @staticmethod
+    def _backward(ctx, dlogits, dexp):
         L = _lib.lib()
         Y, Wc, Z, ls, text, anchors = ctx.saved_tensors
+        st = _lib.stream(Z)
         B, C, Hh, Ww, cdtype, ydt, wshape, nhwc = ctx.meta
         P, HW, NB = B * Hh * Ww, Hh * Ww, text.shape[0]
         dev = Z.device
@@ -255,11 +277,11 @@ class _HeadFn(torch.autograd.Function):
         dscale = torch.empty(1, device=dev, dtype=torch.float32)
         _lib.check(L.ebc_head_bwd(_lib.EBC_F32, dt, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
                                   _lib.ptr(dl), _lib.ptr(de), None, _lib.ptr(dZ), _lib.ptr(dbias), _lib.ptr(dscale),
-                                  P, HW, NB, _lib.stream()), "ebc_head_bwd")
+                                  P, HW, NB, st), "ebc_head_bwd")
         Wt = Wc.t().contiguous()                                   # [C, 512]
         dY = torch.empty(P, C, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dZ), _lib.ptr(Wt), _lib.ptr(dY), None, None, None,
-                              P, C, EMBED, _lib.stream()), "ebc_gemm(projection dX)")
+                              P, C, EMBED, st), "ebc_gemm(projection dX)")
         # dW = dZ^T Y over K = B*H*W pixels: both operands transposed to K-contiguous, split-K MFMA GEMM
         # (K padded with zero columns to the GEMM's K step when B*H*W is not a multiple of it)
         kstep = 32 if cdtype == torch.float32 else 64
@@ -267,13 +289,13 @@ class _HeadFn(torch.autograd.Function):
         alloc = torch.empty if Pp == P else torch.zeros
         dZT = alloc(EMBED, Pp, device=dev, dtype=cdtype)
         YT = alloc(C, Pp, device=dev, dtype=cdtype)
-        _lib.check(L.ebc_transpose(dt, _lib.ptr(dZ), _lib.ptr(dZT), P, EMBED, Pp, _lib.stream()), "ebc_transpose(dZ)")
-        _lib.check(L.ebc_transpose(dt, _lib.ptr(Y), _lib.ptr(YT), P, C, Pp, _lib.stream()), "ebc_transpose(Y)")
+        _lib.check(L.ebc_transpose(dt, _lib.ptr(dZ), _lib.ptr(dZT), P, EMBED, Pp, st), "ebc_transpose(dZ)")
+        _lib.check(L.ebc_transpose(dt, _lib.ptr(Y), _lib.ptr(YT), P, C, Pp, st), "ebc_transpose(Y)")
         dW = torch.empty(EMBED, C, device=dev, dtype=torch.float32)
         nb = L.ebc_gemm_wgrad_workspace_bytes(dt, EMBED, C, Pp)
         ws = _dec_workspace(dev, nb, slot=2)
         _lib.check(L.ebc_gemm_wgrad(dt, _lib.ptr(dZT), _lib.ptr(YT), _lib.ptr(dW), EMBED, C, Pp, _lib.ptr(ws), ws.numel(),
-                                    _lib.stream()), "ebc_gemm_wgrad(projection dW)")
+                                    st), "ebc_gemm_wgrad(projection dW)")
         dW = dW.reshape(wshape)
         dy = dY.view(B, Hh, Ww, C) if nhwc else dY.view(B, Hh, Ww, C).permute(0, 3, 1, 2).to(ydt)
         return dy, dW, dbias, dscale.reshape(()), None, None, None, None
@@ -332,13 +354,18 @@ class _DecoderFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, feat, w1, g1, b1, w2, g2, b2, blk, up, cdtype, training):
+        with _lib.on(feat):
+            return _DecoderFn._forward(ctx, feat, w1, g1, b1, w2, g2, b2, blk, up, cdtype, training)
+
+    @staticmethod
+    def _forward(ctx, feat, w1, g1, b1, w2, g2, b2, blk, up, cdtype, training):
         L = _lib.lib()
         feat = feat.detach().contiguous()
         B, h, w, C = feat.shape
         H, W, N = h * up, w * up, w1.shape[0]
         if N != C or w2.shape[0] != C or C % 64:
             raise NotImplementedError("fused decoder: BasicBlock(C, C) with C % 64 == 0 only")
-        dev, dt, st = feat.device, _lib.dtype_code(cdtype), _lib.stream()
+        dev, dt, st = feat.device, _lib.dtype_code(cdtype), _lib.stream(feat)
         geo = (ctypes.c_long * 6)()
         _lib.check(L.ebc_dec_geometry(dt, B, H, W, C, geo), "ebc_dec_geometry")
         Q, Qs = geo[4], geo[5]
@@ -360,14 +387,18 @@ class _DecoderFn(torch.autograd.Function):
             wflip.append(wf)
             z = torch.empty(P, N, device=dev, dtype=cdtype)
             use_batch = training or not bn.track_running_stats
-            colsum = torch.empty(2, N, device=dev, dtype=torch.float64) if use_batch else None
+            pg = _bn_group(bn) if use_batch else None
+            # SyncBatchNorm: [sum | sum of squares | this rank's count] all-reduced in ONE f64 buffer, the total
+            # count read on device (count = -1), so ranks may hold different batch sizes (torch.nn.SyncBatchNorm
+            # gathers the per-rank counts the same way)
+            colsum = torch.empty(2 * N + (pg is not None), device=dev, dtype=torch.float64) if use_batch else None
             _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(inp), _lib.ptr(wk), _lib.ptr(z), _lib.ptr(colsum), None, None,
                                          _lib.ptr(ws), ws.numel(), B, H, W, C, N, st), "ebc_conv3x3_fwd")
             count = float(P)
-            pg = _bn_group(bn) if use_batch else None
             if pg is not None:
+                colsum[2 * N].fill_(float(P))
                 torch.distributed.all_reduce(colsum, group=pg)
-                count *= torch.distributed.get_world_size(pg)
+                count = -1.0
             mean, rstd, scale, shift = (torch.empty(N, **f32) for _ in range(4))
             upd = use_batch and training and bn.track_running_stats
             if upd:
@@ -378,13 +409,13 @@ class _DecoderFn(torch.autograd.Function):
                                          _lib.ptr(shift), _lib.ptr(bn.running_mean) if (upd or not use_batch) else None,
                                          _lib.ptr(bn.running_var) if (upd or not use_batch) else None, N, st),
                        "ebc_bn_finalize")
-            outs.append((z, mean, rstd, scale, shift, count, pg))
+            outs.append((z, mean, rstd, scale, shift, count, pg, colsum))
             if i == 0:
                 hpad = torch.empty(Q, N, device=dev, dtype=cdtype)
                 _lib.check(L.ebc_bn_relu_pad(dt, _lib.ptr(z), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(hpad),
                                              B, H, W, N, st), "ebc_bn_relu_pad")
                 inp = hpad
-        z2, _, _, scale2, shift2, _, _ = outs[1]
+        z2, _, _, scale2, shift2, _, _, _ = outs[1]
         y = torch.empty(B, H, W, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_bn_add_relu(dt, _lib.ptr(z2), _lib.ptr(scale2), _lib.ptr(shift2), _lib.ptr(feat), up,
                                      _lib.ptr(y), B, H, W, N, st), "ebc_bn_add_relu")
@@ -395,10 +426,15 @@ class _DecoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        with _lib.on(gy):
+            return _DecoderFn._backward(ctx, gy)
+
+    @staticmethod
+    def _backward(ctx, gy):
         L = _lib.lib()
         xpad, hpad, y, wf1, g1, wf2, g2 = ctx.saved_tensors
         B, h, w, H, W, C, N, up, cdtype, Q, Qs, P = ctx.meta
-        dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream()
+        dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream(y)
         gy = gy.to(cdtype).contiguous()
         nbytes = L.ebc_dec_workspace_bytes(dt, B, H, W, C, N)
         ws = _dec_workspace(dev, nbytes)
@@ -410,14 +446,15 @@ class _DecoderFn(torch.autograd.Function):
         dnext = gy                                    # gradient at the current BN output's ReLU
         mask = y                                      # ReLU mask source (None: recompute from z)
         for i in (1, 0):
-            z, mean, rstd, scale, shift, count, pg = ctx.outs[i]
+            z, mean, rstd, scale, shift, count, pg, colsum = ctx.outs[i]
             gm = (g1, g2)[i]
-            sums = torch.empty(2, N, device=dev, dtype=torch.float64)
+            sums = torch.empty(2 * N + (pg is not None), device=dev, dtype=torch.float64)
             _lib.check(L.ebc_bn_bwd_reduce(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
                                            _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(sums),
                                            _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce")
             if pg is not None:
-                torch.distributed.all_reduce(sums, group=pg)
+                torch.distributed.all_reduce(sums[: 2 * N], group=pg)     # sum_dy, sum_dy_xmu (torch SyncBN C5)
+                sums[2 * N:].copy_(colsum[2 * N:])                          # the forward's all-reduced count
             dg, db, coef = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty(3, N, **f32)
             _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
                                              _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize")
@@ -467,7 +504,7 @@ class CLIP_EBC(nn.Module):
                  reduction: Optional[int] = None, freeze_text_encoder: bool = True, prompt_type: str = "number",
                  input_size: Optional[int] = None, num_vpt: Optional[int] = None, deep_vpt: Optional[bool] = None,
                  vpt_drop: Optional[float] = None, decoder_cfg: Optional[List[int]] = None, vit_layers: int = 12,
-                 text_layers: int = 12, text_features: Optional[Tensor] = None, weights_seed: Optional[int] = 0,
+                 text_layers: int = 12, text_features: Optional[Tensor] = None, weights_seed: Optional[int] = None,
                  **kwargs: Any) -> None:
         super().__init__()
         if backbone not in vit_backbones:

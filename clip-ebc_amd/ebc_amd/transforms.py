@@ -220,7 +220,7 @@ class CropAugment:
         ddesc = _upload(descs, dev)
         src_base = ctypes.c_void_p(base)
         _lib.check(L.ebc_augment_crops(src_base, _lib.ptr(ddesc), n, max_ch, out_h, _lib.ptr(out), _lib.ptr(ws),
-                                       self.const, _lib.stream()), "ebc_augment_crops")
+                                       self.const, _lib.stream(dev)), "ebc_augment_crops")
         return out     # temporaries are released stream-ordered (caching allocator), after the launches
 
     def _resize_whole(self, img: Tensor, h: int, w: int) -> Tensor:
@@ -235,7 +235,7 @@ class CropAugment:
         ws = torch.empty(3 * max(img.shape[1], h) * w, device=img.device)
         ddesc = _upload(d, img.device)
         _lib.check(L.ebc_augment_crops(_lib.ptr(img), _lib.ptr(ddesc), 1, img.shape[1], h, _lib.ptr(out), _lib.ptr(ws),
-                                       self.const, _lib.stream()), "ebc_augment_crops (pre-resize)")
+                                       self.const, _lib.stream(img)), "ebc_augment_crops (pre-resize)")
         return out[0]
 
     def __call__(self, images: Sequence[Tensor], labels: Sequence[Tensor], num_crops: int = 1):
@@ -265,5 +265,5 @@ def generate_density_map(points: Sequence[Tensor], height: int, width: int, devi
     doffs = torch.tensor(offs, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
     out = torch.empty(B, 1, height, width, device=dev)
     _lib.check(L.ebc_point_map(_lib.ptr(dpts), _lib.ptr(doffs), B, height, width, max(counts, default=0), _lib.ptr(out),
-                               _lib.stream()), "ebc_point_map")
+                               _lib.stream(dev)), "ebc_point_map")
     return out

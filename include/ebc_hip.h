@@ -28,7 +28,7 @@ typedef void* ebc_stream_t;
 
 enum { EBC_F32 = 0, EBC_F16 = 1, EBC_BF16 = 2 };
 enum { EBC_OK = 0, EBC_E_ARG = -1, EBC_E_LAUNCH = -2, EBC_E_UNSUPPORTED = -3 };
-enum { EBC_COUNT_DMCOUNT = 0, EBC_COUNT_MAE = 1, EBC_COUNT_MSE = 2 };
+enum { EBC_COUNT_DMCOUNT = 0, EBC_COUNT_MAE = 1, EBC_COUNT_MSE = 2, EBC_COUNT_OT_ONLY = 3 };
 
 /* Library version / self-description (host-only, no device work). */
 int ebc_version(void);
@@ -51,7 +51,11 @@ int ebc_version(void);
  *   losses       [5] f32: loss, ot_loss, tv_loss, count_loss, ce_loss (loss_info keys)
  *   crop_stats   [B, 8] f32: ce_b, tv_b*n_b, count_b, ot_b, wd_b, iters, rolled_back, err_last
  *   beta_out     [B, g*g] f32 or NULL;  status [B] int32 or NULL (iterations, negative = rollback)
- * count_mode: EBC_COUNT_DMCOUNT / _MAE / _MSE (DACELoss count_loss="dmcount"/"mae"/"mse").
+ * count_mode: EBC_COUNT_DMCOUNT / _MAE / _MSE (DACELoss count_loss="dmcount"/"mae"/"mse"), or
+ *   EBC_COUNT_OT_ONLY: OTLoss.forward alone (losses/dm_loss.py:38-79): grad_density = the OT gradient
+ *   (weight_count_loss * weight_ot times it), losses[1] = sum of the crops' OT losses, no TV / count terms.
+ * size / reduction (the density grid g) must be 28 or 56 (224 or 448 crops at reduction 8, 448 at 16);
+ * grid cell k sits at k * reduction + reduction / 2 (dm_loss.py:31).
  * norm_cood: OTLoss norm_cood (dm_loss.py:31-34,51): coordinates mapped to [-1, 1].
  * workspace: ebc_dace_workspace_bytes(...) bytes of device memory.
  */
@@ -66,6 +70,20 @@ int ebc_dace_loss(const float* pred_class, const float* pred_density, const floa
                   ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
+ * General dense Sinkhorn-Knopp, one problem: replaces sinkhorn(a, b, C, reg, maxIter, stopThr, verbose,
+ * log, eval_freq, print_freq) (losses/bregman_pytorch.py:11-144) for callers of that function itself
+ * (the DMCount path uses ebc_dace_loss, whose cost is separable).  a [na], b [nb], C [na, nb] f32.
+ * Outputs (each may be NULL except info): P [na, nb] = u K v; u [na], v [nb]; alpha = reg log(u + 1e-16),
+ * beta = reg log(v + 1e-16); err [ceil(max_iter / eval_freq)] (the log's err list, only when log != 0);
+ * info [2] int32 = {iterations run (negative: NaN/Inf rollback at that iteration), err entries}.
+ * workspace: ebc_sinkhorn_workspace_bytes(na, nb) bytes (0 when K fits LDS).  EBC_E_UNSUPPORTED when
+ * u and v together exceed LDS (na + nb beyond ~20000). */
+size_t ebc_sinkhorn_workspace_bytes(int na, int nb);
+int ebc_sinkhorn(const float* a, const float* b, const float* C, int na, int nb, float reg, int max_iter,
+                 float stop_thr, int eval_freq, int log, float* P, float* u, float* v, float* alpha, float* beta,
+                 float* err, int* info, void* workspace, size_t workspace_bytes, ebc_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
  * GEMM  C[M,N] = A[M,K] . B[N,K]^T (+bias[N]) with a fused epilogue.  A, B of `dtype`; K % 64 == 0
  * (K % 32 for f32), N % 64 == 0.  Replaces the nn.Linear / nn.MultiheadAttention projections of
  * ResidualAttentionBlock (models/clip/_clip/blocks.py:22-42), the patch-embed conv1
@@ -78,6 +96,10 @@ int ebc_dace_loss(const float* pred_class, const float* pred_density, const floa
 enum { EBC_EPI_STORE = 0, EBC_EPI_GELU = 1, EBC_EPI_RESID = 2, EBC_EPI_GELU_BWD = 3 };
 int ebc_gemm(int dtype, int epilogue, int out_f32, const void* A, const void* B, void* C,
              const float* bias, const float* resid, void* aux, int M, int N, int K, ebc_stream_t stream);
+/* The tile configuration ebc_gemm / ebc_gemm_ws dispatch for this shape (host-only, no device work):
+ * returns the configuration id (> 0; EBC_GEMM_CFG overrides are honoured as in the launch) and writes
+ * out[3] = {tile rows, tile columns, split-K factor}.  Lets tests pin which kernel instance a shape runs. */
+int ebc_gemm_tile_config(int dtype, int M, int N, int K, int* out);
 /* Same, allowed to split K over workgroups (16-bit dtypes) when the output has too few 256-wide
  * tiles to fill the GPU.  `workspace` (>= ebc_gemm_workspace_bytes; 0 = no split for this shape)
  * must be zero-filled before its first use and is then owned by the stream: every call leaves
@@ -229,11 +251,18 @@ int ebc_dec_upsample_pad(int dtype, const float* feat, void* xpad, int B, int h,
  * gradient of conv1): out += add_gy * (add_y > 0), the residual branch's gradient through the final ReLU */
 int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, double* colsum, const void* add_gy,
                     const void* add_y, void* ws, size_t wsb, int B, int H, int W, int C, int N, ebc_stream_t stream);
+/* The implicit-GEMM tile configuration of a decoder conv product (mode 1: forward / data gradient,
+ * M = B*H*W rows, N output channels, K = 9*C; mode 2: weight gradient, M = N channels, N = 9*C,
+ * K = interior pixel rows): returns its id, out[3] = {tile rows, tile columns, split-K}. Host-only. */
+int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, int* out);
 /* dw[N][C][3][3] f32 = weight gradient from dzT and xT3 */
 int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, float* dw, void* ws, size_t wsb, int B, int H,
                       int W, int C, int N, ebc_stream_t stream);
 /* BatchNorm2d statistics -> mean, rstd, scale = gamma*rstd, shift = beta - mean*scale; running stats
- * updated (momentum, unbiased variance) when colsum != NULL, read (eval) when colsum == NULL */
+ * updated (momentum, unbiased variance) when colsum != NULL, read (eval) when colsum == NULL.
+ * count < 0: the element count is the DEVICE value colsum[2*C] (SyncBatchNorm: each rank stores its own
+ * count there and all-reduces it with the sums, so ranks may hold different batch sizes, as
+ * torch.nn.SyncBatchNorm allows) */
 int ebc_bn_finalize(const double* colsum, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* mean, float* rstd, float* scale, float* shift, float* running_mean,
                     float* running_var, int C, ebc_stream_t stream);
@@ -247,7 +276,7 @@ int ebc_bn_add_relu(int dtype, const void* z, const float* scale, const float* s
 int ebc_bn_bwd_reduce(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
                       const float* rstd, const float* scale, const float* shift, double* sums, void* ws, size_t wsb,
                       long P, int C, ebc_stream_t stream);
-/* dgamma, dbeta (may be NULL) and coef[3][C] for ebc_bn_bwd_apply */
+/* dgamma, dbeta (may be NULL) and coef[3][C] for ebc_bn_bwd_apply; count < 0: device count at sums[2*C] */
 int ebc_bn_bwd_finalize(const double* sums, double count, const float* gamma, const float* rstd, float* dgamma,
                         float* dbeta, float* coef, int C, ebc_stream_t stream);
 /* dz = BatchNorm input gradient -> dzpad (padded NHWC) and dzT (transposed) */
@@ -261,6 +290,26 @@ int ebc_dec_prep_weights(int dtype, const float* w, void* wk, void* wf, int N, i
 /* dfeat [B][h][w][C] f32 = bilinear_up^T(g), g [B*H*W][C] (up = 1 or 2) */
 int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int B, int h, int w, int C, int up,
                          ebc_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Measurement (bench.py): in-step kernel durations and profile windows.  Not on the reference's
+ * surface; the reference has no instrumentation.
+ * ebc_probe_begin(capacity): from now on every launch of the instrumented kernels is bracketed by HIP
+ *   events on its own stream (at most `capacity` launches recorded).
+ * ebc_probe_end(out, capacity): stops recording, waits for the last event and writes one record per
+ *   launch (returns the number recorded; records beyond `capacity` are dropped).
+ * ebc_marker(id, stream): launches the named empty kernel `ebc_marker_kernel` (profile window edges). */
+enum { EBC_PROBE_GEMM = 1, EBC_PROBE_DACE = 2, EBC_PROBE_ATTN_FWD = 3, EBC_PROBE_ATTN_BWD_DQ = 4,
+       EBC_PROBE_ATTN_BWD_DKV = 5, EBC_PROBE_LN_FWD = 6, EBC_PROBE_LN_BWD = 7 };
+typedef struct {
+    int kind;                 /* EBC_PROBE_* */
+    int epi, bm, bn, mode;    /* GEMM: epilogue, tile, MODE (0 plain, 1 implicit 3x3 conv, 2 conv weight gradient) */
+    int m, n, k;              /* GEMM: problem; DACE: B, total points, grid g; attention: B, L, heads; LN: rows */
+    float ms;                 /* measured duration */
+} EbcProbeRecord;
+int ebc_probe_begin(int capacity);
+int ebc_probe_end(EbcProbeRecord* out, int capacity);
+int ebc_marker(int id, ebc_stream_t stream);
 
 #ifdef __cplusplus
 }

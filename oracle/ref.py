@@ -30,9 +30,13 @@ def oracle_lib() -> ctypes.CDLL:
         f = lib.oracle_ot_crop
         fp = ctypes.POINTER(ctypes.c_float)
         dp = ctypes.POINTER(ctypes.c_double)
-        f.argtypes = [fp, ctypes.c_int, fp, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+        f.argtypes = [fp, ctypes.c_int, fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                       ctypes.c_float, ctypes.c_int, fp, fp, fp, fp, ctypes.POINTER(ctypes.c_int), fp, dp, dp, dp]
         f.restype = ctypes.c_int
+        s = lib.oracle_sinkhorn
+        s.argtypes = [fp, fp, fp, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_float,
+                      ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, fp, fp, ctypes.POINTER(ctypes.c_int)]
+        s.restype = ctypes.c_int
         _LIB = lib
     return _LIB
 
@@ -42,7 +46,7 @@ def _fp(a: np.ndarray):
 
 
 def ot_crop(points: np.ndarray, pred_density: np.ndarray, size: int, reduction: int = 8, reg: float = 10.0,
-            max_iter: int = 100, stop_thr: float = 1e-9, eval_freq: int = 10) -> Dict[str, np.ndarray]:
+            max_iter: int = 100, stop_thr: float = 1e-9, eval_freq: int = 10, norm_cood: bool = False) -> Dict[str, np.ndarray]:
     """One crop of OTLoss.forward (losses/dm_loss.py:49-77) + sinkhorn (bregman_pytorch.py:11-144)."""
     lib = oracle_lib()
     g = size // reduction
@@ -54,12 +58,28 @@ def ot_crop(points: np.ndarray, pred_density: np.ndarray, size: int, reduction: 
     beta = np.zeros(M, np.float32); v = np.zeros(M, np.float32); grad = np.zeros(M, np.float32)
     u = np.zeros(max(n, 1), np.float32); err = np.full(max_iter // eval_freq + 1, -1.0, np.float32)
     ne = ctypes.c_int(0); wd = ctypes.c_double(0); obj = ctypes.c_double(0); loss = ctypes.c_double(0)
-    it = lib.oracle_ot_crop(_fp(pts), n, _fp(pd), size, reduction, reg, max_iter, stop_thr, eval_freq,
+    it = lib.oracle_ot_crop(_fp(pts), n, _fp(pd), size, reduction, int(norm_cood), reg, max_iter, stop_thr, eval_freq,
                             _fp(beta), _fp(u), _fp(v), _fp(err), ctypes.byref(ne), _fp(grad),
                             ctypes.byref(wd), ctypes.byref(obj), ctypes.byref(loss))
     return dict(beta=beta, u=u[:n], v=v, err=err[:ne.value], ot_grad=grad, wd=wd.value, ot_obj=obj.value,
                 loss=loss.value, iters=abs(it), rolled_back=it < 0)
 
+
+
+def sinkhorn(a: np.ndarray, b: np.ndarray, C: np.ndarray, reg: float, max_iter: int, stop_thr: float = 1e-9,
+             eval_freq: int = 10, log: bool = True) -> Dict[str, np.ndarray]:
+    """bregman_pytorch.py:11-144 on a general dense cost (the C restatement)."""
+    lib = oracle_lib()
+    na, nb = C.shape
+    a = np.ascontiguousarray(a, np.float32); b = np.ascontiguousarray(b, np.float32)
+    C = np.ascontiguousarray(C, np.float32)
+    P = np.zeros((na, nb), np.float32); u = np.zeros(na, np.float32); v = np.zeros(nb, np.float32)
+    alpha = np.zeros(na, np.float32); beta = np.zeros(nb, np.float32)
+    err = np.zeros(max(1, -(-max_iter // eval_freq)), np.float32); ne = ctypes.c_int(0)
+    it = lib.oracle_sinkhorn(_fp(a), _fp(b), _fp(C), na, nb, reg, max_iter, stop_thr, eval_freq, int(log), _fp(P),
+                             _fp(u), _fp(v), _fp(alpha), _fp(beta), _fp(err), ctypes.byref(ne))
+    return dict(P=P, u=u, v=v, alpha=alpha, beta=beta, err=err[:ne.value], iters=abs(it), rolled_back=it < 0,
+                roll=-it if it < 0 else 0)
 
 # ----------------------------------------------------------------------------- loss
 def reshape_density(d: torch.Tensor, r: int) -> torch.Tensor:
@@ -91,7 +111,8 @@ class _OTGrad(torch.autograd.Function):
 
 def dace_loss(pred_class: torch.Tensor, pred_density: torch.Tensor, target_density: torch.Tensor,
               points: List[np.ndarray], bins, reduction: int = 8, input_size: int = 224,
-              weight_count_loss: float = 1.0, weight_ot: float = 0.1, weight_tv: float = 0.01):
+              weight_count_loss: float = 1.0, weight_ot: float = 0.1, weight_tv: float = 0.01,
+              norm_cood: bool = False):
     """DACELoss(count_loss='dmcount').forward — dace_loss.py:49-70 with DMLoss dm_loss.py:99-124."""
     if target_density.shape[-2:] != pred_density.shape[-2:]:
         target_density = reshape_density(target_density, reduction)
@@ -106,7 +127,7 @@ def dace_loss(pred_class: torch.Tensor, pred_density: torch.Tensor, target_densi
     pdn = pred_density.detach().cpu().numpy()
     for b, p in enumerate(points):
         if len(p) > 0:
-            grads[b] = ot_crop(p, pdn[b, 0], input_size, reduction)["ot_grad"].reshape(pdn.shape[1:])
+            grads[b] = ot_crop(p, pdn[b, 0], input_size, reduction, norm_cood=norm_cood)["ot_grad"].reshape(pdn.shape[1:])
     ot_loss = _OTGrad.apply(pred_density, torch.from_numpy(grads))
     tv = ((normed_pred - normed_target).abs().sum(dim=(1, 2, 3)) * target_count).mean()
     cnt = (pred_count - target_count).abs().mean()

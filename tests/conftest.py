@@ -16,6 +16,19 @@ ANCHORS_NWPU = [0.0, 1.0, 2.0, 3.0, 4.21931]
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device) and the built libebc_hip.so")
+    mexpr = config.getoption("markexpr", "") or ""
+    if "gpu" in mexpr and "not gpu" not in mexpr:
+        # Multi-process GPU tests (test_gpu_ddp.py) start their ranks from a forkserver launched NOW, before
+        # this process touches the GPU: a process that has initialised HIP must never exec (the ranks are
+        # forked from the server, which never initialises HIP).  PYTHONPATH lets the server import the
+        # rank bodies.
+        import multiprocessing as mp
+        from multiprocessing import forkserver
+        here = os.path.dirname(os.path.abspath(__file__))
+        os.environ["PYTHONPATH"] = os.pathsep.join([here, REPO, os.path.join(REPO, "clip-ebc_amd")] +
+                                                   [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+        mp.get_context("forkserver")
+        forkserver.ensure_running()
 
 
 def golden(name: str):

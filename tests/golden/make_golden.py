@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 REF = "/root/reference"
+sys.dont_write_bytecode = True          # never write __pycache__ into the (read-only) reference tree
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
 sys.path.insert(0, os.path.join(REPO, "clip-ebc_amd"))
@@ -170,6 +171,122 @@ def loss_case(ref, size: int, counts, seed: int):
     return out
 
 
+def _capture_sinkhorn(ref):
+    """Wrap the reference's sinkhorn as dm_loss.py calls it: record every call's log and the
+    iteration its NaN/Inf rollback warning names (bregman_pytorch.py:111-115)."""
+    import contextlib
+    import io
+    dm = sys.modules["losses.dm_loss"]
+    calls = []
+    orig = dm.sinkhorn
+
+    def wrapped(*a, **k):
+        f = io.StringIO()
+        with contextlib.redirect_stdout(f):
+            r = orig(*a, **k)
+        msg = f.getvalue().strip()
+        calls.append((r, int(msg.split()[-1]) if msg else 0))
+        return r
+    dm.sinkhorn = wrapped
+    return calls, lambda: setattr(dm, "sinkhorn", orig)
+
+
+def sinkhorn_case(ref):
+    """F1b: the reference `sinkhorn` on general dense problems (losses/bregman_pytorch.py:11-144): early
+    stop on stopThr, the NaN/Inf rollback at iteration 1 (a negative cost: K = inf) and 2 (marginals of
+    mass 1 vs 1e24), log=False (err never updated: every iteration runs), a DMCount-shaped crop and one
+    whose K exceeds LDS.  Inputs are stored (they are small); `roll` = the iteration of the warning."""
+    import contextlib
+    import io
+    out = {}
+    cases = []
+    g = torch.Generator().manual_seed(4242)
+    # 0: converges before maxIter (loose stopThr)
+    C = torch.rand(9, 30, generator=g) * 20
+    a = torch.rand(9, generator=g); a /= a.sum(); b = torch.rand(30, generator=g); b /= b.sum()
+    cases.append((a, b, C, 5.0, 1000, 1e-4, True))
+    # 1: a negative cost -> K = inf -> NaN at iteration 1
+    C = torch.rand(5, 16, generator=g) * 5; C[1, 3] = -2000.0
+    a = torch.ones(5) / 5; b = torch.rand(16, generator=g); b /= b.sum()
+    cases.append((a, b, C, 1.0, 50, 1e-9, True))
+    # 2: |b| = 1e24 vs |a| = 1: v overflows at iteration 2
+    C = torch.rand(7, 20, generator=torch.Generator().manual_seed(1)) * 4
+    a = torch.ones(7) / 7; b = torch.rand(20, generator=torch.Generator().manual_seed(2)); b = b / b.sum() * 1e24
+    cases.append((a, b, C, 0.5, 100, 1e-9, True))
+    # 3: log=False: err stays 1, all maxIter iterations run
+    C = torch.rand(12, 50, generator=g) * 30
+    a = torch.rand(12, generator=g); a /= a.sum(); b = torch.rand(50, generator=g); b /= b.sum()
+    cases.append((a, b, C, 3.0, 37, 1e-9, False))
+    # 4, 5: DMCount-shaped (pixel costs at 224, reduction 8, reg 10): 47 points (K in LDS), 300 points (K global)
+    cood = torch.arange(0, 224, step=8, dtype=torch.float32).unsqueeze(0) + 4.0
+    for n in (47, 300):
+        pts = torch.rand(n, 2, generator=g) * 224
+        x = pts[:, 0].unsqueeze(1); y = pts[:, 1].unsqueeze(1)
+        xd = -2 * torch.matmul(x, cood) + x * x + cood * cood
+        yd = -2 * torch.matmul(y, cood) + y * y + cood * cood
+        C = (yd.unsqueeze(2) + xd.unsqueeze(1)).view(n, -1)
+        b = torch.rand(784, generator=g); b /= b.sum()
+        cases.append((torch.ones(n) / n, b, C, 10.0, 100, 1e-9, True))
+    for i, (a, b, C, reg, it, thr, log) in enumerate(cases):
+        f = io.StringIO()
+        with contextlib.redirect_stdout(f):
+            r = ref.sinkhorn(a, b, C, reg, maxIter=it, stopThr=thr, log=log)
+        msg = f.getvalue().strip()
+        P, lg = (r if log else (r, None))
+        out[f"a_{i}"], out[f"b_{i}"], out[f"C_{i}"] = a.numpy(), b.numpy(), C.numpy()
+        out[f"cfg_{i}"] = np.asarray([reg, it, thr, float(log)], np.float64)
+        out[f"P_{i}"] = P.numpy()
+        out[f"roll_{i}"] = np.asarray(int(msg.split()[-1]) if msg else 0)
+        if log:
+            for k in ("u", "v", "alpha", "beta"):
+                out[f"{k}_{i}"] = lg[k].numpy()
+            out[f"err_{i}"] = np.asarray(lg["err"], np.float32)
+    out["n_cases"] = np.asarray(len(cases))
+    return out
+
+
+def loss_extra_case(ref):
+    """F1c: DACE/DMCount beyond the default geometry: reduction 16 at 448 (grid 28, cell pitch 16) and
+    norm_cood=True (coordinates in [-1, 1]: dense K); per-crop beta and any rollback iteration recorded
+    through the reference's own sinkhorn.  (A NaN density cannot reach the rollback there: sinkhorn
+    asserts b >= 0 first, bregman_pytorch.py:81.)"""
+    out = {}
+    calls, restore = _capture_sinkhorn(ref)
+    specs = [("r16", 448, 16, False, [0, 30, 300, 4], 303), ("norm", 224, 8, True, [12, 0, 150], 304)]
+    for tag, size, red, norm, counts, seed in specs:
+        g = np.random.Generator(np.random.PCG64(seed))
+        B, h = len(counts), size // red
+        points = [(g.random((n, 2)) * size).astype(np.float32) for n in counts]
+        density = np.stack([syn.point_map(p, size, size)[None] for p in points])
+        pred_class = g.standard_normal((B, 5, h, h)).astype(np.float32)
+        pred_density = (g.random((B, 1, h, h)) * 1.5).astype(np.float32)
+        pc = torch.tensor(pred_class, requires_grad=True)
+        pd = torch.tensor(pred_density, requires_grad=True)
+        loss_fn = ref.losses.DACELoss(BINS, red, weight_count_loss=1.0, count_loss="dmcount", input_size=size,
+                                      norm_cood=norm)
+        del calls[:]
+        loss, info = loss_fn(pc, pd, torch.from_numpy(density), [torch.from_numpy(p) for p in points])
+        loss.backward()
+        flat, offs = pack_points(points)
+        beta = np.zeros((B, h * h), np.float32)
+        roll = np.zeros(B, np.int32)
+        k = 0
+        for b, p in enumerate(points):
+            if len(p):
+                (P, lg), rl = calls[k]
+                beta[b] = lg["beta"].numpy()
+                roll[b] = rl
+                k += 1
+        out.update({f"{tag}_size": size, f"{tag}_red": red, f"{tag}_norm": int(norm), f"{tag}_counts": np.asarray(counts),
+                    f"{tag}_points": flat, f"{tag}_offsets": offs, f"{tag}_pred_class": pred_class,
+                    f"{tag}_pred_density": pred_density, f"{tag}_grad_pred_class": pc.grad.numpy(),
+                    f"{tag}_grad_pred_density": pd.grad.numpy(), f"{tag}_beta": beta, f"{tag}_roll": roll})
+        for kk, v in info.items():
+            out[f"{tag}_info_{kk}"] = v.detach().numpy().reshape(())
+    restore()
+    return out
+
+
 def head_case(ref, seed: int = 5):
     """F2: projection + similarity head on a given decoder output."""
     m = build_ref_model(ref, layers=1)
@@ -270,13 +387,61 @@ def prompt_table(ref):
     print("wrote", path, len(table), "prompts")
 
 
+TOKENIZER_TEXTS = [
+    "There are more than one hundred and twenty-five people.", "There is 0 person.", "  Crowd   of\tpeople\n  ",
+    "A photo of 3,141 pedestrians at 5:30pm!", "CAFÉ crowd: naïve façade, Zürich — 東京 😀", "it's they'll we've I'd",
+    "&amp; &lt;tag&gt; html &quot;entities&quot;", "numbers 1234567890 and x1.5e-3", "",
+    "a " * 100,
+]
+
+
+def tokenizer_case(ref):
+    """F6b: the reference tokenizer (simple_tokenizer.py + tokenize, restated above) on assorted texts,
+    including a long one truncated to the context (truncate=True semantics checked separately)."""
+    st = sys.modules["models.clip._clip.simple_tokenizer"]
+    tok = st.SimpleTokenizer()
+    ids = [tok.encode(t) for t in TOKENIZER_TEXTS]
+    flat = np.concatenate([np.asarray(i, np.int64) for i in ids]) if any(ids) else np.zeros(0, np.int64)
+    offs = np.zeros(len(ids) + 1, np.int64)
+    offs[1:] = np.cumsum([len(i) for i in ids])
+    return dict(texts=np.asarray(TOKENIZER_TEXTS), ids=flat, offsets=offs)
+
+
+def bpe_merges():
+    """Data asset for ebc_amd/tokenizer.py: the 48894 BPE merges CLIP uses (lines 1..48894 of the reference's
+    models/clip/_clip/bpe_simple_vocab_16e6.txt.gz, simple_tokenizer.py's `merges[1:49152-256-2+1]`)."""
+    import gzip
+    with gzip.open(f"{REF}/models/clip/_clip/bpe_simple_vocab_16e6.txt.gz", "rt", encoding="utf-8") as f:
+        lines = f.read().split("\n")
+    merges = lines[1:49152 - 256 - 2 + 1]
+    path = os.path.join(REPO, "clip-ebc_amd", "ebc_amd", "data", "clip_bpe_merges.txt.gz")
+    with gzip.open(path, "wt", encoding="utf-8", compresslevel=9) as f:
+        f.write("\n".join(merges) + "\n")
+    print("wrote", path, len(merges), "merges", f"{os.path.getsize(path) / 1024:.0f} KiB")
+
+
 def main():
     torch.set_num_threads(8)
     ref = load_reference()
+    if "--only" in sys.argv:                     # e.g. --only f1b,f1c: regenerate just those fixtures
+        want = sys.argv[sys.argv.index("--only") + 1].split(",")
+        if "f1b" in want:
+            save("f1b_sinkhorn.npz", **sinkhorn_case(ref))
+        if "f1c" in want:
+            save("f1c_loss_extra.npz", **loss_extra_case(ref))
+        if "bpe" in want:
+            bpe_merges()
+        if "f6b" in want:
+            save("f6b_tokens.npz", **tokenizer_case(ref))
+        return
     prompt_table(ref)
+    bpe_merges()
     if "--tokens-only" in sys.argv:
         return
+    save("f1b_sinkhorn.npz", **sinkhorn_case(ref))
+    save("f1c_loss_extra.npz", **loss_extra_case(ref))
     save("f6_text.npz", **text_case(ref))
+    save("f6b_tokens.npz", **tokenizer_case(ref))
     save("f1_loss_224.npz", **loss_case(ref, 224, [0, 1, 3, 10, 47, 200, 1000, 25], seed=101))
     save("f1_loss_448.npz", **loss_case(ref, 448, [5, 0, 150, 2000], seed=202))
     save("f2_head.npz", **head_case(ref))

@@ -107,3 +107,80 @@ def _ddp_contract(rank, world, path):
 
 def test_ddp_gradient_contract_of_dace_loss():
     _run(_ddp_contract, 2, None)
+
+
+# ------------------------------------------------------------------ drop-in train() (train.py:14-69)
+class _TinyCounter(torch.nn.Module):
+    """A stand-in CLIP-EBC-shaped model for the host logic of train(): (pred_class, pred_density)."""
+    bins = [(0, 0), (1, 1)]
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.conv = torch.nn.Conv2d(3, 3, 8, stride=8)
+
+    def forward(self, x):
+        y = self.conv(x)
+        return y[:, :2], y[:, 2:].abs()
+
+
+def _tiny_loss(pred_class, pred_density, target_density, target_points):
+    n = torch.tensor([float(len(p)) for p in target_points])
+    ce = pred_class.square().mean()
+    cnt = (pred_density.sum(dim=(1, 2, 3)) - n).abs().mean()
+    loss = ce + cnt
+    return loss, {"loss": loss.detach(), "ce_loss": ce.detach(), "count_loss": cnt.detach()}
+
+
+def _loader(rank, steps=3, B=2):
+    g = torch.Generator().manual_seed(100 + rank)
+    return [(torch.randn(B, 3, 16, 16, generator=g), [torch.rand(int(k), 2, generator=g) for k in torch.randint(0, 9, (B,), generator=g)],
+             torch.zeros(B, 1, 16, 16)) for _ in range(steps)]
+
+
+def _reference_epoch(model, loader, opt, rank, nprocs):
+    """The reference's loop (train.py:30-69): per step five reduce_means + .item(), np.mean over steps."""
+    from ebc_amd.distributed import reduce_mean
+    per = {}
+    for image, pts, dens in loader:
+        pc, pd = model(image)
+        loss, info = _tiny_loss(pc, pd, dens, pts)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        for k, v in info.items():
+            per.setdefault(k, []).append(float(reduce_mean(v, nprocs)) if nprocs > 1 else float(v))
+        if nprocs > 1:
+            dist.barrier()
+    return {k: float(np.mean(v)) for k, v in per.items()}
+
+
+def _train_world2(rank, world):
+    from ebc_amd.train import train
+    a = torch.nn.parallel.DistributedDataParallel(_TinyCounter())
+    b = torch.nn.parallel.DistributedDataParallel(_TinyCounter())
+    oa = torch.optim.SGD(a.parameters(), lr=0.05)
+    ob = torch.optim.SGD(b.parameters(), lr=0.05)
+    _, _, _, got = train(a, _loader(rank), _tiny_loss, oa, None, torch.device("cpu"), rank, world, progress=False)
+    want = _reference_epoch(b, _loader(rank), ob, rank, world)
+    assert got.keys() == want.keys()
+    for k in want:
+        assert abs(got[k] - want[k]) <= 1e-6 * max(1.0, abs(want[k])), (k, got[k], want[k])
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, atol=1e-7)
+
+
+def test_train_epoch_matches_reference_loop_world2():
+    """One packed all-reduce at the end of the epoch == the reference's per-step reduce_mean + np.mean;
+    the parameters after the epoch are the same as the reference loop's (DDP gradient averaging)."""
+    _run(_train_world2)
+
+
+def test_train_epoch_single_process():
+    from ebc_amd.train import train
+    a, b = _TinyCounter(), _TinyCounter()
+    oa, ob = torch.optim.SGD(a.parameters(), lr=0.05), torch.optim.SGD(b.parameters(), lr=0.05)
+    _, _, _, got = train(a, _loader(0), _tiny_loss, oa, None, torch.device("cpu"), 0, 1, progress=False)
+    want = _reference_epoch(b, _loader(0), ob, 0, 1)
+    for k in want:
+        assert abs(got[k] - want[k]) <= 1e-6 * max(1.0, abs(want[k]))

@@ -1,0 +1,82 @@
+"""World-2 DDP + SyncBatchNorm on the HIP path (trainer.py:143-147): both ranks on cuda:0 over gloo.
+
+DDP averages the ranks' gradients, so the single-process equivalent of one step is the mean of the
+ranks' losses, each over its own crops, with BatchNorm statistics over all crops (SyncBN).  The ranks
+hold UNEQUAL batches (2 and 1 crops): SyncBN must weight the statistics by the per-rank counts, as
+torch.nn.SyncBatchNorm does.  Gradients of every trainable parameter, the BN running statistics and
+the packed loss_info reduce are compared with that single-process step.
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import _ddp_worker as W
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_ddp_syncbn_step_matches_single_process(tmp_path):
+    from multiprocessing import forkserver
+    if getattr(forkserver._forkserver, "_forkserver_pid", None) is None:
+        pytest.skip("run with -m gpu: the ranks need the forkserver conftest.py starts before GPU init")
+    ctx = mp.get_context("forkserver")
+    port = _free_port()
+    procs = [ctx.Process(target=W.rank_main, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=110)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0, 0], codes
+    r0 = torch.load(os.path.join(tmp_path, "rank0.pt"), weights_only=True)
+    r1 = torch.load(os.path.join(tmp_path, "rank1.pt"), weights_only=True)
+
+    # single process: one forward over all crops (BN batch statistics over all of them), the mean of the
+    # ranks' losses
+    from ebc_amd.losses import DACELoss
+    dev = torch.device("cuda:0")
+    m = W.build(dev)
+    img, pts, dens = W.batch()
+    logits, exp = m(torch.from_numpy(img).to(dev))
+    fn = DACELoss(W.BINS, 8, count_loss="dmcount", input_size=224)
+    total, infos, b0 = 0.0, [], 0
+    for n in W.SPLIT:
+        sl = slice(b0, b0 + n)
+        loss, info = fn(logits[sl], exp[sl], torch.from_numpy(dens[sl]).to(dev), [torch.from_numpy(p).to(dev) for p in pts[sl]])
+        total = total + loss / len(W.SPLIT)
+        infos.append(info)
+        b0 += n
+    total.backward()
+    for k, p in m.named_parameters():
+        if not p.requires_grad:
+            continue
+        g = p.grad.detach().cpu().numpy()
+        for r in (r0, r1):
+            err = rel_l2(r[k].numpy(), g)
+            assert err < 2e-4, (k, err)
+    for k, b in m.named_buffers():
+        if "running" in k:
+            for r in (r0, r1):
+                assert rel_l2(r["buf:" + k].numpy(), b.detach().cpu().numpy()) < 1e-5, k
+        if "num_batches" in k:
+            assert int(r0["buf:" + k]) == int(b) == 1
+    for key in ("loss", "ce_loss", "count_loss", "tv_loss"):
+        want = float(sum(float(i[key]) for i in infos) / len(infos))
+        for r in (r0, r1):
+            assert abs(float(r["info:" + key]) - want) <= 1e-4 * abs(want) + 1e-6, key

@@ -33,7 +33,7 @@ def test_sliding_window_full_model_counts():
     from ebc_amd.eval_utils import sliding_window_predict, tile_grid
     from ebc_amd.model import get_model
     txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
-    m = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", vit_layers=2, text_features=txt).cuda().eval()
+    m = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", vit_layers=2, text_features=txt, weights_seed=0).cuda().eval()
     img = torch.randn(1, 3, 500, 700, device="cuda")
     out = sliding_window_predict(m, img, 224, 224)
     rows, cols = tile_grid(500, 700, (224, 224), (224, 224))
@@ -49,3 +49,48 @@ def test_sliding_window_full_model_counts():
         acc[:, y // 8:(y + 224) // 8, x // 8:(x + 224) // 8] += preds[t]
         cnt[:, y // 8:(y + 224) // 8, x // 8:(x + 224) // 8] += 1
     np.testing.assert_allclose(out[0].numpy(), (acc / cnt).numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _assemble(preds, H, W, win=224, r=8):
+    from ebc_amd.eval_utils import tile_grid
+    rows, cols = tile_grid(H, W, (win, win), (win, win))
+    acc = torch.zeros(preds.shape[1], H // r, W // r, dtype=torch.float64)
+    cnt = torch.zeros_like(acc)
+    t = 0
+    for i in range(rows):
+        for j in range(cols):
+            y, x = min(i * win, H - win), min(j * win, W - win)
+            acc[:, y // r:(y + win) // r, x // r:(x + win) // r] += preds[t].double()
+            cnt[:, y // r:(y + win) // r, x // r:(x + win) // r] += 1
+            t += 1
+    return (acc / cnt).float()
+
+
+def test_sliding_window_qnrf_140_tiles():
+    """BASELINE config 5's image: 2048x3072, window = stride = 224 -> 140 tiles in ONE forward (the M = 32060
+    eval-batch GEMM instances), 12 layers.  fp32 (the reference's eval precision): equals the per-tile
+    outputs (16 tiles per forward) assembled on the host; fp16 autocast: within 2e-2 of fp32."""
+    from ebc_amd.eval_utils import sliding_window_predict, tile_grid
+    from ebc_amd.model import get_model
+    txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
+    m = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", text_features=txt,
+                  weights_seed=0).cuda().eval()
+    H, W = 2048, 3072
+    g = np.random.Generator(np.random.PCG64(7))
+    mean = np.array([0.485, 0.456, 0.406], np.float32).reshape(1, 3, 1, 1)
+    std = np.array([0.229, 0.224, 0.225], np.float32).reshape(1, 3, 1, 1)
+    img = torch.from_numpy(((g.random((1, 3, H, W), dtype=np.float32) - mean) / std).astype(np.float32)).cuda()
+    rows, cols = tile_grid(H, W, (224, 224), (224, 224))
+    assert rows * cols == 140
+    out32 = sliding_window_predict(m, img, 224, 224)
+    tiles = [img[:, :, min(i * 224, H - 224):min(i * 224, H - 224) + 224, min(j * 224, W - 224):min(j * 224, W - 224) + 224]
+             for i in range(rows) for j in range(cols)]
+    with torch.no_grad():
+        preds = torch.cat([m(torch.cat(tiles[k:k + 16])).cpu() for k in range(0, 140, 16)])
+    want = _assemble(preds, H, W)
+    assert out32.shape == (1, 1, H // 8, W // 8)
+    np.testing.assert_allclose(out32[0].numpy(), want.numpy(), rtol=2e-4, atol=1e-5)
+    with torch.autocast("cuda", dtype=torch.float16):
+        out16 = sliding_window_predict(m, img, 224, 224)
+    rel = float((out16 - out32).norm() / out32.norm())
+    assert rel < 2e-2, rel

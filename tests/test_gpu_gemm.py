@@ -105,9 +105,12 @@ def _gemm_ws(dt, epi, out_f32, A, B, ws, bias=None, resid=None, aux=None, C=None
 
 @pytest.mark.parametrize("dname", ["f16", "bf16"])
 def test_gemm_wide_tile_gelu(dname):
-    """M=3664, N=3072 picks the 256x256 tile (4-stage ring of 64-B K rows, single fragment set)."""
+    """M=3664, N=3072 picks the 256x192 tile (cfg 3: 8 waves, 2-stage ring of 128-B K rows)."""
+    import ctypes
     dt = DT[dname]
     M, N, K = 3664, 3072, 768
+    tile = (ctypes.c_int * 3)()
+    assert _lib.lib().ebc_gemm_tile_config(_lib.dtype_code(dt), M, N, K, tile) == 3 and tuple(tile) == (256, 192, 1)
     g = torch.Generator(device="cuda").manual_seed(5)
     A = torch.randn(M, K, device="cuda", generator=g).to(dt)
     B = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(dt)

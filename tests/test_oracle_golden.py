@@ -118,3 +118,57 @@ def test_sliding_window_fixture_shapes():
     for i in range(4):
         H, W, win, stride = d[f"cfg_{i}"]
         assert d[f"pred_{i}"].shape == (1, 1, H // 8, W // 8)
+
+
+# ------------------------------------------------------------------ F1b / F1c (general sinkhorn, geometry)
+def plan_close(P, Pref, tol):
+    """Same non-finite pattern (a negative cost makes K = inf: P holds inf / nan there), finite parts close."""
+    P, Pref = np.asarray(P, np.float64), np.asarray(Pref, np.float64)
+    assert np.array_equal(np.isnan(P), np.isnan(Pref)) and np.array_equal(np.isinf(P), np.isinf(Pref))
+    m = np.isfinite(Pref)
+    return rel_l2(P[m], Pref[m]) < tol
+
+
+def _f1b_case(d, i):
+    reg, it, thr, log = (float(x) for x in d[f"cfg_{i}"])
+    return d[f"a_{i}"], d[f"b_{i}"], d[f"C_{i}"], reg, int(it), thr, bool(log)
+
+
+def test_dense_sinkhorn_oracle_matches_reference():
+    """oracle.sinkhorn (C) vs the reference's own sinkhorn on F1b: early stop, rollback at iterations 1
+    and 2 (the returned u, v are the pre-failure pair), log=False, DMCount-shaped crops."""
+    d = golden("f1b_sinkhorn.npz")
+    for i in range(int(d["n_cases"])):
+        a, b, C, reg, it, thr, log = _f1b_case(d, i)
+        r = ref.sinkhorn(a, b, C, reg, it, thr, log=log)
+        assert r["roll"] == int(d[f"roll_{i}"]), (i, r["roll"])
+        assert plan_close(r["P"], d[f"P_{i}"], 1e-5), i
+        if log:
+            for k in ("u", "v", "alpha", "beta"):
+                assert rel_max(r[k], d[f"{k}_{i}"]) < 5e-5, (i, k)
+            np.testing.assert_allclose(r["err"], d[f"err_{i}"], rtol=1e-3, atol=1e-12)
+
+
+@pytest.mark.parametrize("tag", ["r16", "norm"])
+def test_dace_loss_oracle_matches_reference_extra_geometry(tag):
+    """Reduction 16 at 448 (cell pitch 16) and norm_cood=True (F1c)."""
+    d = golden("f1c_loss_extra.npz")
+    size, red, norm = int(d[f"{tag}_size"]), int(d[f"{tag}_red"]), bool(d[f"{tag}_norm"])
+    offs, flat = d[f"{tag}_offsets"], d[f"{tag}_points"]
+    pts = [flat[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    dens = np.stack([syn.point_map(p, size, size)[None] for p in pts])
+    pc = torch.tensor(d[f"{tag}_pred_class"], requires_grad=True)
+    pd = torch.tensor(d[f"{tag}_pred_density"], requires_grad=True)
+    loss, info = ref.dace_loss(pc, pd, torch.from_numpy(dens), pts, BINS, reduction=red, input_size=size,
+                               norm_cood=norm)
+    loss.backward()
+    for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
+        ref_v = float(d[f"{tag}_info_{k}"])
+        assert abs(float(info[k]) - ref_v) <= 1e-5 * abs(ref_v) + 1e-5, (k, float(info[k]), ref_v)
+    assert rel_max(pc.grad.numpy(), d[f"{tag}_grad_pred_class"]) < 1e-5
+    assert rel_l2(pd.grad.numpy(), d[f"{tag}_grad_pred_density"]) < 1e-4
+    for b, p in enumerate(pts):
+        if len(p):
+            r = ref.ot_crop(p, d[f"{tag}_pred_density"][b, 0], size, red, norm_cood=norm)
+            assert rel_max(r["beta"], d[f"{tag}_beta"][b]) < 1e-4, (tag, b)
+            assert not r["rolled_back"] and int(d[f"{tag}_roll"][b]) == 0

@@ -1,0 +1,43 @@
+#!/bin/bash
+# One GPU session on the box (run through gpurun from the repo root):
+#   tools/gpu_check.sh TAG [tests] [smoke] [bench] [prof] [ddp]
+# tests  the -m gpu suite (per-test timeout, stops at the first failure)
+# smoke  __graft_entry__.smoke()
+# bench  the default bench.py line (in-step roofline probe + CPU baseline) -> gpurun_out/TAG_bench.json
+# prof   rocprofv3 --kernel-trace --stats of bench.py, cut to the timed steps (tools/kstats.py --window)
+# ddp    the 2-rank DDP + SyncBN bench path with both ranks on cuda:0 over gloo (a rehearsal, not a scaling number)
+# Every GPU step has its own time limit and the steps are chained: the first failure ends the session.
+set -o pipefail
+TAG=${1:?tag}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+for what in "$@"; do
+  case $what in
+    tests)
+      timeout -k 10 900 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu tests > $O/${TAG}_tests.log 2>&1 \
+        || { tail -60 $O/${TAG}_tests.log; exit 1; }
+      tail -1 $O/${TAG}_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 \
+        || { tail -30 $O/${TAG}_smoke.log; exit 1; }
+      tail -1 $O/${TAG}_smoke.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > $O/${TAG}_bench.log 2>&1 || { tail -30 $O/${TAG}_bench.log; exit 1; }
+      tail -1 $O/${TAG}_bench.log > $O/${TAG}_bench.json; cut -c1-400 $O/${TAG}_bench.json ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o run -- \
+        python3 $R/bench.py --steps 20 --warmup 10 --no-cpu-baseline --no-probe > $O/${TAG}_prof.log 2>&1) \
+        || { tail -30 $O/${TAG}_prof.log; exit 1; }
+      db=$(find $O/${TAG}_prof -name "*.db" | head -1)
+      python3 $R/tools/kstats.py "$db" --window --per 20 --top 45 --csv $O/${TAG}_kstats.csv > $O/${TAG}_kstats.txt \
+        || { echo "kstats failed"; exit 1; }
+      head -25 $O/${TAG}_kstats.txt ;;
+    ddp)
+      EBC_BENCH_ONE_DEVICE=1 EBC_BENCH_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 2 --steps 6 --warmup 3 \
+        --no-probe > $O/${TAG}_ddp2.log 2>&1 || { tail -40 $O/${TAG}_ddp2.log; exit 1; }
+      tail -1 $O/${TAG}_ddp2.log | cut -c1-400 ;;
+    *) echo "unknown step $what"; exit 2 ;;
+  esac
+done
+echo "gpu_check $TAG done"

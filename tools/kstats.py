@@ -1,9 +1,11 @@
 """Summarise a rocprofv3 rocpd database (``--kernel-trace`` output) as per-kernel stats.
 
-usage: python tools/kstats.py <results.db> [--csv out.csv] [--top N] [--per STEPS]
+usage: python tools/kstats.py <results.db> [--csv out.csv] [--top N] [--per STEPS] [--window]
 
 Prints calls / total / average / share per kernel name (templated names shortened), and with
-``--per`` the per-step time of each kernel (total / STEPS).
+``--per`` the per-step time of each kernel (total / STEPS).  ``--window`` keeps only the kernels that run
+between the first two `ebc_marker_kernel` launches (bench.py brackets its timed steps with them), so
+warm-up, the probe pass and the CPU-baseline leg are excluded.
 """
 import argparse
 import csv
@@ -24,10 +26,21 @@ def main():
     ap.add_argument("--csv")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--per", type=float, default=0.0)
+    ap.add_argument("--window", action="store_true")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
+    where = ""
+    if a.window:
+        cols = {r[1] for r in con.execute("pragma table_info(kernels)")}
+        if not {"start", "end"} <= cols:
+            raise SystemExit(f"kernels view has no start/end columns ({sorted(cols)})")
+        marks = con.execute("select start, end from kernels where name like '%ebc_marker_kernel%' order by start").fetchall()
+        if len(marks) < 2:
+            raise SystemExit(f"--window: {len(marks)} ebc_marker_kernel launches in the trace (need 2)")
+        where = f" where start > {marks[0][1]} and end < {marks[1][0]}"
+        print(f"window: {(marks[1][0] - marks[0][1]) / 1e6:.3f} ms between the markers")
     rows = con.execute("select name, count(*), sum(duration), avg(duration), min(duration), max(duration) "
-                       "from kernels group by name order by sum(duration) desc").fetchall()
+                       f"from kernels{where} group by name order by sum(duration) desc").fetchall()
     total = sum(r[2] for r in rows)
     out = []
     for name, n, tot, avg, mn, mx in rows:
