@@ -136,7 +136,7 @@ def ptr(t: Optional[torch.Tensor], device: Optional[torch.device] = None):
     if t is None:
         return None
     assert t.is_cuda and t.is_contiguous(), "ebc_amd kernels take contiguous device tensors"
-    if device is not None and t.device != device:
+    if device is not None and t.device != _as_device(device):
         raise RuntimeError(f"ebc_amd: operand on {t.device}, launch stream on {device}")
     return ctypes.c_void_p(t.data_ptr())
 
@@ -144,9 +144,10 @@ def ptr(t: Optional[torch.Tensor], device: Optional[torch.device] = None):
 def _as_device(where) -> Optional[torch.device]:
     if where is None:
         return None
-    if isinstance(where, torch.Tensor):
-        return where.device
-    return torch.device(where)
+    dev = where.device if isinstance(where, torch.Tensor) else torch.device(where)
+    if dev.type == "cuda" and dev.index is None:                     # "cuda" = the current device
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
 
 
 def stream(where=None) -> ctypes.c_void_p:

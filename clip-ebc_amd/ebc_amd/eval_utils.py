@@ -50,7 +50,8 @@ def sliding_window_predict(model: nn.Module, image: Tensor, window_size: Union[i
     assert window[0] > 0 and window[1] > 0, f"Window size must be a positive integer tuple (h, w), got {window}"
     assert strd[0] > 0 and strd[1] > 0, f"Stride must be a positive integer tuple (h, w), got {strd}"
     assert strd[0] <= window[0] and strd[1] <= window[1], f"Stride must be smaller than window size, got {strd} and {window}"
-    dev = next(model.parameters()).device if any(True for _ in model.parameters()) else torch.device("cuda")
+    params = list(model.parameters())
+    dev = params[0].device if params else (image.device if image.is_cuda else torch.device("cuda"))
     img = image.to(dev, torch.float32).contiguous()[0]
     C, H, W = img.shape
     rows, cols = tile_grid(H, W, window, strd)

@@ -279,7 +279,7 @@ class OTLoss(nn.Module):
         has = torch.tensor([float(len(p) > 0) for p in target_points], device=dev).view(B, 1)
         ot_obj = (normed_pred_density.detach().float().reshape(B, -1) * it.beta * has).sum().reshape(1)
         wd = float(stats[:, 4].sum())
-        return losses[1].reshape(1), wd, ot_obj
+        return losses[0].reshape(1), wd, ot_obj          # OT-only mode: losses[0] = losses[1] = sum of the crops' OT
 
 
 def sinkhorn(a: Tensor, b: Tensor, C: Tensor, reg: float = 1e-1, maxIter: int = 1000, stopThr: float = 1e-9,

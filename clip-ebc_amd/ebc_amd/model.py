@@ -452,12 +452,20 @@ class _DecoderFn(torch.autograd.Function):
             _lib.check(L.ebc_bn_bwd_reduce(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
                                            _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(sums),
                                            _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce")
-            if pg is not None:
-                torch.distributed.all_reduce(sums[: 2 * N], group=pg)     # sum_dy, sum_dy_xmu (torch SyncBN C5)
-                sums[2 * N:].copy_(colsum[2 * N:])                          # the forward's all-reduced count
             dg, db, coef = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty(3, N, **f32)
-            _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
-                                             _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize")
+            if pg is not None:
+                # SyncBatchNorm backward (torch nn/modules/_functions.py, C5): d gamma / d beta come from THIS
+                # rank's sums (DDP then averages them over the ranks); the input gradient uses the all-reduced
+                # sums and the all-reduced count
+                _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), float(P), _lib.ptr(gm.detach()), _lib.ptr(rstd),
+                                                 _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize")
+                torch.distributed.all_reduce(sums[: 2 * N], group=pg)     # sum_dy, sum_dy_xmu
+                sums[2 * N:].copy_(colsum[2 * N:])                          # the forward's all-reduced count
+                _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
+                                                 None, None, _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize(sync)")
+            else:
+                _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
+                                                 _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize")
             dzpad = torch.empty(Q, N, device=dev, dtype=cdtype)
             dzT = torch.empty(N, Qs, device=dev, dtype=cdtype)
             _lib.check(L.ebc_bn_bwd_apply(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),

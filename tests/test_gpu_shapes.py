@@ -158,13 +158,14 @@ def test_decoder_at_bench_batch(dname, B):
     g = torch.Generator(device="cuda").manual_seed(B)
     feat = torch.randn(B, h, h, C, device="cuda", generator=g)
     gy = torch.randn(B, 2 * h, 2 * h, C, device="cuda", generator=g)
-    params = [p.detach().cuda().double().requires_grad_() for p in
+    # reference in f32 on the GPU (MIOpen; no xf32 on gfx950): ~1e-6 relative, far inside the 16-bit bars
+    params = [p.detach().cuda().float().requires_grad_() for p in
               (blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias)]
-    fr = feat.double().requires_grad_()
-    rm = [blk.bn1.running_mean.cuda().double().clone(), blk.bn2.running_mean.cuda().double().clone()]
-    rv = [blk.bn1.running_var.cuda().double().clone(), blk.bn2.running_var.cuda().double().clone()]
+    fr = feat.clone().requires_grad_()
+    rm = [blk.bn1.running_mean.cuda().float().clone(), blk.bn2.running_mean.cuda().float().clone()]
+    rv = [blk.bn1.running_var.cuda().float().clone(), blk.bn2.running_var.cuda().float().clone()]
     yr = _decoder_ref(fr, *params, rm, rv)
-    (yr * gy.double()).sum().backward()
+    (yr * gy).sum().backward()
     blk = blk.cuda().train()
     fd = feat.clone().requires_grad_()
     y = _DecoderFn.apply(fd, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
