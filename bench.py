@@ -1,6 +1,8 @@
 """Benchmark: train crops/s for clip_vit_b_16 + deep VPT(32) + DMCount at 224x224 on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--crops-per-gpu B] [--dtype fp16|bf16|fp32]
+    python bench.py --model clip_resnet50      (BASELINE configs[1]: 448 crops, reduction 8, word prompts,
+                                                DMCount, bf16, 8 crops per GPU; a secondary line)
 
 One step = forward (autocast, like the reference train.py:36-40) + DACE/DMCount loss (on-device
 Sinkhorn) + backward + GradScaler/Adam step over the 11.3 M trainable parameters, on synthetic crops
@@ -39,6 +41,7 @@ import torch.distributed as dist  # noqa: E402
 
 BINS = [(0.0, 0.0), (1.0, 1.0), (2.0, 2.0), (3.0, 3.0), (4.0, float("inf"))]
 ANCHORS_NWPU = [0.0, 1.0, 2.0, 3.0, 4.21931]     # configs/reduction_8.json ["4"]["nwpu"]["average"]
+ANCHORS_SHA = [0.0, 1.0, 2.0, 3.0, 4.29992]      # configs/reduction_8.json ["4"]["sha"]["average"]
 FLOP_PER_CROP = 135.63e9                          # 58.33 fwd + 77.30 bwd GFLOP
 MFMA_PEAK_TF = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.3}   # MI355X dense (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -52,7 +55,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--crops-per-gpu", type=int, default=None,
                     help="default 16 at N = 1 (BASELINE configs[2]), 32 at N > 1 (configs[3]: 128 images x 2 crops / 8)")
-    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
+    ap.add_argument("--model", default="clip_vit_b_16", choices=["clip_vit_b_16", "clip_resnet50"])
+    ap.add_argument("--dtype", default=None, choices=["fp16", "bf16", "fp32"],
+                    help="default fp16 (the reference's AMP) for clip_vit_b_16, bf16 for clip_resnet50 (configs[1])")
     ap.add_argument("--pool", type=int, default=64, help="distinct synthetic batches (cycled beyond that)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crops", type=int, default=16, help="crops per CPU-baseline step (BASELINE.md: 16)")
@@ -66,8 +71,12 @@ def parse(argv=None):
                     help="SURVEY §8f row f2 instead: the reference's training augmentation on device (RandomResizedCrop + "
                          "flip + RandomApply(jitter, blur, noise) + normalise + dot maps), 16 images x 2 crops per step")
     a = ap.parse_args(argv)
+    rn = a.model == "clip_resnet50"
     if a.crops_per_gpu is None:
-        a.crops_per_gpu = 16 if a.gpus == 1 else 32
+        a.crops_per_gpu = 8 if rn else (16 if a.gpus == 1 else 32)
+    if a.dtype is None:
+        a.dtype = "bf16" if rn else "fp16"
+    a.size = 448 if rn else 224
     return a
 
 
@@ -84,10 +93,10 @@ def relaunch(args) -> int:
     return subprocess.call(cmd)
 
 
-def make_batch(B, rank, step, device):
+def make_batch(B, rank, step, device, size=224):
     """BASELINE.md synthetic crops: seed 1000 + rank*100003 + step, lognormal(ln 20, 1.2) points."""
     from ebc_amd import synthetic as syn
-    img, pts, dens = syn.synthetic_crops(B, 224, seed=1000 + rank * 100003 + step)
+    img, pts, dens = syn.synthetic_crops(B, size, seed=1000 + rank * 100003 + step)
     return (torch.from_numpy(img).to(device), [torch.from_numpy(p).to(device) for p in pts],
             torch.from_numpy(dens).to(device), [len(p) for p in pts])
 
@@ -125,25 +134,78 @@ def cpu_baseline(args, crops, steps):
                       f"({affinity} CPUs in the affinity mask); {dt:.1f}s"}
 
 
+def resnet_flop_per_crop(size=448, reduction=8):
+    """Algorithmic FLOP of one clip_resnet50 training crop: every convolution of the ModifiedResNet encoder
+    (counted on the meta device with forward hooks), the Bottleneck(2048) decoder at size/reduction, and the
+    2048 -> 1024 projection; backward = 2 x forward (every layer is trainable)."""
+    from ebc_amd.resnet import ModifiedResNet
+    total = [0.0]
+
+    def hook(m, i, o):
+        total[0] += 2.0 * o.numel() * (m.in_channels // m.groups) * m.kernel_size[0] * m.kernel_size[1]
+
+    with torch.device("meta"):
+        enc = ModifiedResNet(reduction=reduction).eval()
+        hs = [m.register_forward_hook(hook) for m in enc.modules() if isinstance(m, torch.nn.Conv2d)]
+        with torch.no_grad():
+            enc(torch.empty(1, 3, size, size))
+    for h in hs:
+        h.remove()
+    P, C, E = (size // reduction) ** 2, 2048, 1024
+    fwd = total[0] + 2.0 * P * C * C * (1 + 9 + 1) + 2.0 * P * C * E
+    return 3.0 * fwd
+
+
+def cpu_baseline_resnet(args, crops, steps):
+    """clip_resnet50 step on the host cores: the oracle's functional restatement (oracle/ref.py resnet_forward,
+    pinned by F7) + DACE/DMCount + backward + Adam over every trainable tensor, fp32."""
+    from oracle import ref
+    from ebc_amd import synthetic as syn
+    nthreads = torch.get_num_threads()
+    p = ref.resnet_params_from_state(syn.resnet50_full_state(0, include_text=False))
+    opt = torch.optim.Adam([v for v in p.values() if v.requires_grad], lr=1e-4, weight_decay=1e-4)
+    txt = torch.randn(5, 1024, generator=torch.Generator().manual_seed(0))
+
+    def step(s):
+        img, pts, dens = syn.synthetic_crops(crops, 448, seed=5000 + s)
+        logits, exp, _ = ref.resnet_forward(p, torch.from_numpy(img), txt, ANCHORS_SHA)
+        loss, _ = ref.dace_loss(logits, exp, torch.from_numpy(dens), pts, BINS, input_size=448)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step(0)                                                  # warm-up
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step(1 + s)
+    dt = time.perf_counter() - t0
+    return {"value": round(crops * steps / dt, 4), "unit": "crops/s", "cores": nthreads, "kind": "port",
+            "sample": f"{steps} timed step(s) (after 1 warm-up) x {crops} crops of 448 through oracle/ref.py resnet_forward "
+                      f"(fwd + DACE/DMCount + bwd + Adam, fp32) on {nthreads} torch threads; {dt:.1f}s"}
+
+
 def setup(args, rank, world, local, device):
     """Model, loss, optimizer and the per-step closure (shared with tools/torch_prof.py)."""
     torch.manual_seed(42 + rank)
     from ebc_amd.model import get_model
     from ebc_amd.losses import DACELoss
-    model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
-                      vpt_drop=0.0, deep_vpt=True, weights_seed=0).to(device)
+    if args.model == "clip_resnet50":
+        model = get_model("clip_resnet50", 448, 8, BINS, ANCHORS_SHA, prompt_type="word", weights_seed=0).to(device)
+    else:
+        model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
+                          vpt_drop=0.0, deep_vpt=True, weights_seed=0).to(device)
     model.train()
     if world > 1:
         from ebc_amd.distributed import wrap_ddp       # SyncBatchNorm + DDP, as trainer.py:147
         model = wrap_ddp(model, device.index)
-    loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=224).to(device)
+    loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=args.size).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
     opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
     amp_dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.dtype]
     scaler = torch.amp.GradScaler("cuda", enabled=args.dtype == "fp16")
     B = args.crops_per_gpu
     npool = min(args.pool, args.warmup + args.steps)
-    pool = [make_batch(B, rank, s, device) for s in range(npool)]
+    pool = [make_batch(B, rank, s, device, args.size) for s in range(npool)]
     info_buf = torch.zeros(5, device=device)
 
     def step(i):
@@ -169,7 +231,7 @@ def _attn_flops(B, L, H, d=64):
     return 4.0 * B * H * L * L * d
 
 
-def probe_steps(step, first, n, device, counts_of):
+def probe_steps(step, first, n, device, counts_of, cells=784):
     """Run n extra steps with every instrumented launch bracketed by HIP events (ebc_probe_*); returns the
     per-step kernel classes sorted by time, and the Sinkhorn roofline entry."""
     from ebc_amd import _lib
@@ -215,15 +277,17 @@ def probe_steps(step, first, n, device, counts_of):
     out.sort(key=lambda r: -r["per_step_us"])
     sink = None
     if dace:
-        # 4 n 784 (2 I + I/10) + 3*4*784 + 8 n bytes per crop, I = 100 iterations executed
+        # 4 n M (2 I + I/10) + 3*4*M + 8 n bytes per crop, M = 784 cells (28x28; 3136 at 448),
+        # I = 100 iterations executed
         byts = []
         for i in range(n):
             cnt = counts_of(first + i)
-            byts.append(sum(4 * c * 784 * (2 * 100 + 10) + 3 * 4 * 784 + 8 * c for c in cnt if c > 0))
+            byts.append(sum(4 * c * cells * (2 * 100 + 10) + 3 * 4 * cells + 8 * c for c in cnt if c > 0))
         avg_b, avg_s = sum(byts) / len(byts), sum(dace) / len(dace) * 1e-3
         sink = {"bound": "hbm", "achieved": round(avg_b / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(avg_b / avg_s / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": int(avg_b),
-                "avg_us": round(avg_s * 1e6, 1), "kernel": "dace_loss_kernel<28> (fused DACE + DMCount + Sinkhorn, 100 its)",
+                "avg_us": round(avg_s * 1e6, 1),
+                "kernel": f"dace_loss_kernel<{int(cells ** 0.5)}> (fused DACE + DMCount + Sinkhorn, 100 its)",
                 "note": "reference-algorithm bytes (materialised K); the kernel keeps K factored in LDS, so this "
                         "is an equivalent rate, not HBM traffic"}
     return out, sink
@@ -408,20 +472,32 @@ def main():
     kernels, sink = None, None
     if not args.no_probe:
         first = args.warmup + args.steps
-        kernels, sink = probe_steps(step, first, 3, device, lambda i: step.pool[i % len(step.pool)][3])
+        kernels, sink = probe_steps(step, first, 3, device, lambda i: step.pool[i % len(step.pool)][3],
+                                    cells=(args.size // 8) ** 2)
     if rank == 0:
         peak = MFMA_PEAK_TF[args.dtype]
-        cfgname = "configs[2]" if (world == 1 and B == 16) else ("configs[3] per-rank shape" if B == 32 else "custom")
+        rn = args.model == "clip_resnet50"
+        flop_per_crop = resnet_flop_per_crop() if rn else FLOP_PER_CROP
+        if rn:
+            metric = "train crops/sec clip_resnet50 448px reduction 8 word-prompt DMCount bf16 (configs[1])"
+            workload = (f"clip_resnet50 448x448 reduction 8 truncation 4 word prompts + DACE/DMCount train step, {B} crops/GPU, "
+                        f"{args.dtype}, SHA anchors (BASELINE configs[1]); encoder on MIOpen, decoder + head + loss on HIP")
+            seq = None
+        else:
+            metric = METRIC
+            cfgname = "configs[2]" if (world == 1 and B == 16) else ("configs[3] per-rank shape" if B == 32 else "custom")
+            workload = (f"clip_vit_b_16 224x224 deep-VPT(32) + DACE/DMCount train step, {B} crops/GPU, "
+                        f"AMP {args.dtype}, NWPU anchors (BASELINE {cfgname})")
+            seq = 229
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric, "value": round(value, 3), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "median_ms_per_step": round(statistics.median(step_ms), 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (BASELINE.md crops, a distinct batch per step, pre-staged in HBM; synthetic random-init weights)",
-            "config": {"workload": f"clip_vit_b_16 224x224 deep-VPT(32) + DACE/DMCount train step, {B} crops/GPU, "
-                                   f"AMP {args.dtype}, NWPU anchors (BASELINE {cfgname})",
-                       "global_batch": B * world, "seq_len": 229, "parallelism": f"dp{world}"},
-            "step_roofline": {"flop_per_crop": FLOP_PER_CROP, "achieved_tflops": round(value / world * FLOP_PER_CROP / 1e12, 2),
-                              "frac": round(value / world * FLOP_PER_CROP / 1e12 / peak, 4)},
+            "config": {"workload": workload, "global_batch": B * world, "seq_len": seq, "parallelism": f"dp{world}"},
+            "step_roofline": {"flop_per_crop": flop_per_crop,
+                              "achieved_tflops": round(value / world * flop_per_crop / 1e12, 2),
+                              "frac": round(value / world * flop_per_crop / 1e12 / peak, 4)},
         }
         if world > 1:
             out["per_rank_crops_s"] = [round(B * args.steps / t, 2) for t in per_rank]
@@ -435,7 +511,10 @@ def main():
             out["kernels"] = kernels[:12]
             out["sinkhorn"] = sink
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args, args.cpu_crops, args.cpu_steps)
+            if rn:
+                out["cpu_baseline"] = cpu_baseline_resnet(args, 2, 1)
+            else:
+                out["cpu_baseline"] = cpu_baseline(args, args.cpu_crops, args.cpu_steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -16,6 +16,11 @@
 //   dzT    [N][Qs] T                   transposed padded dz (0 outside the interior)
 //   dw     [N][C][3][3] f32            weight gradient, nn.Conv2d layout
 // Every kernel is HBM-bound elementwise / transpose work (4-wide vector accesses).
+//
+// The ResNet-50 decoder Bottleneck (models/utils.py:306-363, expansion 1: conv1x1-bn-relu-conv3x3-bn-relu-
+// conv1x1-bn-add-relu) reuses the 3x3 machinery for its middle conv; its two 1x1 convs are plain MFMA GEMMs
+// on the unpadded [B*H*W][C] rows, with the flat-layout helpers below (upsample, BN statistics, BN+ReLU,
+// BN input gradient with the identity branch's masked gradient).
 #include <algorithm>
 
 #include "ebc_common.h"
@@ -235,6 +240,81 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __re
     shift[c] = beta[c] - (float)m * sc;
 }
 
+// x[p][c] = bilinear x`up` upsample of feat, unpadded rows (the Bottleneck's conv1x1 input)
+template <class T>
+__global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__ feat, T* __restrict__ x, long P, int H,
+                                                       int W, int C, int h, int w, float scale)
+{
+    const int C4 = C / 4;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= P * C4) return;
+    const long p = e / C4;
+    const int c = (int)(e - p * C4) * 4;
+    const int hw = H * W, b = (int)(p / hw), r = (int)(p - (long)b * hw), yy = r / W, xx = r - yy * W;
+    st4(x + p * C + c, bilinear4(feat, b, yy, xx, h, w, C, c, scale));
+}
+
+// out = relu(z*scale + shift), unpadded rows, 8 channels per thread
+template <class T>
+__global__ __launch_bounds__(256) void bn_relu_kernel(const T* __restrict__ z, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, T* __restrict__ out, long P, int C)
+{
+    const int C8 = C / 8;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= P * C8) return;
+    const long p = e / C8;
+    const int c = (int)(e - p * C8) * 8;
+    float v[8];
+    ld8(z + p * C + c, v);
+    const float4 s0 = ld4(scale + c), s1 = ld4(scale + c + 4), h0 = ld4(shift + c), h1 = ld4(shift + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = fmaxf(fmaf(v[i], sc[i], sh[i]), 0.f);
+    st8(out + p * C + c, v);
+}
+
+// column partials of sum(z) and sum(z*z) (BatchNorm batch statistics of a 1x1 conv output); the
+// bn_bwd_partial_kernel scheme: (C/8) x RL threads, UNR rows per load batch, row order kept
+template <class T, int UNR>
+__global__ __launch_bounds__(512) void bn_stats_partial_kernel(const T* __restrict__ z, float* __restrict__ part, long P,
+                                                               int C, int rows_per_block)
+{
+    extern __shared__ float red[];                // [RL][2][C]
+    const int C8 = C / 8, RL = blockDim.x / C8;
+    const int rl = threadIdx.x / C8, c = (threadIdx.x - rl * C8) * 8;
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = std::min<long>(P, r0 + rows_per_block);
+    float s1[8], s2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+    for (long r = r0 + rl; r < r1; r += UNR * RL) {
+        float zv[UNR][8];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) ld8(z + std::min<long>(r + k * RL, r1 - 1) * C + c, zv[k]);
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            if (r + k * RL >= r1) continue;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                s1[i] += zv[k][i];
+                s2[i] = fmaf(zv[k][i], zv[k][i], s2[i]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        red[(size_t)rl * 2 * C + c + i] = s1[i];
+        red[(size_t)rl * 2 * C + C + c + i] = s2[i];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < RL; ++k) s += red[(size_t)k * 2 * C + e];
+        part[(size_t)blockIdx.x * 2 * C + e] = s;
+    }
+}
+
 // ------------------------------------------------------------------ backward
 // g = gy * relu'(.)  with the ReLU mask from the stored output (mask_y) or recomputed from z (HAS_MY false)
 
@@ -311,6 +391,42 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
     coef[c] = gamma[c] * rstd[c];
     coef[C + c] = (float)(sg / count);
     coef[2 * C + c] = (float)(sgx / count);
+}
+
+// dz = gamma*rstd * (g - mean(g) - xhat * mean(g*xhat)), g = gy * relu'(.), unpadded rows (a 1x1 conv's
+// output gradient); gmask != NULL also gets g itself in f32 (the identity branch's gradient of the block)
+template <class T, bool HAS_MY>
+__global__ __launch_bounds__(256) void bn_bwd_apply_flat_kernel(const T* __restrict__ gy, const T* __restrict__ my,
+                                                                const T* __restrict__ z, const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift,
+                                                                const float* __restrict__ coef, T* __restrict__ dz,
+                                                                float* __restrict__ gmask, long P, int C)
+{
+    const int C8 = C / 8;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= P * C8) return;
+    const long p = e / C8;
+    const int c = (int)(e - p * C8) * 8;
+    const size_t off = (size_t)p * C + c;
+    float gv[8], zv[8], mv[8];
+    ld8(gy + off, gv);
+    ld8(z + off, zv);
+    if (HAS_MY) ld8(my + off, mv);
+    float v[8], gm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int cc = c + i;
+        const float m = HAS_MY ? mv[i] : fmaf(zv[i], scale[cc], shift[cc]);
+        gm[i] = m > 0.f ? gv[i] : 0.f;
+        v[i] = coef[cc] * (gm[i] - coef[C + cc] - (zv[i] - mean[cc]) * rstd[cc] * coef[2 * C + cc]);
+    }
+    st8(dz + off, v);
+    if (gmask) {
+        *reinterpret_cast<float4*>(gmask + off) = make_float4(gm[0], gm[1], gm[2], gm[3]);
+        *reinterpret_cast<float4*>(gmask + off + 4) = make_float4(gm[4], gm[5], gm[6], gm[7]);
+    }
 }
 
 // Tiles of 64 padded positions x 64 channels, staged through LDS so that both the NHWC-padded image
@@ -521,6 +637,25 @@ int bn_bwd_reduce_t(const void* gy, const void* my, const void* z, const float* 
     return EBC_OK;
 }
 
+template <class T>
+int bn_stats_t(const void* z, double* colsum, void* ws, size_t wsb, long P, int C, hipStream_t st)
+{
+    if (C % 8 || C / 8 > 512) return EBC_E_UNSUPPORTED;
+    const int C8 = C / 8;
+    const int RL = std::max(1, 512 / C8);
+    const int rpb = bn_partial_rows(C);
+    const long nb = (P + rpb - 1) / rpb;
+    const size_t need = CONV_WS_STATS_OFFSET + (size_t)nb * 2 * C * 4;
+    if (!ws || wsb < need) return EBC_E_ARG;
+    float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + CONV_WS_STATS_OFFSET);
+    hipLaunchKernelGGL((bn_stats_partial_kernel<T, 4>), dim3((unsigned)nb), dim3(C8 * RL), (size_t)RL * 2 * C * 4, st,
+                       (const T*)z, part, P, C, rpb);
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
+                       2 * C, colsum);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- C-ABI
@@ -718,6 +853,63 @@ extern "C" int ebc_dec_prep_weights(int dtype, const float* w, void* wk, void* w
     const dim3 grid((unsigned)(N / 32), (unsigned)(C / 32));
     EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(prep_weights_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, w,
                                                (T*)wk, (T*)wf, N, C));
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+// ------------------------------------------------------------------ flat-layout helpers (Bottleneck decoder)
+extern "C" int ebc_dec_upsample(int dtype, const float* feat, void* x, int B, int h, int w, int C, int up,
+                                ebc_stream_t stream)
+{
+    if (!feat || !x || up < 1 || B <= 0 || h <= 0 || w <= 0 || C % 4) return EBC_E_ARG;
+    const int H = h * up, W = w * up;
+    const long P = (long)B * H * W;
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(upsample_kernel<T>, dim3(nblk(P * (C / 4))), dim3(256), 0,
+                                               (hipStream_t)stream, feat, (T*)x, P, H, W, C, h, w, 1.0f / (float)up));
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+extern "C" int ebc_bn_stats(int dtype, const void* z, double* colsum, void* ws, size_t wsb, long P, int C,
+                            ebc_stream_t stream)
+{
+    if (!z || !colsum || P <= 0 || C % 8) return EBC_E_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    switch (dtype) {
+        case EBC_F32: return bn_stats_t<float>(z, colsum, ws, wsb, P, C, st);
+        case EBC_F16: return bn_stats_t<_Float16>(z, colsum, ws, wsb, P, C, st);
+        case EBC_BF16: return bn_stats_t<__bf16>(z, colsum, ws, wsb, P, C, st);
+    }
+    return EBC_E_ARG;
+}
+
+extern "C" int ebc_bn_relu(int dtype, const void* z, const float* scale, const float* shift, void* out, long P, int C,
+                           ebc_stream_t stream)
+{
+    if (!z || !scale || !shift || !out || P <= 0 || C % 8) return EBC_E_ARG;
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(bn_relu_kernel<T>, dim3(nblk(P * (C / 8))), dim3(256), 0,
+                                               (hipStream_t)stream, (const T*)z, scale, shift, (T*)out, P, C));
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+extern "C" int ebc_bn_bwd_apply_flat(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
+                                     const float* rstd, const float* scale, const float* shift, const float* coef,
+                                     void* dz, float* gmask, long P, int C, ebc_stream_t stream)
+{
+    if (!gy || !z || !mean || !rstd || !coef || !dz || P <= 0 || C % 8 || (!mask_y && (!scale || !shift)))
+        return EBC_E_ARG;
+    const unsigned grid = nblk(P * (C / 8));
+    const hipStream_t st = (hipStream_t)stream;
+    if (mask_y) {
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_flat_kernel<T, true>), dim3(grid), dim3(256), 0, st,
+                                                   (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale, shift,
+                                                   coef, (T*)dz, gmask, P, C));
+    } else {
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_flat_kernel<T, false>), dim3(grid), dim3(256), 0, st,
+                                                   (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale, shift,
+                                                   coef, (T*)dz, gmask, P, C));
+    }
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

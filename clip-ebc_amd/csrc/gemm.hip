@@ -731,6 +731,9 @@ int pick_cfg(int M, int N, int K, bool wide) {
     // tools/gpu72.sh): the 256-wide tiles win once they fill >= 1.5 waves of CUs -- qkv 161.6 -> 149.0 us,
     // out-proj 88.1 -> 66.4, c_fc 236.0 -> 205.7 (256x256), c_proj 250.8 -> 173.4
     if (N % 256 == 0 && N >= 3072 && K <= 1024 && ntiles(M, N, 256, 256) >= 384) return 7;
+    // the ResNet-50 decoder's 2048-wide 1x1 convs and the 2048 -> 1024 projection (M = B*56*56 rows): no
+    // 192- or 96-wide tile divides N; 256x256 keeps the L2 -> LDS fill below the MFMA rate
+    if (N % 256 == 0 && N % 192 != 0 && N >= 1024 && ntiles(M, N, 256, 256) >= 384) return 7;
     if (N % 192 == 0 && ntiles(M, N, 256, 192) >= 384) return 3;
     if (N % 192 == 0 && N % 256 != 0 && K <= 1024 && ntiles(M, N, 192, 192) >= 128) return 4;
     // r01 sweep: MLP c_fc / GELU' (N = 3072, K = 768): 256x192 27.6 / 31.9 us vs 34.3 / 37.0 (128x64);
@@ -859,6 +862,7 @@ int launch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st)
     if (cfg == 2) return launch_gemm<E, TO, EPI, 128, 64, 2, 2, 2, 128, MODE>(g, st);
     if constexpr (E::BYTES == 2) {
         if (cfg == 3) return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2, 128, MODE>(g, st);
+        if (cfg == 7) return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2, 128, MODE>(g, st);
         if (cfg == 13) return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, MODE>(g, st);
         if (cfg == 20) return launch_gemm<E, TO, EPI, 256, 256, 4, 4, 2, 64, MODE>(g, st);
         if (cfg == 21) return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64, MODE>(g, st);
@@ -872,8 +876,10 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
     if (!sixteen) return 2;
     if (const int f = forced_conv_cfg()) {
         const TileCfg* c = find_cfg(f);
-        if (c && N % c->bn == 0 && (f == 2 || f == 3 || f == 13 || f == 20 || f == 21)) return f;
+        if (c && N % c->bn == 0 && (f == 2 || f == 3 || f == 7 || f == 13 || f == 20 || f == 21)) return f;
     }
+    // ResNet-50 decoder 3x3 conv (C = N = 2048, M = B*56*56): 256x256 tiles, several waves of them
+    if (mode == 1 && N % 256 == 0 && N % 192 != 0 && ntiles(M, N, 256, 256) >= 256) return 7;
     // r01: 160x256 tiles (237 instead of 196 tiles at M = 16*784, N = 768) measured only 2-3 % faster on the
     // forward convs (their 80x64 wave tiles lose per-CU throughput), not kept
     if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;

@@ -310,16 +310,16 @@ extern "C" int ebc_attention_bwd(int dtype, const void* qkv, const void* dout, c
     return ebc::attention_bwd(dtype, qkv, dout, out, lse, delta_ws, dqkv, B, L, H, (hipStream_t)stream);
 }
 extern "C" int ebc_head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
-                            float* logits, float* expo, int P, int HW, int NB, ebc_stream_t stream)
+                            float* logits, float* expo, int P, int HW, int NB, int embed, ebc_stream_t stream)
 {
-    return ebc::head_fwd(dtype_z, Z, text, logit_scale, anchors, logits, expo, P, HW, NB, (hipStream_t)stream);
+    return ebc::head_fwd(dtype_z, Z, text, logit_scale, anchors, logits, expo, P, HW, NB, embed, (hipStream_t)stream);
 }
 extern "C" int ebc_head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
                             const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
-                            float* dbias, float* dscale, int P, int HW, int NB, ebc_stream_t stream)
+                            float* dbias, float* dscale, int P, int HW, int NB, int embed, ebc_stream_t stream)
 {
     return ebc::head_bwd(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW,
-                         NB, (hipStream_t)stream);
+                         NB, embed, (hipStream_t)stream);
 }
 extern "C" int ebc_cast_f32(int dtype, const float* in, void* out, size_t n, ebc_stream_t stream)
 {

@@ -305,18 +305,22 @@ __global__ __launch_bounds__(256) void vpt_grad_kernel(float* __restrict__ dX, T
 }
 
 // ----------------------------------------------------------------------------- similarity head
-// One wave per pixel, CH = 512 channels (8 per lane), NB <= 16 bins.  Text features normalised in LDS.
-constexpr int CH = 512;
+// One wave per pixel, CH channels (CH / 64 per lane, in float4 pieces 256 apart), NB <= 16 bins; the text
+// features are normalised in LDS.  CH = 512 (ViT-B/16) or 1024 (ResNet-50, models/clip/model.py:85-95).
 constexpr int PIX_PER_BLOCK = 16;
 
-template <class TZ>
-__device__ __forceinline__ void load_pix(const TZ* z, float (&v)[8]) {
+template <class TZ, int CH>
+__device__ __forceinline__ void load_pix(const TZ* z, float (&v)[CH / 64]) {
     const int lane = threadIdx.x & 63;
-    const float4 a = ld4<TZ>(z + 4 * lane), b = ld4<TZ>(z + 256 + 4 * lane);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+    for (int q = 0; q < CH / 256; ++q) {
+        const float4 a = ld4<TZ>(z + 256 * q + 4 * lane);
+        v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+    }
 }
 
-__device__ void load_text(const float* text, int NB, float* tn, float* scratch) {
+template <int CH>
+__device__ void load_text(const float* text, int NB, float* tn) {
     // tn[k][c] = text[k][c] / max(||text[k]||, 1e-12)   (F.normalize, model.py:204)
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     for (int k = w; k < NB; k += blockDim.x / 64) {
@@ -329,18 +333,32 @@ __device__ void load_text(const float* text, int NB, float* tn, float* scratch) 
     __syncthreads();
 }
 
-template <class TZ>
+// <scaled pixel, normalised text row> partial of this lane (its CH / 64 channels)
+template <int CH>
+__device__ __forceinline__ float text_dot(const float* t, const float* zs) {
+    const int lane = threadIdx.x & 63;
+    float d = 0.f;
+#pragma unroll
+    for (int q = 0; q < CH / 256; ++q) {
+        const float4 a = *reinterpret_cast<const float4*>(t + 256 * q + 4 * lane);
+        d += zs[4 * q] * a.x + zs[4 * q + 1] * a.y + zs[4 * q + 2] * a.z + zs[4 * q + 3] * a.w;
+    }
+    return d;
+}
+
+template <class TZ, int CH>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z, const float* text, const float* logit_scale,
                                                        const float* anchors, float* logits, float* expo, int P, int HW, int NB)
 {
+    constexpr int NV = CH / 64;
     extern __shared__ __attribute__((aligned(16))) float tn[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front,
-    float vv[PPW][8];                                 // before the text normalisation (latencies overlap)
+    float vv[PPW][NV];                                // before the text normalisation (latencies overlap)
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) load_pix<TZ>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+    for (int j = 0; j < PPW; ++j) load_pix<TZ, CH>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
     const float s = expf(*logit_scale);
-    load_text(text, NB, tn, nullptr);
+    load_text<CH>(text, NB, tn);
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
         const int p = blockIdx.x * PIX_PER_BLOCK + w + 4 * j;
@@ -348,16 +366,15 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z,
         float* v = vv[j];
         float ss = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+        for (int j = 0; j < NV; ++j) ss += v[j] * v[j];
         const float inv = 1.0f / fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
+        float zs[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) zs[j] = s * (v[j] * inv);
         float lg[16];
         float mx = -INFINITY;
         for (int k = 0; k < NB; ++k) {
-            const float* t = tn + k * CH;
-            const float4 a = *reinterpret_cast<const float4*>(t + 4 * lane), b = *reinterpret_cast<const float4*>(t + 256 + 4 * lane);
-            float d = (s * (v[0] * inv)) * a.x + (s * (v[1] * inv)) * a.y + (s * (v[2] * inv)) * a.z + (s * (v[3] * inv)) * a.w;
-            d += (s * (v[4] * inv)) * b.x + (s * (v[5] * inv)) * b.y + (s * (v[6] * inv)) * b.z + (s * (v[7] * inv)) * b.w;
-            lg[k] = wave_sum(d);
+            lg[k] = wave_sum(text_dot<CH>(tn + k * CH, zs));
             mx = fmaxf(mx, lg[k]);
         }
         float se = 0.f;
@@ -374,24 +391,27 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z,
 
 // dZ = d/dZ of (logits, exp) given upstream dlogits [B,NB,HW], dexp [B,1,HW] (x *gscale if given);
 // also d bias (column sums of dZ) and d logit_scale, accumulated with atomics (zeroed by the launcher).
-template <class TZ, class TD>
+template <class TZ, class TD, int CH>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z, const float* text, const float* logit_scale,
                                                        const float* anchors, const float* dlogits, const float* dexp,
                                                        const float* gscale, TD* dZ, float* dbias, float* dscale,
                                                        int P, int HW, int NB)
 {
+    constexpr int NV = CH / 64;
     extern __shared__ __attribute__((aligned(16))) float tn[];
     float* dbias_l = tn + NB * CH;       // [4 waves][CH]
     float* dsc_l = dbias_l + 4 * CH;     // [4]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front,
-    float vv[PPW][8];                                 // before the text normalisation (latencies overlap)
+    float vv[PPW][NV];                                // before the text normalisation (latencies overlap)
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) load_pix<TZ>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+    for (int j = 0; j < PPW; ++j) load_pix<TZ, CH>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
     const float ls = *logit_scale, s = expf(ls);
     const float gs = gscale ? *gscale : 1.0f;
-    load_text(text, NB, tn, nullptr);
-    float db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    load_text<CH>(text, NB, tn);
+    float db[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) db[j] = 0.f;
     float dsc = 0.f;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
@@ -400,20 +420,16 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
         float* v = vv[j];
         float ss = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+        for (int j = 0; j < NV; ++j) ss += v[j] * v[j];
         const float nrm = sqrtf(wave_sum(ss));
         const float den = fmaxf(nrm, 1e-12f), inv = 1.0f / den;
-        float zn[8];
+        float zn[NV], zs[NV];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) zn[j] = v[j] * inv;
+        for (int j = 0; j < NV; ++j) { zn[j] = v[j] * inv; zs[j] = s * zn[j]; }
         float lg[16], pr[16];
         float mx = -INFINITY;
         for (int k = 0; k < NB; ++k) {
-            const float* t = tn + k * CH;
-            const float4 a = *reinterpret_cast<const float4*>(t + 4 * lane), b = *reinterpret_cast<const float4*>(t + 256 + 4 * lane);
-            float d = (s * zn[0]) * a.x + (s * zn[1]) * a.y + (s * zn[2]) * a.z + (s * zn[3]) * a.w;
-            d += (s * zn[4]) * b.x + (s * zn[5]) * b.y + (s * zn[6]) * b.z + (s * zn[7]) * b.w;
-            lg[k] = wave_sum(d);
+            lg[k] = wave_sum(text_dot<CH>(tn + k * CH, zs));
             mx = fmaxf(mx, lg[k]);
         }
         float se = 0.f;
@@ -422,30 +438,38 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
         for (int k = 0; k < NB; ++k) { pr[k] /= se; e += pr[k] * anchors[k]; }
         const int b = p / HW, hw = p % HW;
         const float de = dexp[(size_t)b * HW + hw] * gs;
-        float dzn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        float dzn[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) dzn[j] = 0.f;
         for (int k = 0; k < NB; ++k) {
             // d logit_k = dlogits_k + dexp * p_k (anchor_k - e)   (softmax + expectation backward)
             const float dl = dlogits[((size_t)b * NB + k) * HW + hw] * gs + de * pr[k] * (anchors[k] - e);
             dsc += dl * lg[k];                             // logits = exp(ls) * cos  ->  d ls = dl * logits
             const float* t = tn + k * CH;
-            const float4 a = *reinterpret_cast<const float4*>(t + 4 * lane), bq = *reinterpret_cast<const float4*>(t + 256 + 4 * lane);
             const float c = dl * s;
-            dzn[0] += c * a.x; dzn[1] += c * a.y; dzn[2] += c * a.z; dzn[3] += c * a.w;
-            dzn[4] += c * bq.x; dzn[5] += c * bq.y; dzn[6] += c * bq.z; dzn[7] += c * bq.w;
+#pragma unroll
+            for (int q = 0; q < NV / 4; ++q) {
+                const float4 a = *reinterpret_cast<const float4*>(t + 256 * q + 4 * lane);
+                dzn[4 * q] += c * a.x; dzn[4 * q + 1] += c * a.y; dzn[4 * q + 2] += c * a.z; dzn[4 * q + 3] += c * a.w;
+            }
         }
         // F.normalize backward: dz = (dzn - zn * <zn, dzn>) / ||z||   (or dzn / eps when clamped)
         float dot = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dot += zn[j] * dzn[j];
+        for (int j = 0; j < NV; ++j) dot += zn[j] * dzn[j];
         dot = (nrm > 1e-12f) ? wave_sum(dot) : 0.f;
-        float dz[8];
+        float dz[NV];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { dz[j] = (dzn[j] - zn[j] * dot) * inv; db[j] += dz[j]; }
-        st4<TD>(dZ + (size_t)p * CH + 4 * lane, make_float4(dz[0], dz[1], dz[2], dz[3]));
-        st4<TD>(dZ + (size_t)p * CH + 256 + 4 * lane, make_float4(dz[4], dz[5], dz[6], dz[7]));
+        for (int j = 0; j < NV; ++j) { dz[j] = (dzn[j] - zn[j] * dot) * inv; db[j] += dz[j]; }
+#pragma unroll
+        for (int q = 0; q < NV / 4; ++q)
+            st4<TD>(dZ + (size_t)p * CH + 256 * q + 4 * lane, make_float4(dz[4 * q], dz[4 * q + 1], dz[4 * q + 2], dz[4 * q + 3]));
     }
     // lane 0's dsc is the wave's per-pixel sum (wave_sum results are lane-uniform)
-    for (int j = 0; j < 4; ++j) { dbias_l[w * CH + 4 * lane + j] = db[j]; dbias_l[w * CH + 256 + 4 * lane + j] = db[4 + j]; }
+#pragma unroll
+    for (int q = 0; q < NV / 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dbias_l[w * CH + 256 * q + 4 * lane + j] = db[4 * q + j];
     if (lane == 0) dsc_l[w] = dsc;
     __syncthreads();
     for (int c = threadIdx.x; c < CH; c += blockDim.x) {
@@ -629,32 +653,41 @@ int vpt_grad(int dtype, float* dX, void* dXt, float* dvpt, int B, int L, int NVP
     return EBC_OK;
 }
 
-int head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
-             float* logits, float* expo, int P, int HW, int NB, hipStream_t st)
+template <int CH>
+static int head_fwd_t(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+                      float* logits, float* expo, int P, int HW, int NB, hipStream_t st)
 {
-    if (NB <= 0 || NB > 16) return EBC_E_UNSUPPORTED;
     const dim3 grid((P + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
     const size_t lds = (size_t)NB * CH * 4;
     switch (dtype_z) {
-        case EBC_F32: hipLaunchKernelGGL(head_fwd_kernel<float>, grid, dim3(256), lds, st, (const float*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
-        case EBC_F16: hipLaunchKernelGGL(head_fwd_kernel<_Float16>, grid, dim3(256), lds, st, (const _Float16*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
-        case EBC_BF16: hipLaunchKernelGGL(head_fwd_kernel<__bf16>, grid, dim3(256), lds, st, (const __bf16*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
+        case EBC_F32: hipLaunchKernelGGL((head_fwd_kernel<float, CH>), grid, dim3(256), lds, st, (const float*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
+        case EBC_F16: hipLaunchKernelGGL((head_fwd_kernel<_Float16, CH>), grid, dim3(256), lds, st, (const _Float16*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
+        case EBC_BF16: hipLaunchKernelGGL((head_fwd_kernel<__bf16, CH>), grid, dim3(256), lds, st, (const __bf16*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
         default: return EBC_E_ARG;
     }
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
 
-int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale, const float* anchors,
-             const float* dlogits, const float* dexp, const float* gscale, void* dZ, float* dbias, float* dscale,
-             int P, int HW, int NB, hipStream_t st)
+int head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+             float* logits, float* expo, int P, int HW, int NB, int embed, hipStream_t st)
 {
     if (NB <= 0 || NB > 16) return EBC_E_UNSUPPORTED;
+    if (embed == 512) return head_fwd_t<512>(dtype_z, Z, text, logit_scale, anchors, logits, expo, P, HW, NB, st);
+    if (embed == 1024) return head_fwd_t<1024>(dtype_z, Z, text, logit_scale, anchors, logits, expo, P, HW, NB, st);
+    return EBC_E_UNSUPPORTED;
+}
+
+template <int CH>
+static int head_bwd_t(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
+                      const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
+                      float* dbias, float* dscale, int P, int HW, int NB, hipStream_t st)
+{
     if (dbias && hipMemsetAsync(dbias, 0, CH * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
     if (dscale && hipMemsetAsync(dscale, 0, sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
     const dim3 grid((P + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
     const size_t lds = ((size_t)NB * CH + 4 * CH + 4) * 4;
-#define HB(TZ, TD) hipLaunchKernelGGL((head_bwd_kernel<TZ, TD>), grid, dim3(256), lds, st, (const TZ*)Z, text, logit_scale, anchors, dlogits, dexp, gscale, (TD*)dZ, dbias, dscale, P, HW, NB)
+#define HB(TZ, TD) hipLaunchKernelGGL((head_bwd_kernel<TZ, TD, CH>), grid, dim3(256), lds, st, (const TZ*)Z, text, logit_scale, anchors, dlogits, dexp, gscale, (TD*)dZ, dbias, dscale, P, HW, NB)
     // the dZ element type is the caller's buffer type (dtype_dz), independent of Z's
 #define HBZ(TZ)                                                   \
     switch (dtype_dz) {                                           \
@@ -673,6 +706,18 @@ int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const 
 #undef HB
     EBC_CHECK_LAUNCH();
     return EBC_OK;
+}
+
+int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale, const float* anchors,
+             const float* dlogits, const float* dexp, const float* gscale, void* dZ, float* dbias, float* dscale,
+             int P, int HW, int NB, int embed, hipStream_t st)
+{
+    if (NB <= 0 || NB > 16) return EBC_E_UNSUPPORTED;
+    if (embed == 512)
+        return head_bwd_t<512>(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW, NB, st);
+    if (embed == 1024)
+        return head_bwd_t<1024>(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW, NB, st);
+    return EBC_E_UNSUPPORTED;
 }
 
 int attn_delta(int dtype, const void* dO, const void* O, float* delta, int B, int L, int H, hipStream_t st)

@@ -76,8 +76,8 @@ SIGNATURES = {
     "ebc_layernorm_bwd": (_I, [_I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "ebc_attention_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _P]),
     "ebc_attention_bwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
-    "ebc_head_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
-    "ebc_head_bwd": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "ebc_head_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_head_bwd": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_cast_f32": (_I, [_I, _P, _P, _Z, _P]),
     "ebc_tile_gather": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "ebc_tile_assemble": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
@@ -95,6 +95,10 @@ SIGNATURES = {
     "ebc_dec_transpose3": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_dec_prep_weights": (_I, [_I, _P, _P, _P, _I, _I, _P]),
     "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "ebc_dec_upsample": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "ebc_bn_stats": (_I, [_I, _P, _P, _P, _Z, _L, _I, _P]),
+    "ebc_bn_relu": (_I, [_I, _P, _P, _P, _P, _L, _I, _P]),
+    "ebc_bn_bwd_apply_flat": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, EbcAugConst, _P]),
     "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "ebc_probe_begin": (_I, [_I]),

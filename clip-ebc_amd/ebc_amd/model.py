@@ -11,8 +11,9 @@ Reference surface kept:
     statistics; without autocast the whole path is exact-f32 (parity mode).
 
 Execution: the 12-block encoder forward/backward is ONE C-ABI call each (`ebc_vit_forward/backward`);
-the projection + similarity head is an MFMA GEMM + a fused head kernel.  The BasicBlock decoder
-(models/utils.py:254-303) stays on PyTorch-ROCm (MIOpen) in this round.
+the BasicBlock decoder (models/utils.py:254-303) runs as implicit-GEMM 3x3 convs with BatchNorm statistics
+in the GEMM epilogue plus fused BN/ReLU/residual kernels (`_DecoderFn`); the projection + similarity head
+is an MFMA GEMM + a fused head kernel (`_HeadFn`).  The clip_resnet50 backbone (config 2) is in resnet.py.
 """
 from __future__ import annotations
 
@@ -242,16 +243,17 @@ class _HeadFn(torch.autograd.Function):
             Y = y.detach().reshape(P, C)
         else:
             Y = (y.detach() if nhwc else y.detach().permute(0, 2, 3, 1)).to(cdtype).reshape(P, C).contiguous()
-        Wc = weight.detach().reshape(EMBED, C).to(cdtype).contiguous()
+        E = weight.shape[0]                                        # CLIP joint width: 512 / 1024 (RN50)
+        Wc = weight.detach().reshape(E, C).to(cdtype).contiguous()
         bf = bias.detach().float().contiguous()
-        Z = torch.empty(P, EMBED, device=y.device, dtype=torch.float32)
+        Z = torch.empty(P, E, device=y.device, dtype=torch.float32)
         _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(Y), _lib.ptr(Wc), _lib.ptr(Z), _lib.ptr(bf), None, None,
-                              P, EMBED, C, st), "ebc_gemm(projection)")
+                              P, E, C, st), "ebc_gemm(projection)")
         ls = logit_scale.detach().float().reshape(1).contiguous()
         logits = torch.empty(B, NB, Hh, Ww, device=y.device, dtype=torch.float32)
         expo = torch.empty(B, 1, Hh, Ww, device=y.device, dtype=torch.float32)
         _lib.check(L.ebc_head_fwd(_lib.EBC_F32, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
-                                  _lib.ptr(logits), _lib.ptr(expo), P, HW, NB, st), "ebc_head_fwd")
+                                  _lib.ptr(logits), _lib.ptr(expo), P, HW, NB, E, st), "ebc_head_fwd")
         ctx.save_for_backward(Y, Wc, Z, ls, text, anchors)
         ctx.meta = (B, C, Hh, Ww, cdtype, y.dtype, weight.shape, nhwc)
         return logits, expo
@@ -272,31 +274,18 @@ class _HeadFn(torch.autograd.Function):
         dl = torch.zeros(B, NB, Hh, Ww, device=dev) if dlogits is None else dlogits.float().contiguous()
         de = torch.zeros(B, 1, Hh, Ww, device=dev) if dexp is None else dexp.float().contiguous()
         dt = _lib.dtype_code(cdtype)
-        dZ = torch.empty(P, EMBED, device=dev, dtype=cdtype)
-        dbias = torch.empty(EMBED, device=dev, dtype=torch.float32)
+        E = Wc.shape[0]
+        dZ = torch.empty(P, E, device=dev, dtype=cdtype)
+        dbias = torch.empty(E, device=dev, dtype=torch.float32)
         dscale = torch.empty(1, device=dev, dtype=torch.float32)
         _lib.check(L.ebc_head_bwd(_lib.EBC_F32, dt, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
                                   _lib.ptr(dl), _lib.ptr(de), None, _lib.ptr(dZ), _lib.ptr(dbias), _lib.ptr(dscale),
-                                  P, HW, NB, st), "ebc_head_bwd")
-        Wt = Wc.t().contiguous()                                   # [C, 512]
+                                  P, HW, NB, E, st), "ebc_head_bwd")
+        Wt = Wc.t().contiguous()                                   # [C, E]
         dY = torch.empty(P, C, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dZ), _lib.ptr(Wt), _lib.ptr(dY), None, None, None,
-                              P, C, EMBED, st), "ebc_gemm(projection dX)")
-        # dW = dZ^T Y over K = B*H*W pixels: both operands transposed to K-contiguous, split-K MFMA GEMM
-        # (K padded with zero columns to the GEMM's K step when B*H*W is not a multiple of it)
-        kstep = 32 if cdtype == torch.float32 else 64
-        Pp = -(-P // kstep) * kstep
-        alloc = torch.empty if Pp == P else torch.zeros
-        dZT = alloc(EMBED, Pp, device=dev, dtype=cdtype)
-        YT = alloc(C, Pp, device=dev, dtype=cdtype)
-        _lib.check(L.ebc_transpose(dt, _lib.ptr(dZ), _lib.ptr(dZT), P, EMBED, Pp, st), "ebc_transpose(dZ)")
-        _lib.check(L.ebc_transpose(dt, _lib.ptr(Y), _lib.ptr(YT), P, C, Pp, st), "ebc_transpose(Y)")
-        dW = torch.empty(EMBED, C, device=dev, dtype=torch.float32)
-        nb = L.ebc_gemm_wgrad_workspace_bytes(dt, EMBED, C, Pp)
-        ws = _dec_workspace(dev, nb, slot=2)
-        _lib.check(L.ebc_gemm_wgrad(dt, _lib.ptr(dZT), _lib.ptr(YT), _lib.ptr(dW), EMBED, C, Pp, _lib.ptr(ws), ws.numel(),
-                                    st), "ebc_gemm_wgrad(projection dW)")
-        dW = dW.reshape(wshape)
+                              P, C, E, st), "ebc_gemm(projection dX)")
+        dW = _wgrad_rows(L, dZ, Y, cdtype, dev, st).reshape(wshape)
         dy = dY.view(B, Hh, Ww, C) if nhwc else dY.view(B, Hh, Ww, C).permute(0, 3, 1, 2).to(ydt)
         return dy, dW, dbias, dscale.reshape(()), None, None, None, None
 
@@ -318,6 +307,27 @@ def _dec_workspace(dev: torch.device, nbytes: int, slot: int = 0) -> Tensor:
         ws = torch.zeros(max(nbytes, 1 << 20), device=dev, dtype=torch.uint8)
         _DEC_WS[(dev, slot)] = ws
     return ws
+
+
+def _wgrad_rows(L, dZ: Tensor, Y: Tensor, cdtype: torch.dtype, dev: torch.device, st) -> Tensor:
+    """dW [E, C] f32 = dZ^T Y for row matrices dZ [P, E], Y [P, C] (a 1x1 conv's weight gradient over
+    K = B*H*W pixels): both operands transposed to K-contiguous, then the split-K MFMA GEMM (K padded with
+    zero columns to the GEMM's K step when P is not a multiple of it)."""
+    dt = _lib.dtype_code(cdtype)
+    P, E = dZ.shape
+    C = Y.shape[1]
+    kstep = 32 if cdtype == torch.float32 else 64
+    Pp = -(-P // kstep) * kstep
+    alloc = torch.empty if Pp == P else torch.zeros
+    dZT = alloc(E, Pp, device=dev, dtype=cdtype)
+    YT = alloc(C, Pp, device=dev, dtype=cdtype)
+    _lib.check(L.ebc_transpose(dt, _lib.ptr(dZ), _lib.ptr(dZT), P, E, Pp, st), "ebc_transpose(dZ)")
+    _lib.check(L.ebc_transpose(dt, _lib.ptr(Y), _lib.ptr(YT), P, C, Pp, st), "ebc_transpose(Y)")
+    dW = torch.empty(E, C, device=dev, dtype=torch.float32)
+    ws = _dec_workspace(dev, L.ebc_gemm_wgrad_workspace_bytes(dt, E, C, Pp), slot=2)
+    _lib.check(L.ebc_gemm_wgrad(dt, _lib.ptr(dZT), _lib.ptr(YT), _lib.ptr(dW), E, C, Pp, _lib.ptr(ws), ws.numel(), st),
+               "ebc_gemm_wgrad")
+    return dW
 
 
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
@@ -506,7 +516,8 @@ vit_backbones = ["vit_b_16"]
 
 
 class CLIP_EBC(nn.Module):
-    """models/clip/model.py:30-217 for the vit_b_16 backbone."""
+    """models/clip/model.py:30-217 for the vit_b_16 (deep VPT, frozen encoder) and resnet50 (trainable
+    ModifiedResNet, Bottleneck decoder; ebc_amd/resnet.py) backbones."""
 
     def __init__(self, backbone: str, bins: List[Tuple[float, float]], anchor_points: List[float],
                  reduction: Optional[int] = None, freeze_text_encoder: bool = True, prompt_type: str = "number",
@@ -515,38 +526,49 @@ class CLIP_EBC(nn.Module):
                  text_layers: int = 12, text_features: Optional[Tensor] = None, weights_seed: Optional[int] = None,
                  **kwargs: Any) -> None:
         super().__init__()
-        if backbone not in vit_backbones:
-            raise NotImplementedError(f"backbone {backbone!r}: only vit_b_16 is on the MI355X path (SURVEY.md §8)")
-        assert input_size is not None, "Expected input_size to be an integer, got None."
-        assert num_vpt is not None, "Expected num_vpt to be an integer, got None."
-        assert deep_vpt is not None, "Expected deep_vpt to be a boolean, got None."
-        assert vpt_drop is not None, "Expected vpt_drop to be a float, got None."
+        if backbone not in vit_backbones + ["resnet50"]:
+            raise NotImplementedError(f"backbone {backbone!r}: vit_b_16 and resnet50 are on the MI355X path (SURVEY.md §8)")
         self.backbone = backbone
-        self.image_encoder = VisionTransformer(input_size, PATCH, EMBED, WIDTH, vit_layers, HEADS)
-        self.image_encoder_depth = vit_layers
-        for p in self.image_encoder.parameters():
-            p.requires_grad = False
-        self.num_vpt, self.deep_vpt, self.vpt_drop = num_vpt, deep_vpt, vpt_drop
-        val = math.sqrt(6.0 / float(3 * PATCH + WIDTH))
-        for idx in range(vit_layers if deep_vpt else 1):
-            setattr(self, f"vpt_{idx}", nn.Parameter(torch.empty(num_vpt, WIDTH).uniform_(-val, val)))
-        self.encoder_reduction = PATCH
-        self.reduction = self.encoder_reduction if reduction is None else reduction
-        self.channels, self.clip_embed_dim = WIDTH, EMBED
-        decoder_cfg = decoder_cfg or [WIDTH]
-        if list(decoder_cfg) != [WIDTH]:
-            raise NotImplementedError("vit_b_16 decoder is BasicBlock [768] (models/clip/model.py:250-251)")
-        if reduction is not None and (PATCH % reduction or PATCH // reduction not in (1, 2)):
-            raise NotImplementedError("reduction must be 16 or 8 for vit_b_16 (x1 / x2 bilinear adapt)")
-        layers, cin = [], WIDTH
-        for v in decoder_cfg:
-            layers.append(BasicBlock(cin, v))
-            cin = v
-        self.image_decoder = nn.Sequential(*layers)
-        self.channels = decoder_cfg[-1]
-        self.projection = nn.Conv2d(self.channels, EMBED, kernel_size=1)
+        if backbone == "resnet50":
+            from .resnet import Bottleneck, ModifiedResNet
+            from .synthetic import RN50_CHANNELS, RN50_EMBED
+            # models/clip/model.py:51-52 (trainable encoder), :83-95 (decoder cfg [2048] + projection)
+            self.image_encoder = ModifiedResNet(reduction=reduction).to(memory_format=torch.channels_last)
+            self.encoder_reduction = self.image_encoder.reduction
+            self.reduction = self.encoder_reduction if reduction is None else reduction
+            decoder_cfg = decoder_cfg or [RN50_CHANNELS]
+            if list(decoder_cfg) != [RN50_CHANNELS]:
+                raise NotImplementedError("resnet50 decoder is Bottleneck [2048] (models/clip/model.py:237-238)")
+            if self.encoder_reduction % self.reduction or self.encoder_reduction // self.reduction not in (1, 2):
+                raise NotImplementedError("resnet50: reduction must give a x1 / x2 bilinear adapt")
+            self.image_decoder = nn.Sequential(Bottleneck(RN50_CHANNELS, RN50_CHANNELS, expansion=1))
+            embed = RN50_EMBED
+        else:
+            assert input_size is not None, "Expected input_size to be an integer, got None."
+            assert num_vpt is not None, "Expected num_vpt to be an integer, got None."
+            assert deep_vpt is not None, "Expected deep_vpt to be a boolean, got None."
+            assert vpt_drop is not None, "Expected vpt_drop to be a float, got None."
+            self.image_encoder = VisionTransformer(input_size, PATCH, EMBED, WIDTH, vit_layers, HEADS)
+            self.image_encoder_depth = vit_layers
+            for p in self.image_encoder.parameters():
+                p.requires_grad = False
+            self.num_vpt, self.deep_vpt, self.vpt_drop = num_vpt, deep_vpt, vpt_drop
+            val = math.sqrt(6.0 / float(3 * PATCH + WIDTH))
+            for idx in range(vit_layers if deep_vpt else 1):
+                setattr(self, f"vpt_{idx}", nn.Parameter(torch.empty(num_vpt, WIDTH).uniform_(-val, val)))
+            self.encoder_reduction = PATCH
+            self.reduction = self.encoder_reduction if reduction is None else reduction
+            decoder_cfg = decoder_cfg or [WIDTH]
+            if list(decoder_cfg) != [WIDTH]:
+                raise NotImplementedError("vit_b_16 decoder is BasicBlock [768] (models/clip/model.py:250-251)")
+            if reduction is not None and (PATCH % reduction or PATCH // reduction not in (1, 2)):
+                raise NotImplementedError("reduction must be 16 or 8 for vit_b_16 (x1 / x2 bilinear adapt)")
+            self.image_decoder = nn.Sequential(BasicBlock(WIDTH, WIDTH))
+            embed = EMBED
+        self.channels, self.clip_embed_dim = decoder_cfg[-1], embed
+        self.projection = nn.Conv2d(self.channels, embed, kernel_size=1)
         self.prompt_type = prompt_type
-        self.text_encoder = CLIPTextEncoder(EMBED, 77, 49408, 512, 8, text_layers)
+        self.text_encoder = CLIPTextEncoder(embed, 77, 49408, 512, 8, text_layers)
         self.freeze_text_encoder = freeze_text_encoder
         for p in self.text_encoder.parameters():
             p.requires_grad = False
@@ -558,7 +580,7 @@ class CLIP_EBC(nn.Module):
         if weights_seed is not None:
             self._load_synthetic(weights_seed, vit_layers, text_layers, input_size)
         self._given_text = text_features
-        self.register_buffer("text_features", torch.zeros(len(bins), EMBED), persistent=False)
+        self.register_buffer("text_features", torch.zeros(len(bins), embed), persistent=False)
         self.register_buffer("_anchors", self.anchor_points.reshape(-1).clone(), persistent=False)
         self._refresh_text()
         self._cache: Optional[_EncoderCache] = None
@@ -566,7 +588,10 @@ class CLIP_EBC(nn.Module):
 
     # -- weights ---------------------------------------------------------------------------
     def _load_synthetic(self, seed, vit_layers, text_layers, input_size):
-        sd = synthetic.full_state(seed, layers=vit_layers, text_layers=text_layers, input_size=input_size)
+        if self.backbone == "resnet50":
+            sd = synthetic.resnet50_full_state(seed, text_layers=text_layers)
+        else:
+            sd = synthetic.full_state(seed, layers=vit_layers, text_layers=text_layers, input_size=input_size)
         own = self.state_dict()
         sd = {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items() if k in own}
         self.load_state_dict(sd, strict=False)
@@ -626,10 +651,28 @@ class CLIP_EBC(nn.Module):
         """[B,3,H,W] -> [B,768,H/16,W/16] (channels_last memory), models/clip/model.py:142-189."""
         return self._forward_vpt_nhwc(x).permute(0, 3, 1, 2)
 
+    def _forward_resnet(self, x: Tensor, cdt: torch.dtype) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+        """models/clip/model.py:191-217 for the resnet50 backbone: the trainable ModifiedResNet on PyTorch-ROCm
+        (channels_last, the caller's autocast), then the HIP Bottleneck decoder and head."""
+        from .resnet import _BottleneckFn
+        feat = self.image_encoder(x.contiguous(memory_format=torch.channels_last))
+        feat = feat.permute(0, 2, 3, 1).float().contiguous()                # NHWC rows, f32
+        up = self.encoder_reduction // self.reduction
+        blk = self.image_decoder[0]
+        with torch.autocast("cuda", enabled=False):
+            y = _BottleneckFn.apply(feat, blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn1.weight,
+                                    blk.bn1.bias, blk.bn2.weight, blk.bn2.bias, blk.bn3.weight, blk.bn3.bias, blk, up,
+                                    cdt, self.training)
+            logits, exp = _HeadFn.apply(y, self.projection.weight, self.projection.bias, self.logit_scale,
+                                        self.text_features, self._anchors, cdt, True)
+        return (logits, exp) if self.training else exp
+
     def forward(self, x: Tensor) -> Union[Tensor, Tuple[Tensor, Tensor]]:
         if not x.is_cuda:
             raise RuntimeError("ebc_amd.CLIP_EBC runs on the MI355X HIP path only (input is on the CPU)")
         cdt = self._compute_dtype(x)
+        if self.backbone == "resnet50":
+            return self._forward_resnet(x, cdt)
         feat = self._forward_vpt_nhwc(x)
         up = self.encoder_reduction // self.reduction                      # model.py:195-196 (x2 for reduction 8)
         blk = self.image_decoder[0]
@@ -644,7 +687,7 @@ class CLIP_EBC(nn.Module):
 def _clip_ebc(backbone: str, bins, anchor_points, reduction=None, freeze_text_encoder=True, prompt_type="number",
               input_size=None, num_vpt=None, deep_vpt=None, vpt_drop=None, decoder_block=None, decoder_cfg=None,
               **kw) -> CLIP_EBC:
-    """models/clip/model.py:220-270 (vit_b_16: BasicBlock decoder [768])."""
+    """models/clip/model.py:220-270 (vit_b_16: BasicBlock decoder [768]; resnet50: Bottleneck decoder [2048])."""
     return CLIP_EBC(backbone, bins, anchor_points, reduction=reduction, freeze_text_encoder=freeze_text_encoder,
                     prompt_type=prompt_type, input_size=input_size, num_vpt=num_vpt, deep_vpt=deep_vpt,
                     vpt_drop=vpt_drop, decoder_cfg=decoder_cfg, **kw)
@@ -652,10 +695,10 @@ def _clip_ebc(backbone: str, bins, anchor_points, reduction=None, freeze_text_en
 
 def get_model(backbone: str, input_size: int, reduction: int, bins: Optional[List[Tuple[float, float]]] = None,
               anchor_points: Optional[List[float]] = None, **kwargs: Any) -> CLIP_EBC:
-    """models/__init__.py:10-44.  Only the CLIP ViT-B/16 family is on the MI355X path."""
+    """models/__init__.py:10-44.  clip_vit_b_16 and clip_resnet50 are on the MI355X path."""
     backbone = backbone.lower()
     if "clip" not in backbone:
-        raise NotImplementedError(f"{backbone}: only clip_vit_b_16 is built for MI355X (SURVEY.md §8)")
+        raise NotImplementedError(f"{backbone}: only clip_vit_b_16 / clip_resnet50 are built for MI355X (SURVEY.md §8)")
     backbone = backbone[5:]
     assert bins is not None and anchor_points is not None, "CLIP-EBC needs bins and anchor_points"
     kwargs.setdefault("prompt_type", "number")

@@ -1,4 +1,4 @@
-"""Deterministic synthetic weights and crops for CLIP-EBC (ViT-B/16 + deep VPT).
+"""Deterministic synthetic weights and crops for CLIP-EBC (ViT-B/16 + deep VPT; CLIP ResNet-50, config 2).
 
 There are no CLIP checkpoints offline (the reference downloads them on import,
 `models/clip/_clip/__init__.py:31-36`), so parity and benchmarking run on weights
@@ -79,7 +79,7 @@ def vit_state(seed: int = 0, layers: int = 12, input_size: int = 224) -> Dict[st
     return sd
 
 
-def text_state(seed: int = 0, layers: int = 12) -> Dict[str, np.ndarray]:
+def text_state(seed: int = 0, layers: int = 12, embed: int = EMBED) -> Dict[str, np.ndarray]:
     """Frozen CLIP text tower (`text_encoder.py:7-53`)."""
     sd: Dict[str, np.ndarray] = {}
     p = "text_encoder."
@@ -89,7 +89,7 @@ def text_state(seed: int = 0, layers: int = 12) -> Dict[str, np.ndarray]:
         _block(sd, seed, f"{p}transformer.resblocks.{i}.", TEXT_WIDTH)
     sd[p + "ln_final.weight"] = _normal(seed, p + "ln_final.weight", (TEXT_WIDTH,), 0.05, 1.0)
     sd[p + "ln_final.bias"] = _normal(seed, p + "ln_final.bias", (TEXT_WIDTH,), 0.05)
-    sd[p + "text_projection"] = _normal(seed, p + "text_projection", (TEXT_WIDTH, EMBED), TEXT_WIDTH ** -0.5)
+    sd[p + "text_projection"] = _normal(seed, p + "text_projection", (TEXT_WIDTH, embed), TEXT_WIDTH ** -0.5)
     return sd
 
 
@@ -125,6 +125,74 @@ def full_state(seed: int = 0, layers: int = 12, text_layers: int = 12, input_siz
     sd.update(trainable_state(seed, layers))
     if include_text:
         sd.update(text_state(seed, text_layers))
+    return sd
+
+
+# ----------------------------------------------------------------------------- CLIP ResNet-50 (config 2)
+RN50_LAYERS = (3, 4, 6, 3)
+RN50_WIDTH = 64
+RN50_EMBED = 1024          # clip_resnet50 joint embedding (models/clip/model.py:16)
+RN50_CHANNELS = 2048       # layer4 output = decoder cfg [2048] (models/clip/model.py:237-238)
+
+
+def _bn(sd, seed, key, n, gamma_mean=1.0):
+    sd[key + ".weight"] = _normal(seed, key + ".weight", (n,), 0.05, gamma_mean)
+    sd[key + ".bias"] = _normal(seed, key + ".bias", (n,), 0.05)
+    sd[key + ".running_mean"] = np.zeros(n, np.float32)
+    sd[key + ".running_var"] = np.ones(n, np.float32)
+    sd[key + ".num_batches_tracked"] = np.zeros((), np.int64)
+
+
+def _conv(sd, seed, key, cout, cin, k):
+    sd[key + ".weight"] = _normal(seed, key + ".weight", (cout, cin, k, k), math.sqrt(2.0 / (cin * k * k)))
+
+
+def resnet50_state(seed: int = 0, layers=RN50_LAYERS, width: int = RN50_WIDTH) -> Dict[str, np.ndarray]:
+    """CLIP ModifiedResNet image tower, features_only (`image_encoder.py:10-77`, blocks.py:56-101): He-normal
+    convs, BatchNorm gamma ~1 (the residual branch's bn3 at 0.25 so 16 stacked blocks stay well scaled)."""
+    sd: Dict[str, np.ndarray] = {}
+    p = "image_encoder."
+    _conv(sd, seed, p + "conv1", width // 2, 3, 3); _bn(sd, seed, p + "bn1", width // 2)
+    _conv(sd, seed, p + "conv2", width // 2, width // 2, 3); _bn(sd, seed, p + "bn2", width // 2)
+    _conv(sd, seed, p + "conv3", width, width // 2, 3); _bn(sd, seed, p + "bn3", width)
+    inplanes = width
+    for li, nblocks in enumerate(layers):
+        planes = width * (2 ** li)
+        for bi in range(nblocks):
+            q = f"{p}layer{li + 1}.{bi}."
+            _conv(sd, seed, q + "conv1", planes, inplanes, 1); _bn(sd, seed, q + "bn1", planes)
+            _conv(sd, seed, q + "conv2", planes, planes, 3); _bn(sd, seed, q + "bn2", planes)
+            _conv(sd, seed, q + "conv3", planes * 4, planes, 1); _bn(sd, seed, q + "bn3", planes * 4, 0.25)
+            if bi == 0:
+                _conv(sd, seed, q + "downsample.0", planes * 4, inplanes, 1); _bn(sd, seed, q + "downsample.1", planes * 4)
+            inplanes = planes * 4
+    return sd
+
+
+def resnet50_trainable_state(seed: int = 0) -> Dict[str, np.ndarray]:
+    """Decoder Bottleneck(2048, 2048, expansion=1) and projection 2048 -> 1024 with the reference's init laws:
+    kaiming_normal(fan_out, relu) convs, BN (1, 0) (`models/utils.py:366-379`), logit_scale = ln(1/0.07)."""
+    sd: Dict[str, np.ndarray] = {}
+    d = "image_decoder.0."
+    C = RN50_CHANNELS
+    for c, bn, k in (("conv1", "bn1", 1), ("conv2", "bn2", 3), ("conv3", "bn3", 1)):
+        sd[d + c + ".weight"] = _normal(seed, d + c + ".weight", (C, C, k, k), math.sqrt(2.0 / (C * k * k)))
+        sd[d + bn + ".weight"] = np.ones(C, np.float32)
+        sd[d + bn + ".bias"] = np.zeros(C, np.float32)
+        sd[d + bn + ".running_mean"] = np.zeros(C, np.float32)
+        sd[d + bn + ".running_var"] = np.ones(C, np.float32)
+        sd[d + bn + ".num_batches_tracked"] = np.zeros((), np.int64)
+    sd["projection.weight"] = _normal(seed, "projection.weight", (RN50_EMBED, C, 1, 1), math.sqrt(2.0 / RN50_EMBED))
+    sd["projection.bias"] = np.zeros(RN50_EMBED, np.float32)
+    sd["logit_scale"] = np.array(math.log(1 / 0.07), np.float32)
+    return sd
+
+
+def resnet50_full_state(seed: int = 0, text_layers: int = 12, include_text: bool = True) -> Dict[str, np.ndarray]:
+    sd = resnet50_state(seed)
+    sd.update(resnet50_trainable_state(seed))
+    if include_text:
+        sd.update(text_state(seed, text_layers, embed=RN50_EMBED))
     return sd
 
 

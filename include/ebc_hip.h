@@ -174,14 +174,15 @@ int ebc_attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, 
 int ebc_attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse,
                       float* delta_ws, void* dqkv, int B, int L, int H, ebc_stream_t stream);
 /* Blockwise image-text similarity head (models/clip/model.py:200-217):
- * Z [P=B*HW, 512] projected features (NHWC rows) -> logits [B,NB,HW], exp [B,1,HW].
+ * Z [P=B*HW, embed] projected features (NHWC rows) -> logits [B,NB,HW], exp [B,1,HW]; text [NB, embed];
+ * embed = the CLIP joint width: 512 (ViT-B/16) or 1024 (ResNet-50), NB <= 16.
  * Backward: dZ (element type dtype_dz), d projection bias (column sums), d logit_scale; gscale (device scalar) scales the
  * upstream gradients (NULL = 1). */
 int ebc_head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
-                 float* logits, float* expo, int P, int HW, int NB, ebc_stream_t stream);
+                 float* logits, float* expo, int P, int HW, int NB, int embed, ebc_stream_t stream);
 int ebc_head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
                  const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
-                 float* dbias, float* dscale, int P, int HW, int NB, ebc_stream_t stream);
+                 float* dbias, float* dscale, int P, int HW, int NB, int embed, ebc_stream_t stream);
 int ebc_cast_f32(int dtype, const float* in, void* out, size_t n, ebc_stream_t stream);
 
 /* Sliding-window evaluation (utils/eval_utils.py:26-96).  Tiles t = i*cols + j, rows/cols =
@@ -290,6 +291,23 @@ int ebc_dec_prep_weights(int dtype, const float* w, void* wk, void* wf, int N, i
 /* dfeat [B][h][w][C] f32 = bilinear_up^T(g), g [B*H*W][C] (up = 1 or 2) */
 int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int B, int h, int w, int C, int up,
                          ebc_stream_t stream);
+/* Flat-layout helpers of the ResNet-50 decoder Bottleneck (models/utils.py:306-363 with expansion 1, cfg [2048],
+ * models/clip/model.py:234-246): its 1x1 convs are ebc_gemm products on unpadded rows [P = B*H*W][C]; the middle
+ * 3x3 conv uses ebc_conv3x3_* above.
+ *   ebc_dec_upsample:      x [P][C] T = bilinear x`up` upsample of feat [B][h][w][C] f32 (unpadded)
+ *   ebc_bn_stats:          colsum [2][C] f64 = (sum z, sum z*z) over the P rows of z (BatchNorm batch statistics);
+ *                          workspace as ebc_bn_bwd_reduce's (>= ebc_dec_workspace_bytes for that geometry)
+ *   ebc_bn_relu:           out [P][C] T = relu(z*scale + shift)
+ *   ebc_bn_bwd_apply_flat: dz [P][C] T = BatchNorm input gradient (coef from ebc_bn_bwd_finalize), g = gy * relu'(mask_y,
+ *                          or z*scale+shift when mask_y == NULL); gmask != NULL also receives g [P][C] f32 (the
+ *                          identity branch's gradient). */
+int ebc_dec_upsample(int dtype, const float* feat, void* x, int B, int h, int w, int C, int up, ebc_stream_t stream);
+int ebc_bn_stats(int dtype, const void* z, double* colsum, void* ws, size_t wsb, long P, int C, ebc_stream_t stream);
+int ebc_bn_relu(int dtype, const void* z, const float* scale, const float* shift, void* out, long P, int C,
+                ebc_stream_t stream);
+int ebc_bn_bwd_apply_flat(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
+                          const float* rstd, const float* scale, const float* shift, const float* coef, void* dz,
+                          float* gmask, long P, int C, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Measurement (bench.py): in-step kernel durations and profile windows.  Not on the reference's

@@ -223,3 +223,68 @@ def params_from_state(sd: Dict[str, np.ndarray], requires_grad: bool = True) -> 
 def forward(p, x, text_features, anchors, layers: int):
     feats = vit_vpt_forward(p, x, layers)
     return head(p, decoder(p, feats), text_features, anchors) + (feats,)
+
+
+# ----------------------------------------------------------------------------- clip_resnet50 (config 2)
+RESNET_TRAINABLE_PREFIXES = ("image_encoder.", "image_decoder.", "projection.", "logit_scale")
+
+
+def _bn_conv(p, x, conv, bn, stride=1, padding=0):
+    o = F.conv2d(x, p[conv + ".weight"], stride=stride, padding=padding)
+    return batch_norm_train(o, p[bn + ".weight"], p[bn + ".bias"])
+
+
+def resnet_encoder(p, x, layers=(3, 4, 6, 3), reduction: int = 8):
+    """ModifiedResNet features_only, out_indices=(-1,) (models/clip/_clip/image_encoder.py:36-115): 3-conv stem +
+    avgpool, Bottleneck stages (blocks.py:56-101: avgpool before conv3 and in the downsample when strided),
+    layer4 at stride 1 when reduction <= 16."""
+    e = "image_encoder."
+    x = F.relu(_bn_conv(p, x, e + "conv1", e + "bn1", stride=2, padding=1))
+    x = F.relu(_bn_conv(p, x, e + "conv2", e + "bn2", padding=1))
+    x = F.relu(_bn_conv(p, x, e + "conv3", e + "bn3", padding=1))
+    x = F.avg_pool2d(x, 2)
+    for li, n in enumerate(layers):
+        stride = 1 if li == 0 else (2 if li < 3 or reduction > 16 else 1)
+        for bi in range(n):
+            q = f"{e}layer{li + 1}.{bi}."
+            s = stride if bi == 0 else 1
+            o = F.relu(_bn_conv(p, x, q + "conv1", q + "bn1"))
+            o = F.relu(_bn_conv(p, o, q + "conv2", q + "bn2", padding=1))
+            if s > 1:
+                o = F.avg_pool2d(o, s)
+            o = _bn_conv(p, o, q + "conv3", q + "bn3")
+            if q + "downsample.0.weight" in p:
+                idt = F.avg_pool2d(x, s) if s > 1 else x
+                idt = _bn_conv(p, idt, q + "downsample.0", q + "downsample.1")
+            else:
+                idt = x
+            x = F.relu(o + idt)
+    return x
+
+
+def bottleneck_decoder(p, x, up: int = 2):
+    """Bottleneck(2048, 2048, expansion=1) (models/utils.py:346-363) after the bilinear x`up` adapt
+    (models/clip/model.py:195-196)."""
+    if up != 1:
+        x = F.interpolate(x, scale_factor=float(up), mode="bilinear")
+    d = "image_decoder.0."
+    o = F.relu(_bn_conv(p, x, d + "conv1", d + "bn1"))
+    o = F.relu(_bn_conv(p, o, d + "conv2", d + "bn2", padding=1))
+    o = _bn_conv(p, o, d + "conv3", d + "bn3")
+    return F.relu(o + x)
+
+
+def resnet_params_from_state(sd: Dict[str, np.ndarray]) -> Dict[str, torch.Tensor]:
+    out = {}
+    for k, v in sd.items():
+        t = torch.tensor(np.asarray(v))
+        if k.startswith(RESNET_TRAINABLE_PREFIXES) and t.is_floating_point() and "running_" not in k:
+            t.requires_grad_(True)
+        out[k] = t
+    return out
+
+
+def resnet_forward(p, x, text_features, anchors, reduction: int = 8):
+    feats = resnet_encoder(p, x, reduction=reduction)
+    return head(p, bottleneck_decoder(p, feats, 16 // reduction if reduction <= 16 else 1), text_features,
+                anchors) + (feats,)

@@ -35,13 +35,19 @@ def golden(name: str):
     return np.load(os.path.join(GOLDEN, name))
 
 
+def _np(a):
+    if hasattr(a, "detach"):                      # torch tensors (any device, grad or not)
+        a = a.detach().float().cpu().numpy() if a.dtype.is_floating_point and a.dtype.itemsize < 4 else a.detach().cpu().numpy()
+    return np.asarray(a, np.float64)
+
+
 def rel_l2(a, b) -> float:
-    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    a = _np(a); b = _np(b)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
 def rel_max(a, b) -> float:
-    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    a = _np(a); b = _np(b)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 

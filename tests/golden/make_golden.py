@@ -88,6 +88,11 @@ def load_reference():
     _clip.vit_b_16_img = lambda features_only=True, input_size=224, **kw: ie.VisionTransformer(
         input_size, 16, 512, 768, state["vit_layers"], 12, features_only=features_only)
     _clip.vit_b_16_txt = lambda: te.CLIPTextEncoder(512, 77, 49408, 512, 8, 12)
+    # clip_image_encoder_resnet50.json / clip_text_encoder_resnet50.json values (models/clip/_clip/__init__.py:73-148):
+    # layers (3,4,6,3), width 64, embed 1024, heads 32, resolution 224; text 512 wide, 8 heads, 12 layers
+    _clip.resnet50_img = lambda features_only=True, out_indices=None, reduction=32, **kw: ie.ModifiedResNet(
+        (3, 4, 6, 3), 1024, 224, 64, 32, features_only=features_only, out_indices=out_indices, reduction=reduction)
+    _clip.resnet50_txt = lambda: te.CLIPTextEncoder(1024, 77, 49408, 512, 8, 12)
     model_mod = _load("models.clip.model", f"{REF}/models/clip/model.py")
     eval_utils = _load("ref_eval_utils", f"{REF}/utils/eval_utils.py")
     return types.SimpleNamespace(losses=losses, sinkhorn=sinkhorn, model_mod=model_mod, state=state,
@@ -339,6 +344,55 @@ def e2e_case(ref, layers: int, seed: int = 7, B: int = 2, counts=(37, 5)):
     return out
 
 
+ANCHORS_SHA = [0.0, 1.0, 2.0, 3.0, 4.29992]     # configs/reduction_8.json ["4"]["sha"]
+
+
+def resnet_case(ref, seed: int = 9, B: int = 2, size: int = 448, counts=(60, 3)):
+    """F7: clip_resnet50 (config 2 geometry: 448 crops, reduction 8, word prompts, SHA anchors) forward + DACE
+    loss + backward in fp32, on the synthetic ResNet-50 weights (ebc_amd.synthetic.resnet50_full_state(0))."""
+    torch.manual_seed(0)
+    m = ref.model_mod._clip_ebc("resnet50", BINS, ANCHORS_SHA, reduction=8, prompt_type="word", input_size=size)
+    sd = syn.resnet50_full_state(0)
+    missing, unexpected = m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, strict=False)
+    assert not unexpected, unexpected
+    assert not missing, missing
+    m._extract_text_features()
+    img, points, density = syn.synthetic_crops(B, size, seed=seed, counts=list(counts))
+    x = torch.from_numpy(img)
+    feats = {}
+    h = m.image_encoder.layer4.register_forward_hook(lambda mod, i, o: feats.__setitem__("enc", o.detach()))
+    m.train()
+    logits, exp = m(x)
+    h.remove()
+    loss_fn = ref.losses.DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=size)
+    loss, info = loss_fn(logits, exp, torch.from_numpy(density), [torch.from_numpy(p) for p in points])
+    loss.backward()
+    dec = m.image_decoder[0]
+    enc = m.image_encoder
+    out = dict(seed=seed, counts=np.asarray(counts), size=size, logits=logits.detach().numpy(),
+               exp=exp.detach().numpy(), enc_out_sub=feats["enc"].numpy()[:, ::7, ::3, ::3],
+               text_features=m.text_features.numpy(),
+               grad_proj_w_sub=m.projection.weight.grad.numpy()[::5, ::7], grad_proj_b=m.projection.bias.grad.numpy(),
+               grad_logit_scale=m.logit_scale.grad.numpy(),
+               grad_dec_conv1_sub=dec.conv1.weight.grad.numpy()[::9, ::9],
+               grad_dec_conv2_sub=dec.conv2.weight.grad.numpy()[::17, ::17],
+               grad_dec_conv3_sub=dec.conv3.weight.grad.numpy()[::9, ::9],
+               grad_dec_bn1_w=dec.bn1.weight.grad.numpy(), grad_dec_bn2_b=dec.bn2.bias.grad.numpy(),
+               grad_dec_bn3_w=dec.bn3.weight.grad.numpy(), grad_dec_bn3_b=dec.bn3.bias.grad.numpy(),
+               grad_enc_conv1=enc.conv1.weight.grad.numpy(),
+               grad_enc_l4_conv3_sub=enc.layer4[2].conv3.weight.grad.numpy()[::11, ::7],
+               grad_enc_l1_bn1_w=enc.layer1[0].bn1.weight.grad.numpy(),
+               dec_bn2_running_mean=dec.bn2.running_mean.numpy(), dec_bn3_running_var=dec.bn3.running_var.numpy(),
+               state_keys=np.asarray(sorted(m.state_dict().keys())),
+               trainable_keys=np.asarray(sorted(k for k, p in m.named_parameters() if p.requires_grad)))
+    for k, v in info.items():
+        out["info_" + k] = v.detach().numpy().reshape(())
+    m.eval()
+    with torch.no_grad():
+        out["exp_eval"] = m(x).numpy()
+    return out
+
+
 def sliding_case(ref):
     """F5: sliding-window tiling + overlap averaging with a stub model (utils/eval_utils.py:26-96)."""
     class Stub(torch.nn.Module):
@@ -433,6 +487,8 @@ def main():
             bpe_merges()
         if "f6b" in want:
             save("f6b_tokens.npz", **tokenizer_case(ref))
+        if "f7" in want:
+            save("f7_resnet50.npz", **resnet_case(ref))
         return
     prompt_table(ref)
     bpe_merges()
@@ -448,6 +504,7 @@ def main():
     save("f5_sliding.npz", **sliding_case(ref))
     save("f4_e2e_l2.npz", **e2e_case(ref, layers=2))
     save("f3_e2e_l12.npz", **e2e_case(ref, layers=12))
+    save("f7_resnet50.npz", **resnet_case(ref))
 
 
 if __name__ == "__main__":

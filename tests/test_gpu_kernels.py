@@ -79,23 +79,25 @@ def test_attention_fwd_bwd(dname, B, L):
         assert _rel(d3[:, i], r3[:, i]) < tol, i
 
 
+@pytest.mark.parametrize("embed", [512, 1024])
 @pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
-def test_head_bwd_dz_dtypes(dname):
-    """dZ is written in the caller's dtype (fp16/bf16 under autocast), checked against autograd."""
+def test_head_bwd_dz_dtypes(dname, embed):
+    """dZ is written in the caller's dtype (fp16/bf16 under autocast), checked against autograd; both CLIP joint
+    widths (ViT-B/16 512, ResNet-50 1024)."""
     dt = DT[dname]
     P, HW, NB = 2 * 784, 784, 5
     g = torch.Generator(device="cuda").manual_seed(3)
-    Z = torch.randn(P, 512, device="cuda", generator=g)
-    text = torch.randn(NB, 512, device="cuda", generator=g)
+    Z = torch.randn(P, embed, device="cuda", generator=g)
+    text = torch.randn(NB, embed, device="cuda", generator=g)
     ls = torch.tensor([2.3], device="cuda")
     anchors = torch.tensor(ANCHORS_NWPU, device="cuda")
     dl = torch.randn(2, NB, 28, 28, device="cuda", generator=g)
     de = torch.randn(2, 1, 28, 28, device="cuda", generator=g)
-    dZ = torch.full((P + 64, 512), 7.0, device="cuda", dtype=dt)        # guard rows must survive
-    dbias = torch.empty(512, device="cuda"); dsc = torch.empty(1, device="cuda")
+    dZ = torch.full((P + 64, embed), 7.0, device="cuda", dtype=dt)      # guard rows must survive
+    dbias = torch.empty(embed, device="cuda"); dsc = torch.empty(1, device="cuda")
     _lib.check(_lib.lib().ebc_head_bwd(_lib.EBC_F32, _lib.dtype_code(dt), _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls),
                                        _lib.ptr(anchors), _lib.ptr(dl), _lib.ptr(de), None, _lib.ptr(dZ), _lib.ptr(dbias),
-                                       _lib.ptr(dsc), P, HW, NB, _lib.stream()), "head_bwd")
+                                       _lib.ptr(dsc), P, HW, NB, embed, _lib.stream()), "head_bwd")
     Zr = Z.double().requires_grad_(True)
     lsr = ls.double().requires_grad_(True)
     zn = torch.nn.functional.normalize(Zr, dim=-1)

@@ -1,0 +1,222 @@
+"""GPU parity of config 2 (clip_resnet50): the HIP Bottleneck decoder and the 1024-wide head.
+
+* `_BottleneckFn` (models/utils.py:306-363, expansion 1, after the x`up` bilinear adapt of
+  models/clip/model.py:195-196) against a float64 PyTorch restatement on the same device: output, every
+  gradient and the BatchNorm running statistics; fp32 within 1e-4, bf16 within 2e-2 (rel. L2).
+* the bench shape (8 crops of 448: M = 25088 rows x 2048 channels) with its tile configurations pinned.
+* the whole clip_resnet50 train step (fp32, no autocast) against the reference's own outputs (F7):
+  per-patch class logits within 1e-3 relative, argmax exact where the top-2 margin is clear; bf16 autocast
+  (config 2's dtype) within a mixed-precision tolerance of the same fixture.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import BINS, golden, rel_l2, rel_max
+
+pytestmark = pytest.mark.gpu
+ANCHORS_SHA = [0.0, 1.0, 2.0, 3.0, 4.29992]
+
+
+def _torch_bottleneck(feat_nchw, blk, up, eps=1e-5):
+    """Float64 restatement of the decoder (bilinear adapt + Bottleneck, training-mode BatchNorm)."""
+    x = F.interpolate(feat_nchw, scale_factor=up, mode="bilinear") if up != 1 else feat_nchw
+    ws = [p.detach().double().requires_grad_(True) for p in
+          (blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
+           blk.bn2.bias, blk.bn3.weight, blk.bn3.bias)]
+    w1, w2, w3, g1, b1, g2, b2, g3, b3 = ws
+
+    def bn(z, g, b):
+        m = z.mean((0, 2, 3), keepdim=True)
+        v = z.var((0, 2, 3), unbiased=False, keepdim=True)
+        return (z - m) / torch.sqrt(v + eps) * g.view(1, -1, 1, 1) + b.view(1, -1, 1, 1), m.flatten(), z.var((0, 2, 3)).flatten()
+
+    z1, m1, v1 = bn(F.conv2d(x, w1), g1, b1)
+    h = F.relu(z1)
+    z2, m2, v2 = bn(F.conv2d(h, w2, padding=1), g2, b2)
+    h = F.relu(z2)
+    z3, m3, v3 = bn(F.conv2d(h, w3), g3, b3)
+    return F.relu(z3 + x), ws, (m1, v1, m2, v2, m3, v3)
+
+
+def _block(C, seed, dev):
+    from ebc_amd.resnet import Bottleneck
+    torch.manual_seed(seed)
+    blk = Bottleneck(C, C, expansion=1)
+    with torch.no_grad():
+        for bn in (blk.bn1, blk.bn2, blk.bn3):
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+    return blk.to(dev).train()
+
+
+@pytest.mark.parametrize("dtype,B,h,C,up", [(torch.float32, 2, 7, 256, 2), (torch.float32, 3, 7, 256, 1),
+                                            (torch.bfloat16, 2, 7, 256, 2), (torch.float16, 2, 8, 512, 2)])
+def test_bottleneck_fn_matches_torch(dtype, B, h, C, up):
+    from ebc_amd.resnet import _BottleneckFn
+    dev = torch.device("cuda")
+    blk = _block(C, 3, dev)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    feat = torch.randn(B, h, h, C, device=dev, generator=g)
+    featp = feat.clone().requires_grad_(True)
+    params = [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
+              blk.bn2.bias, blk.bn3.weight, blk.bn3.bias]
+    y = _BottleneckFn.apply(featp, *params, blk, up, dtype, True)
+    gy = torch.randn(y.shape, device=dev, generator=g)
+    y.float().backward(gy)
+    torch.cuda.synchronize()
+    fr = feat.double().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    blk_r = _block(C, 3, dev)
+    yr, ws, stats = _torch_bottleneck(fr, blk_r, up)
+    yr.backward(gy.double().permute(0, 3, 1, 2))
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert rel_l2(y.float().permute(0, 3, 1, 2).cpu(), yr.detach().cpu()) < tol
+    assert rel_l2(featp.grad.permute(0, 3, 1, 2).cpu(), fr.grad.cpu()) < 2 * tol
+    names = ["conv1", "conv2", "conv3", "bn1.w", "bn1.b", "bn2.w", "bn2.b", "bn3.w", "bn3.b"]
+    for n, p, r in zip(names, params, ws):
+        assert p.grad is not None, n
+        assert rel_l2(p.grad.cpu(), r.grad.cpu()) < 3 * tol, n
+    # running statistics (momentum 0.1, unbiased variance), models/utils.py BatchNorm2d defaults
+    m1, v1, m2, v2, m3, v3 = stats
+    for bn, m, v in ((blk.bn1, m1, v1), (blk.bn2, m2, v2), (blk.bn3, m3, v3)):
+        assert rel_l2(bn.running_mean.cpu(), 0.1 * m.detach().cpu()) < tol * 10
+        assert rel_l2(bn.running_var.cpu(), 0.9 + 0.1 * v.detach().cpu()) < tol
+        assert int(bn.num_batches_tracked) == 1
+
+
+def test_bottleneck_eval_uses_running_stats():
+    from ebc_amd.resnet import _BottleneckFn
+    dev = torch.device("cuda")
+    blk = _block(256, 4, dev).eval()
+    with torch.no_grad():
+        for bn in (blk.bn1, blk.bn2, blk.bn3):
+            bn.running_mean.uniform_(-0.1, 0.1)
+            bn.running_var.uniform_(0.5, 2.0)
+    feat = torch.randn(2, 7, 7, 256, device=dev)
+    params = [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
+              blk.bn2.bias, blk.bn3.weight, blk.bn3.bias]
+    with torch.no_grad():
+        y = _BottleneckFn.apply(feat, *params, blk, 2, torch.float32, False)
+        x = F.interpolate(feat.permute(0, 3, 1, 2), scale_factor=2, mode="bilinear")
+        r = F.relu(blk.bn1(blk.conv1(x)))
+        r = F.relu(blk.bn2(blk.conv2(r)))
+        r = F.relu(blk.bn3(blk.conv3(r)) + x)
+    assert rel_l2(y.permute(0, 3, 1, 2).cpu(), r.cpu()) < 1e-4
+    assert int(blk.bn1.num_batches_tracked) == 0
+
+
+def test_bench_shape_tile_configs():
+    """The config-2 bench products (8 crops of 448: 25088 rows) run the 256x256 tiles."""
+    from ebc_amd import _lib
+    L = _lib.lib()
+    out = (ctypes.c_int * 3)()
+    bf = _lib.EBC_BF16
+    assert L.ebc_gemm_tile_config(bf, 25088, 2048, 2048, out) == 7          # conv1 / conv3 and their dX
+    assert L.ebc_gemm_tile_config(bf, 25088, 1024, 2048, out) == 7          # projection
+    assert L.ebc_gemm_tile_config(bf, 25088, 2048, 1024, out) == 7          # projection dX
+    assert L.ebc_conv_tile_config(bf, 1, 25088, 2048, 9 * 2048, out) == 7   # conv2 fwd / dgrad
+    assert L.ebc_conv_tile_config(bf, 2, 2048, 9 * 2048, 0, out) == 3       # conv2 wgrad
+
+
+def test_bottleneck_bench_shape_bf16():
+    """8 x 28 x 28 x 2048 -> 8 x 56 x 56 x 2048 in bf16 (the cfg-7 kernels) against the float64 restatement."""
+    from ebc_amd.resnet import _BottleneckFn
+    dev = torch.device("cuda")
+    blk = _block(2048, 6, dev)
+    g = torch.Generator(device="cuda").manual_seed(8)
+    feat = torch.randn(8, 28, 28, 2048, device=dev, generator=g)
+    featp = feat.clone().requires_grad_(True)
+    params = [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
+              blk.bn2.bias, blk.bn3.weight, blk.bn3.bias]
+    y = _BottleneckFn.apply(featp, *params, blk, 2, torch.bfloat16, True)
+    gy = torch.randn(y.shape, device=dev, generator=g)
+    y.float().backward(gy)
+    torch.cuda.synchronize()
+    blk_r = _block(2048, 6, dev)
+    # float32 restatement (f64 convolutions at this size are too slow on the GPU); TF32 off
+    fr = feat.permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    with torch.backends.cudnn.flags(enabled=True, allow_tf32=False):
+        x = F.interpolate(fr, scale_factor=2, mode="bilinear")
+        r = F.relu(blk_r.bn1(blk_r.conv1(x)))
+        r = F.relu(blk_r.bn2(blk_r.conv2(r)))
+        yr = F.relu(blk_r.bn3(blk_r.conv3(r)) + x)
+        yr.backward(gy.permute(0, 3, 1, 2))
+    assert rel_l2(y.float().permute(0, 3, 1, 2).cpu(), yr.detach().cpu()) < 2e-2
+    assert rel_l2(featp.grad.permute(0, 3, 1, 2).cpu(), fr.grad.cpu()) < 4e-2
+    for p, r in zip(params, [blk_r.conv1.weight, blk_r.conv2.weight, blk_r.conv3.weight, blk_r.bn1.weight,
+                             blk_r.bn1.bias, blk_r.bn2.weight, blk_r.bn2.bias, blk_r.bn3.weight, blk_r.bn3.bias]):
+        assert rel_l2(p.grad.cpu(), r.grad.cpu()) < 6e-2
+
+
+def _model():
+    from ebc_amd.model import get_model
+    d = golden("f7_resnet50.npz")
+    m = get_model("clip_resnet50", 448, 8, BINS, ANCHORS_SHA, prompt_type="word", weights_seed=0,
+                  text_features=torch.from_numpy(d["text_features"]))
+    return m.cuda(), d
+
+
+def _step(m, d, autocast=None):
+    from ebc_amd import synthetic as syn
+    from ebc_amd.losses import DACELoss
+    img, pts, dens = syn.synthetic_crops(2, int(d["size"]), seed=int(d["seed"]), counts=list(d["counts"]))
+    m.train()
+    m.zero_grad(set_to_none=True)
+    x = torch.from_numpy(img).cuda()
+    loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=int(d["size"]))
+    with torch.autocast("cuda", dtype=autocast or torch.float16, enabled=autocast is not None):
+        logits, exp = m(x)
+        loss, info = loss_fn(logits, exp, torch.from_numpy(dens).cuda(), [torch.from_numpy(p).cuda() for p in pts])
+    loss.backward()
+    torch.cuda.synchronize()
+    return x, logits.detach().float().cpu().numpy(), exp.detach().float().cpu().numpy(), \
+        {k: float(v) for k, v in info.items()}
+
+
+def test_resnet_train_step_fp32_matches_reference():
+    m, d = _model()
+    with torch.backends.cudnn.flags(enabled=True, allow_tf32=False):
+        x, logits, exp, info = _step(m, d)
+    per_patch = np.linalg.norm(logits - d["logits"], axis=1) / np.linalg.norm(d["logits"], axis=1)
+    print(f"clip_resnet50 per-patch logits rel err: max {per_patch.max():.2e} median {np.median(per_patch):.2e}")
+    assert per_patch.max() < 1e-3
+    top2 = np.sort(d["logits"], axis=1)[:, -2:]
+    sure = (top2[:, 1] - top2[:, 0]) > 1e-3 * np.abs(top2[:, 1]).clip(min=1.0)
+    assert (logits.argmax(1) == d["logits"].argmax(1))[sure].all()
+    assert rel_max(exp, d["exp"]) < 1e-3
+    for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
+        assert abs(info[k] - float(d["info_" + k])) <= 1e-3 * abs(float(d["info_" + k])), k
+    dec, enc = m.image_decoder[0], m.image_encoder
+    checks = {
+        "grad_proj_w_sub": m.projection.weight.grad[::5, ::7], "grad_proj_b": m.projection.bias.grad,
+        "grad_dec_conv1_sub": dec.conv1.weight.grad[::9, ::9], "grad_dec_conv2_sub": dec.conv2.weight.grad[::17, ::17],
+        "grad_dec_conv3_sub": dec.conv3.weight.grad[::9, ::9], "grad_dec_bn1_w": dec.bn1.weight.grad,
+        "grad_dec_bn2_b": dec.bn2.bias.grad, "grad_dec_bn3_w": dec.bn3.weight.grad, "grad_dec_bn3_b": dec.bn3.bias.grad,
+        "grad_enc_conv1": enc.conv1.weight.grad, "grad_enc_l4_conv3_sub": enc.layer4[2].conv3.weight.grad[::11, ::7],
+        "grad_enc_l1_bn1_w": enc.layer1[0].bn1.weight.grad,
+        "dec_bn2_running_mean": dec.bn2.running_mean, "dec_bn3_running_var": dec.bn3.running_var,
+    }
+    for k, v in checks.items():
+        e = rel_l2(v.detach().cpu().numpy(), d[k])
+        print(f"  {k}: rel L2 {e:.2e}")
+        assert e < 5e-3, k
+    assert abs(float(m.logit_scale.grad) - float(d["grad_logit_scale"])) < 1e-3 * abs(float(d["grad_logit_scale"]))
+    m.eval()
+    with torch.no_grad(), torch.backends.cudnn.flags(enabled=True, allow_tf32=False):
+        ev = m(x).cpu().numpy()
+    assert rel_max(ev, d["exp_eval"]) < 1e-3
+
+
+def test_resnet_train_step_bf16_vs_reference():
+    """Config 2's dtype: bf16 autocast over the MIOpen encoder and the HIP decoder/head."""
+    m, d = _model()
+    _, logits, exp, info = _step(m, d, autocast=torch.bfloat16)
+    e = rel_l2(logits, d["logits"])
+    print(f"clip_resnet50 bf16 logits rel L2 {e:.2e}, loss {info['loss']:.2f} vs {float(d['info_loss']):.2f}")
+    assert e < 6e-2
+    assert abs(info["loss"] - float(d["info_loss"])) <= 6e-2 * abs(float(d["info_loss"]))
+    for k, v in (("grad_proj_b", m.projection.bias.grad), ("grad_dec_bn3_b", m.image_decoder[0].bn3.bias.grad)):
+        assert rel_l2(v.detach().float().cpu().numpy(), d[k]) < 0.2, k

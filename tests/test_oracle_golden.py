@@ -172,3 +172,23 @@ def test_dace_loss_oracle_matches_reference_extra_geometry(tag):
             r = ref.ot_crop(p, d[f"{tag}_pred_density"][b, 0], size, red, norm_cood=norm)
             assert rel_max(r["beta"], d[f"{tag}_beta"][b]) < 1e-4, (tag, b)
             assert not r["rolled_back"] and int(d[f"{tag}_roll"][b]) == 0
+
+
+def test_resnet50_oracle_matches_reference():
+    """F7: the oracle's functional clip_resnet50 restatement (oracle/ref.py resnet_forward) against the
+    reference's own fp32 outputs on the same synthetic weights and crops."""
+    import torch
+    from ebc_amd import synthetic as syn
+    from oracle import ref
+    d = golden("f7_resnet50.npz")
+    p = ref.resnet_params_from_state(syn.resnet50_full_state(0, include_text=False))
+    img, pts, dens = syn.synthetic_crops(2, int(d["size"]), seed=int(d["seed"]), counts=list(d["counts"]))
+    logits, exp, feats = ref.resnet_forward(p, torch.from_numpy(img), torch.from_numpy(d["text_features"]),
+                                            [0.0, 1.0, 2.0, 3.0, 4.29992])
+    assert rel_l2(feats.detach().numpy()[:, ::7, ::3, ::3], d["enc_out_sub"]) < 1e-4
+    assert rel_l2(logits.detach().numpy(), d["logits"]) < 1e-4
+    loss, info = ref.dace_loss(logits, exp, torch.from_numpy(dens), pts, BINS, input_size=int(d["size"]))
+    assert abs(loss.item() - float(d["info_loss"])) < 1e-4 * abs(float(d["info_loss"]))
+    loss.backward()
+    assert rel_l2(p["image_decoder.0.conv3.weight"].grad.numpy()[::9, ::9], d["grad_dec_conv3_sub"]) < 1e-3
+    assert rel_l2(p["image_encoder.conv1.weight"].grad.numpy(), d["grad_enc_conv1"]) < 1e-3

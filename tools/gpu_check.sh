@@ -6,6 +6,9 @@
 # bench  the default bench.py line (in-step roofline probe + CPU baseline) -> gpurun_out/TAG_bench.json
 # prof   rocprofv3 --kernel-trace --stats of bench.py, cut to the timed steps (tools/kstats.py --window)
 # ddp    the 2-rank DDP + SyncBN bench path with both ranks on cuda:0 over gloo (a rehearsal, not a scaling number)
+# t:EXPR only the -m gpu tests whose names match EXPR (pytest -k)
+# rbench the clip_resnet50 bench line (configs[1]) -> gpurun_out/TAG_rbench.json
+# rprof  rocprofv3 --kernel-trace --stats of the clip_resnet50 bench, cut to the timed steps
 # Every GPU step has its own time limit and the steps are chained: the first failure ends the session.
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -37,6 +40,23 @@ for what in "$@"; do
       EBC_BENCH_ONE_DEVICE=1 EBC_BENCH_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 2 --steps 6 --warmup 3 \
         --no-probe > $O/${TAG}_ddp2.log 2>&1 || { tail -40 $O/${TAG}_ddp2.log; exit 1; }
       tail -1 $O/${TAG}_ddp2.log | cut -c1-400 ;;
+    t:*)
+      timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests -k "${what#t:}" \
+        > $O/${TAG}_tsel.log 2>&1 || { tail -60 $O/${TAG}_tsel.log; exit 1; }
+      tail -1 $O/${TAG}_tsel.log ;;
+    rbench)
+      timeout -k 10 600 python -u bench.py --model clip_resnet50 --steps 20 --warmup 5 > $O/${TAG}_rbench.log 2>&1 \
+        || { tail -30 $O/${TAG}_rbench.log; exit 1; }
+      tail -1 $O/${TAG}_rbench.log > $O/${TAG}_rbench.json; cut -c1-600 $O/${TAG}_rbench.json ;;
+    rprof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_rprof -o run -- \
+        python3 $R/bench.py --model clip_resnet50 --steps 10 --warmup 5 --no-cpu-baseline --no-probe > $O/${TAG}_rprof.log 2>&1) \
+        || { tail -30 $O/${TAG}_rprof.log; exit 1; }
+      db=$(find $O/${TAG}_rprof -name "*.db" | head -1)
+      python3 $R/tools/kstats.py "$db" --window --per 10 --top 45 --csv $O/${TAG}_rkstats.csv > $O/${TAG}_rkstats.txt \
+        || { echo "kstats failed"; exit 1; }
+      rm -rf $O/${TAG}_rprof
+      head -40 $O/${TAG}_rkstats.txt ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done
