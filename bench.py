@@ -512,7 +512,7 @@ def main():
             out["sinkhorn"] = sink
         if world == 1 and not args.no_cpu_baseline:
             if rn:
-                out["cpu_baseline"] = cpu_baseline_resnet(args, 2, 1)
+                out["cpu_baseline"] = cpu_baseline_resnet(args, 2, 5)
             else:
                 out["cpu_baseline"] = cpu_baseline(args, args.cpu_crops, args.cpu_steps)
         print(json.dumps(out), flush=True)

@@ -1048,11 +1048,13 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int e = t + 256 * k, cl = e >> 3, rl = (e & 7) * 8;
-        if (c0 + cl < C && r0 + rl < R) {
+        if (c0 + cl < C && r0 + rl + 8 <= R) {
             t8 v;
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[i] = sm[rl + i][cl];
             *reinterpret_cast<t8*>(out + (size_t)(c0 + cl) * ldo + r0 + rl) = v;
+        } else if (c0 + cl < C && r0 + rl < R) {          // ragged last rows (R not a multiple of 8)
+            for (int i = 0; r0 + rl + i < R; ++i) out[(size_t)(c0 + cl) * ldo + r0 + rl + i] = sm[rl + i][cl];
         }
     }
 }
@@ -1081,7 +1083,7 @@ extern "C" int ebc_gemm_wgrad(int dtype, const void* A, const void* B, float* C,
 
 extern "C" int ebc_transpose(int dtype, const void* in, void* out, int R, int C, long ld_out, ebc_stream_t stream)
 {
-    if (!in || !out || R <= 0 || C <= 0 || R % 8 || C % 8 || ld_out < R || ld_out % 8) return EBC_E_ARG;
+    if (!in || !out || R <= 0 || C <= 0 || C % 8 || ld_out < R || ld_out % 8) return EBC_E_ARG;
     const dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
     const hipStream_t st = (hipStream_t)stream;
     switch (dtype) {

@@ -115,8 +115,8 @@ int ebc_gemm_ws(int dtype, int epilogue, int out_f32, const void* A, const void*
 size_t ebc_gemm_wgrad_workspace_bytes(int dtype, int M, int N, int K);
 int ebc_gemm_wgrad(int dtype, const void* A, const void* B, float* C, int M, int N, int K,
                    void* workspace, size_t workspace_bytes, ebc_stream_t stream);
-/* out[c][r] = in[r][c] for in [R][C] (16-bit or f32 elements; R, C and the output row stride ld_out >= R
- * multiples of 8): the K-contiguous operand copies for ebc_gemm_wgrad. */
+/* out[c][r] = in[r][c] for in [R][C] (16-bit or f32 elements; C and the output row stride ld_out >= R
+ * multiples of 8, any R): the K-contiguous operand copies for ebc_gemm_wgrad. */
 int ebc_transpose(int dtype, const void* in, void* out, int R, int C, long ld_out, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------

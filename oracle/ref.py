@@ -203,7 +203,7 @@ def head(p, x, text_features, anchors):
     txt = F.normalize(text_features, p=2, dim=-1)
     logits = (p["logit_scale"].exp() * img @ txt.t()).permute(0, 3, 1, 2)
     probs = logits.softmax(dim=1)
-    exp = (probs * torch.as_tensor(anchors, dtype=probs.dtype).view(1, -1, 1, 1)).sum(dim=1, keepdim=True)
+    exp = (probs * torch.as_tensor(anchors, dtype=probs.dtype, device=probs.device).view(1, -1, 1, 1)).sum(dim=1, keepdim=True)
     return logits, exp
 
 

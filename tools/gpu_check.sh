@@ -41,7 +41,7 @@ for what in "$@"; do
         --no-probe > $O/${TAG}_ddp2.log 2>&1 || { tail -40 $O/${TAG}_ddp2.log; exit 1; }
       tail -1 $O/${TAG}_ddp2.log | cut -c1-400 ;;
     t:*)
-      timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests -k "${what#t:}" \
+      timeout -k 10 900 python -u -m pytest -x -v -s --tb=short --timeout 300 --timeout-method thread -m gpu tests -k "${what#t:}" \
         > $O/${TAG}_tsel.log 2>&1 || { tail -60 $O/${TAG}_tsel.log; exit 1; }
       tail -1 $O/${TAG}_tsel.log ;;
     rbench)
