@@ -694,11 +694,13 @@ def _clip_ebc(backbone: str, bins, anchor_points, reduction=None, freeze_text_en
 
 
 def get_model(backbone: str, input_size: int, reduction: int, bins: Optional[List[Tuple[float, float]]] = None,
-              anchor_points: Optional[List[float]] = None, **kwargs: Any) -> CLIP_EBC:
-    """models/__init__.py:10-44.  clip_vit_b_16 and clip_resnet50 are on the MI355X path."""
+              anchor_points: Optional[List[float]] = None, **kwargs: Any) -> nn.Module:
+    """models/__init__.py:10-44.  clip_vit_b_16 and clip_resnet50 are on the MI355X path; vgg19_ae (configs[0]) is
+    the reference's DM-Count VGG-19 encoder-decoder (ebc_amd/vgg.py)."""
     backbone = backbone.lower()
     if "clip" not in backbone:
-        raise NotImplementedError(f"{backbone}: only clip_vit_b_16 / clip_resnet50 are built for MI355X (SURVEY.md §8)")
+        from . import vgg                     # BASELINE configs[0]: vgg19_ae (models/model.py:94-111)
+        return vgg.build(backbone, input_size, reduction, bins, anchor_points, **kwargs)
     backbone = backbone[5:]
     assert bins is not None and anchor_points is not None, "CLIP-EBC needs bins and anchor_points"
     kwargs.setdefault("prompt_type", "number")

@@ -226,3 +226,33 @@ def point_map(points: np.ndarray, height: int, width: int) -> np.ndarray:
         y = np.clip(p[:, 1], 0, height - 1)
         m[y, x] = 1.0
     return m
+
+
+# ----------------------------------------------------------------------------- vgg19_ae (config 1)
+def vgg19_ae_state(seed: int = 0, n_bins=5) -> Dict[str, np.ndarray]:
+    """VGG-19 features (He-normal convs, small biases: the ImageNet weights are a download), the reg_layer and
+    the classifier (n_bins) / regressor (n_bins None) with the reference's `_init_weights` laws
+    (kaiming_normal fan_out, zero bias; models/utils.py:366-379)."""
+    from .vgg import VGG_CFG_E
+    sd: Dict[str, np.ndarray] = {}
+    idx, cin = 0, 3
+    for v in VGG_CFG_E:
+        if v == "M":
+            idx += 1
+            continue
+        k = f"backbone.features.{idx}"
+        sd[k + ".weight"] = _normal(seed, k + ".weight", (v, cin, 3, 3), math.sqrt(2.0 / (cin * 9)))
+        sd[k + ".bias"] = _normal(seed, k + ".bias", (v,), 0.01)
+        idx += 2
+        cin = v
+    for i, (co, ci) in ((0, (256, 512)), (2, (128, 256))):
+        k = f"backbone.reg_layer.{i}"
+        sd[k + ".weight"] = _normal(seed, k + ".weight", (co, ci, 3, 3), math.sqrt(2.0 / (co * 9)))
+        sd[k + ".bias"] = np.zeros(co, np.float32)
+    if n_bins is None:
+        sd["regressor.0.weight"] = _normal(seed, "regressor.0.weight", (1, 128, 1, 1), math.sqrt(2.0))
+        sd["regressor.0.bias"] = np.zeros(1, np.float32)
+    else:
+        sd["classifier.weight"] = _normal(seed, "classifier.weight", (n_bins, 128, 1, 1), math.sqrt(2.0 / n_bins))
+        sd["classifier.bias"] = np.zeros(n_bins, np.float32)
+    return sd

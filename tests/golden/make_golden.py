@@ -393,6 +393,45 @@ def resnet_case(ref, seed: int = 9, B: int = 2, size: int = 448, counts=(60, 3))
     return out
 
 
+def vgg_case(ref, seed: int = 11, B: int = 2, size: int = 448, counts=(25, 140)):
+    """F8: BASELINE configs[0] (vgg19_ae, 448 crops, reduction 8, SHA anchors, DMCount, batch 2 on the CPU):
+    the reference's own VGG (models/encoder_decoder/vgg.py:13-41, features = make_vgg_layers(cfg E)) under its
+    Classifier (models/model.py:37-75), on ebc_amd.synthetic.vgg19_ae_state(0) (the ImageNet weights are a
+    download)."""
+    _stub_pkg("models.encoder_decoder", f"{REF}/models/encoder_decoder")
+    enc = types.ModuleType("models.encoder")                       # timm-backed encoders: not needed here
+    enc._timm_encoder = None
+    sys.modules["models.encoder"] = enc
+    vgg = _load("models.encoder_decoder.vgg", f"{REF}/models/encoder_decoder/vgg.py")
+    mm = _load("models.model", f"{REF}/models/model.py")
+    mu = sys.modules["models.utils"]
+    torch.manual_seed(0)
+    m = mm.Classifier(vgg.VGG(mu.make_vgg_layers(mu.vgg_cfgs["E"]), reduction=8), BINS, ANCHORS_SHA)
+    sd = syn.vgg19_ae_state(0)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, strict=True)
+    img, points, density = syn.synthetic_crops(B, size, seed=seed, counts=list(counts))
+    x = torch.from_numpy(img)
+    m.train()
+    logits, exp = m(x)
+    loss_fn = ref.losses.DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=size)
+    loss, info = loss_fn(logits, exp, torch.from_numpy(density), [torch.from_numpy(p) for p in points])
+    loss.backward()
+    f = m.backbone.features
+    out = dict(seed=seed, counts=np.asarray(counts), size=size, logits=logits.detach().numpy(), exp=exp.detach().numpy(),
+               state_keys=np.asarray(sorted(m.state_dict().keys())),
+               grad_cls_w=m.classifier.weight.grad.numpy(), grad_cls_b=m.classifier.bias.grad.numpy(),
+               grad_reg0_sub=m.backbone.reg_layer[0].weight.grad.numpy()[::7, ::9],
+               grad_reg2_b=m.backbone.reg_layer[2].bias.grad.numpy(),
+               grad_f0_w=f[0].weight.grad.numpy(), grad_f34_sub=f[34].weight.grad.numpy()[::9, ::11],
+               grad_f34_b=f[34].bias.grad.numpy())
+    for k, v in info.items():
+        out["info_" + k] = v.detach().numpy().reshape(())
+    m.eval()
+    with torch.no_grad():
+        out["exp_eval"] = m(x).numpy()
+    return out
+
+
 def sliding_case(ref):
     """F5: sliding-window tiling + overlap averaging with a stub model (utils/eval_utils.py:26-96)."""
     class Stub(torch.nn.Module):
@@ -489,6 +528,8 @@ def main():
             save("f6b_tokens.npz", **tokenizer_case(ref))
         if "f7" in want:
             save("f7_resnet50.npz", **resnet_case(ref))
+        if "f8" in want:
+            save("f8_vgg19_ae.npz", **vgg_case(ref))
         return
     prompt_table(ref)
     bpe_merges()
@@ -505,6 +546,7 @@ def main():
     save("f4_e2e_l2.npz", **e2e_case(ref, layers=2))
     save("f3_e2e_l12.npz", **e2e_case(ref, layers=12))
     save("f7_resnet50.npz", **resnet_case(ref))
+    save("f8_vgg19_ae.npz", **vgg_case(ref))
 
 
 if __name__ == "__main__":
