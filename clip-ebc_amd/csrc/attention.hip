@@ -7,9 +7,12 @@
 // qkv[row] = [q(768) | k(768) | v(768)], head h at columns h*64 .. h*64+63.
 //
 // The sequence is short (1 CLS + 32 VPT + 196 patches = 229 tokens), so a workgroup keeps the
-// whole K and V (or Q and dO) of one (crop, head) in LDS, padded to LP = 256 rows with a
-// 144-byte row pitch (conflict-free for both ds_read_b128 row reads and ds_read_b64_tr_b16
-// column reads); scores for 16 query rows x 256 keys live in registers, so no online softmax.
+// whole K and V (or Q and dO) of one (crop, head) in LDS, padded to LP = 256 rows; scores for 16
+// query rows x 256 keys live in registers, so no online softmax.  16-bit rows are 128 B with their
+// eight 16-B chunks XOR-swizzled per row pair (chunk c of row r at c ^ SWZ[(r >> 1) & 7]): the
+// ds_read_b128 row fragments (lane groups {0-3,12-15,20-27}, ...) and the ds_read_b64_tr_b16 column
+// fragments (32-lane groups) both cover the 64 banks once per group (the former 144-B pitch left
+// 43-47 % of the LDS cycles as bank conflicts, PMC r02); f32 (parity mode) keeps a padded pitch.
 // Operand orientation ("swapped" S^T = K Q^T) puts each query on one lane, so the probability
 // accumulators are directly the A operand of P.V with no LDS round trip (mfma.h).
 //   grid: B * H * ceil(L/(16 NW)) workgroups of NW waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
@@ -33,10 +36,24 @@ constexpr float LOG2E = 1.4426950408889634f;
 template <class E> struct AttnCfg {
     using T = typename E::T;
     static constexpr int EB = E::BYTES;
-    static constexpr int LDR = HD + 16 / EB;                 // row pitch in elements (144 B / 272 B)
+    static constexpr bool SW = EB == 2;                      // 16-bit: swizzled 128-B rows
+    static constexpr int LDR = SW ? HD : HD + 16 / EB;       // row pitch in elements (128 B / 272 B)
     static constexpr int CPR = HD * EB / 16;                 // 16-B chunks per row
     static constexpr size_t TILE_BYTES = (size_t)LP * LDR * EB;
 };
+
+// chunk swizzle of row r (16-bit tiles): a permutation f of 0..7 indexed by the row pair, chosen so that
+// {f(0),f(1),f(6),f(7)} and {f(2..5)} ^ 1 are disjoint (row fragments) and f(0..3), f(4..7) each take one
+// value from every pair {2k, 2k+1} (transposed column fragments)
+__device__ __forceinline__ int attn_swz(int r) { return (0x71534260u >> (4 * ((r >> 1) & 7))) & 7; }
+
+// element offset of (row, col) in an LDS tile; col a multiple of 4 (16-bit) so a fragment piece stays in its chunk
+template <class E>
+__device__ __forceinline__ int attn_off(int row, int col) {
+    using C = AttnCfg<E>;
+    if constexpr (C::SW) return row * C::LDR + ((((col >> 3) ^ attn_swz(row)) << 3) | (col & 7));
+    else return row * C::LDR + col;
+}
 
 template <class E, int NWV>
 __device__ __forceinline__ void load_rows(typename E::T* dst, const typename E::T* src, int ld, int L)
@@ -55,7 +72,27 @@ __device__ __forceinline__ void load_rows(typename E::T* dst, const typename E::
     for (int k = 0; k < PER; ++k) {
         const int e = threadIdx.x + k * 64 * NWV;
         const int s = e / C::CPR, c = e % C::CPR;
-        *reinterpret_cast<uint4*>(dst + s * C::LDR + c * (16 / C::EB)) = v[k];
+        *reinterpret_cast<uint4*>(dst + attn_off<E>(s, c * (16 / C::EB))) = v[k];
+    }
+}
+
+// B-operand column fragment of rows r0 .. r0+31, columns n0 .. n0+15 (mfma.h load_colfrag on the
+// swizzled 16-bit tiles: each lane's 8-B ds_read_b64_tr_b16 piece stays inside one 16-B chunk)
+template <class E>
+__device__ __forceinline__ typename E::Frag attn_colfrag(const typename E::T* lds, int r0, int n0) {
+    using C = AttnCfg<E>;
+    if constexpr (!C::SW) {
+        return load_colfrag<E>(lds, C::LDR, r0, n0);
+    } else {
+        const int l = threadIdx.x & 63, g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
+        const int r = r0 + 4 * g + q;
+        const typename E::T* a0 = lds + attn_off<E>(r, n0 + 4 * p);
+        const typename E::T* a1 = lds + attn_off<E>(r + 16, n0 + 4 * p);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(typename E::Frag, v);
     }
 }
 
@@ -71,7 +108,7 @@ __device__ __forceinline__ typename E::Frag gload8(const typename E::T* p, bool 
 
 template <class E>
 __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* base, int row, int col) {
-    return load8<E>(base + row * AttnCfg<E>::LDR + col);
+    return load8<E>(base + attn_off<E>(row, col));
 }
 
 // ------------------------------------------------------------------------------ forward
@@ -154,7 +191,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
                              s[2 * st + 1][0], s[2 * st + 1][1], s[2 * st + 1][2], s[2 * st + 1][3]};
         const typename E::Frag pf = pack8<E>(pv);
 #pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) o[dt] = mma(pf, load_colfrag<E>(Vs, C::LDR, 32 * st, 16 * dt), o[dt]);
+        for (int dt = 0; dt < HD / 16; ++dt) o[dt] = mma(pf, attn_colfrag<E>(Vs, 32 * st, 16 * dt), o[dt]);
     }
     // o[dt][i] = O[q = q0 + 4 fg + i][d = 16 dt + fr]; divide by the row sum held on lane (q - q0)
     const float inv = 1.0f / sum;
@@ -258,7 +295,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
         }
         const typename E::Frag dsf = pack8<E>(ds);
 #pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, load_colfrag<E>(Ks, C::LDR, 32 * st, 16 * dt), dq_acc[dt]);
+        for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, attn_colfrag<E>(Ks, 32 * st, 16 * dt), dq_acc[dt]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -342,8 +379,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
         const typename E::Frag pf = pack8<E>(pp), dsf = pack8<E>(ds);
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) {
-            dv[dt] = mma(pf, load_colfrag<E>(Ds, C::LDR, 32 * st, 16 * dt), dv[dt]);
-            dk[dt] = mma(dsf, load_colfrag<E>(Qs, C::LDR, 32 * st, 16 * dt), dk[dt]);
+            dv[dt] = mma(pf, attn_colfrag<E>(Ds, 32 * st, 16 * dt), dv[dt]);
+            dk[dt] = mma(dsf, attn_colfrag<E>(Qs, 32 * st, 16 * dt), dk[dt]);
         }
             }
 #pragma unroll

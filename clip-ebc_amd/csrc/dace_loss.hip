@@ -40,7 +40,10 @@ constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
 
+// G = the LDS grid (a multiple of 4 >= the crop's density grid g = size / reduction); cells with a row or
+// column >= g are dead: zero density, zero kernel factors, v = 0, never written out.
 template <int G> struct Cfg {
+    static_assert(G % 4 == 0, "LDS grid");
     static constexpr int GG = G * G;
     // K^T u: 4x4 cell blocks, the points split over KSPLIT thread groups whose partial sums live
     // in LDS (KSPLIT x GG) and are summed by the consumer (no atomics: LDS float atomics run at
@@ -59,7 +62,7 @@ template <int G> struct Cfg {
     // G - 12): a <= 9-cell window starting at offset <= 3 fits, and a 4x4 block of any bucket that
     // gathers the point lies at offset 0, 4 or 8.  It needs only GG of the partials, so its factors
     // start at part + GG.
-    static constexpr int CW = 12;
+    static constexpr int CW = G < 12 ? G : 12;
     static constexpr int PER_POINT_C = 2 * CW + 6;
     static constexpr size_t FIXED_BYTES_C = (size_t)(5 * GG + 64 + BKT + GG) * 4;
 };
@@ -77,6 +80,7 @@ struct Params {
     const float* points; const int* offsets; const int* order;
     const float* bins_lo; const float* bins_hi;
     int B, N, size, red, count_mode, norm_cood;
+    int g;                 // density grid size / red (<= the kernel's LDS grid G)
     float w_count, w_ot, w_tv, reg, stop_thr;
     int max_iter, eval_freq;
     float* grad_class; float* grad_density; float* crop_stats; float* beta_out; int* status;
@@ -127,7 +131,7 @@ __device__ __forceinline__ float sum8_dpp(float x) {
 }
 
 template <int G, typename FP, typename IP>
-__device__ void sinkhorn_crop(int n, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
+__device__ void sinkhorn_crop(int n, int g, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                               const float* __restrict__ pts, FP Ey, FP Ex, FP u0, FP u1, IP win,
                               const float* b, float* v0, float* v1, float* part, float* misc,
                               int* iters_out, int* rolled_out, float* err_last_out, unsigned long long* pr)
@@ -147,11 +151,11 @@ __device__ void sinkhorn_crop(int n, int size, int red, int norm, float reg, int
         const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
         const float yd = (-2.0f * (y * c) + y * y) + c * c;
         const float xd = (-2.0f * (x * c) + x * x) + c * c;
-        Ey[e] = expf(yd / -reg);
-        Ex[e] = expf(xd / -reg);
+        Ey[e] = k < g ? expf(yd / -reg) : 0.f;               // dead rows / columns of the LDS grid
+        Ex[e] = k < g ? expf(xd / -reg) : 0.f;
     }
     for (int i = t; i < n; i += NT) u0[i] = 1.0f / (float)n;
-    for (int j = t; j < GG; j += NT) v0[j] = 1.0f / (float)GG;
+    for (int j = t; j < GG; j += NT) v0[j] = (j / G < g && j % G < g) ? 1.0f / (float)(g * g) : 0.f;   // ones(M)/M
     __syncthreads();
     // nonzero windows (exp of a convex quadratic: the nonzeros are contiguous)
     int wy_max = 0;
@@ -318,7 +322,7 @@ __device__ __forceinline__ float sum4_dpp(float x) {
 // Returns false (nothing iterated) when a window is wider than 9 cells; the caller then runs
 // sinkhorn_crop.  On return the factors, u (u0), windows and point coordinates (spts) are sorted.
 template <int G, int CW>
-__device__ bool sinkhorn_sorted(int n, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
+__device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                                 const float* __restrict__ pts, float* Ey, float* Ex, float* u0, float* u1, int* win,
                                 int* key, float* spts, int* bk, const float* b, float* v0, float* v1, float* part,
                                 float* misc, int* iters_out, int* rolled_out, float* err_last_out,
@@ -341,7 +345,7 @@ __device__ bool sinkhorn_sorted(int n, int size, int red, int norm, float reg, i
     for (int i = t; i < n; i += NT) {
         const float x = pcoord(pts[2 * i], size, norm), y = pcoord(pts[2 * i + 1], size, norm);
         int ylo = G, yhi = -1, xlo = G, xhi = -1;
-        for (int k = 0; k < G; ++k) {
+        for (int k = 0; k < g; ++k) {
             const float c = cood(k, size, red, norm);
             const float yd = (-2.0f * (y * c) + y * y) + c * c;
             const float xd = (-2.0f * (x * c) + x * x) + c * c;
@@ -376,8 +380,8 @@ __device__ bool sinkhorn_sorted(int n, int size, int red, int norm, float reg, i
             const float cy = cood(yb + k, size, red, norm), cx = cood(xb + k, size, red, norm);
             const float yd = (-2.0f * (y * cy) + y * y) + cy * cy;
             const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
-            Ey[slot * CW + k] = expf(yd / -reg);
-            Ex[slot * CW + k] = expf(xd / -reg);
+            Ey[slot * CW + k] = yb + k < g ? expf(yd / -reg) : 0.f;
+            Ex[slot * CW + k] = xb + k < g ? expf(xd / -reg) : 0.f;
         }
         spts[2 * slot] = px;
         spts[2 * slot + 1] = py;
@@ -385,7 +389,7 @@ __device__ bool sinkhorn_sorted(int n, int size, int red, int norm, float reg, i
     }
     __syncthreads();
     for (int i = t; i < n; i += NT) u0[i] = 1.0f / (float)n;
-    for (int j = t; j < GG; j += NT) v0[j] = 1.0f / (float)GG;
+    for (int j = t; j < GG; j += NT) v0[j] = (j / G < g && j % G < g) ? 1.0f / (float)(g * g) : 0.f;
     const float a = 1.0f / (float)n;
 
     // candidate ranges of block blk: home rows BY-HALO..BY, columns BX-HALO..BX (contiguous per row)
@@ -533,22 +537,24 @@ __device__ bool sinkhorn_sorted(int n, int size, int red, int norm, float reg, i
                 const int w = win[i];
                 const int ylo = w & 255, ylen = (w >> 8) & 255, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
                 if (xlen) {
-                    const int x4 = min(xlo & ~3, G - 12);
+                    // KW cells from the window's 4-aligned start (12: a <= 9-cell window at offset <= 3; the
+                    // whole row on grids narrower than 12)
+                    constexpr int KW = G < 12 ? G : 12;
+                    const int x4 = min(xlo & ~3, G - KW);
                     const float* exr = Ex + i * CW + x4 - row_base<G, CW>(xlo, xlen);
                     const float* eyr = Ey + i * CW + ylo - row_base<G, CW>(ylo, ylen);
-                    const float4 e0 = *reinterpret_cast<const float4*>(exr);
-                    const float4 e1 = *reinterpret_cast<const float4*>(exr + 4);
-                    const float4 e2 = *reinterpret_cast<const float4*>(exr + 8);
+                    float4 e[KW / 4];
+#pragma unroll
+                    for (int c = 0; c < KW / 4; ++c) e[c] = *reinterpret_cast<const float4*>(exr + 4 * c);
                     for (int r = q; r < ylen; r += 4) {
                         const float* vr = vn + (ylo + r) * G + x4;
-                        const float4 a0 = *reinterpret_cast<const float4*>(vr);
-                        const float4 a1 = *reinterpret_cast<const float4*>(vr + 4);
-                        const float4 a2 = *reinterpret_cast<const float4*>(vr + 8);
-                        float sum = e0.x * a0.x;
-                        sum = fmaf(e0.y, a0.y, sum); sum = fmaf(e0.z, a0.z, sum); sum = fmaf(e0.w, a0.w, sum);
-                        sum = fmaf(e1.x, a1.x, sum); sum = fmaf(e1.y, a1.y, sum); sum = fmaf(e1.z, a1.z, sum);
-                        sum = fmaf(e1.w, a1.w, sum); sum = fmaf(e2.x, a2.x, sum); sum = fmaf(e2.y, a2.y, sum);
-                        sum = fmaf(e2.z, a2.z, sum); sum = fmaf(e2.w, a2.w, sum);
+                        float sum = 0.f;
+#pragma unroll
+                        for (int c = 0; c < KW / 4; ++c) {
+                            const float4 a4 = *reinterpret_cast<const float4*>(vr + 4 * c);
+                            sum = fmaf(e[c].x, a4.x, sum); sum = fmaf(e[c].y, a4.y, sum);
+                            sum = fmaf(e[c].z, a4.z, sum); sum = fmaf(e[c].w, a4.w, sum);
+                        }
                         acc = fmaf(eyr[r], sum, acc);
                     }
                 }
@@ -631,6 +637,9 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     using C = Cfg<G>;
     const int t = threadIdx.x;
     const int GG = C::GG, S = P.size;
+    const int g = P.g, gg = g * g;                            // live cells: LDS j = y*G + x with y, x < g
+    auto live = [&](int j) { return j / G < g && j % G < g; };
+    auto gidx = [&](int j) { return (j / G) * g + j % G; };   // LDS cell -> index in the [g][g] global maps
     float* pd = lds;            // pred density
     float* td = pd + GG;        // target block sums
     float* bb = td + GG;        // normed pred density (Sinkhorn b)
@@ -646,10 +655,10 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     if (P.prof && t == 0) { for (int k = 0; k < 16; ++k) P.prof[b * 16 + k] = 0; P.prof[b * 16 + 6] = clock64(); P.prof[b * 16 + 5] = n; }
 
     // 1. pred density, target block sums (losses/utils.py:4-9)
-    for (int j = t; j < GG; j += NT) { pd[j] = P.pred_density[(size_t)b * GG + j]; td[j] = 0.f; }
+    for (int j = t; j < GG; j += NT) { pd[j] = live(j) ? P.pred_density[(size_t)b * gg + gidx(j)] : 0.f; td[j] = 0.f; }
     __syncthreads();
     if (P.target_is_reduced) {
-        for (int j = t; j < GG; j += NT) td[j] = P.target_density[(size_t)b * GG + j];
+        for (int j = t; j < GG; j += NT) td[j] = live(j) ? P.target_density[(size_t)b * gg + gidx(j)] : 0.f;
     } else {
         const float4* src = reinterpret_cast<const float4*>(P.target_density + (size_t)b * S * S);
         const int q4 = S / 4;
@@ -667,21 +676,21 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     // 2. cross-entropy over bins (dace_loss.py:42-55), grad = (softmax - onehot) / B
     const float invB = 1.0f / (float)P.B;
     float ce = 0.f;
-    for (int j = t; j < GG; j += NT) {
-        const float dv = td[j];
+    for (int j = t; j < gg; j += NT) {                        // j: global cell index
+        const float dv = td[(j / g) * G + j % g];
         int cls = 0;
         for (int k = 0; k < P.N; ++k)
             if (dv >= P.bins_lo[k] && dv <= P.bins_hi[k]) cls = k;
-        const float* lg = P.pred_class + (size_t)b * P.N * GG + j;
+        const float* lg = P.pred_class + (size_t)b * P.N * gg + j;
         float mx = -INFINITY;
-        for (int k = 0; k < P.N; ++k) mx = fmaxf(mx, lg[(size_t)k * GG]);
+        for (int k = 0; k < P.N; ++k) mx = fmaxf(mx, lg[(size_t)k * gg]);
         float se = 0.f;
-        for (int k = 0; k < P.N; ++k) se += expf(lg[(size_t)k * GG] - mx);
+        for (int k = 0; k < P.N; ++k) se += expf(lg[(size_t)k * gg] - mx);
         const float lse = mx + logf(se);
-        ce += lse - lg[(size_t)cls * GG];
-        float* gc = P.grad_class + (size_t)b * P.N * GG + j;
+        ce += lse - lg[(size_t)cls * gg];
+        float* gc = P.grad_class + (size_t)b * P.N * gg + j;
         for (int k = 0; k < P.N; ++k)
-            gc[(size_t)k * GG] = (expf(lg[(size_t)k * GG] - lse) - (k == cls ? 1.f : 0.f)) * invB;
+            gc[(size_t)k * gg] = (expf(lg[(size_t)k * gg] - lse) - (k == cls ? 1.f : 0.f)) * invB;
     }
     ce = block_sum(ce, misc);
 
@@ -692,10 +701,11 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         // count_loss "mae" / "mse": per-pixel, summed over HW, mean over B (dace_loss.py:57-62)
         float s = 0.f;
         for (int j = t; j < GG; j += NT) {
+            if (!live(j)) continue;
             const float d = pd[j] - td[j];
             s += (P.count_mode == EBC_COUNT_MAE) ? fabsf(d) : d * d;
-            const float g = (P.count_mode == EBC_COUNT_MAE) ? sgnf(d) : 2.f * d;
-            P.grad_density[(size_t)b * GG + j] = P.w_count * g * invB;
+            const float gd = (P.count_mode == EBC_COUNT_MAE) ? sgnf(d) : 2.f * d;
+            P.grad_density[(size_t)b * gg + gidx(j)] = P.w_count * gd * invB;
         }
         cnt_b = block_sum(s, misc);
     } else {
@@ -730,7 +740,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                     const float be = P.reg * logf(v0[j] + M_EPS);
                     v1[j] = be;
                     sb += pd[j] * be;
-                    if (P.beta_out) P.beta_out[(size_t)b * GG + j] = be;
+                    if (P.beta_out && live(j)) P.beta_out[(size_t)b * gg + gidx(j)] = be;
                 }
                 sb = block_sum(sb, misc);
                 const float den = pc * pc + EPS;
@@ -748,7 +758,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
             auto dense = [&](float* base, auto /*in_lds: one instantiation per address space*/) {
                 float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
                 int* win = reinterpret_cast<int*>(u1 + n);
-                sinkhorn_crop<G>(n, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
+                sinkhorn_crop<G>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
                                  u1, win, bb, v0, v1, part, misc, &iters, &rolled, &err_last,
                                  P.prof ? P.prof + b * 16 : nullptr);
                 post(std::integral_constant<int, G>{}, Ey, Ex, u0, win, pts);
@@ -761,7 +771,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                 int* win = reinterpret_cast<int*>(u1 + n);
                 int* key = win + n;
                 float* spts = reinterpret_cast<float*>(key + n);
-                if (!sinkhorn_sorted<G, CW>(n, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
+                if (!sinkhorn_sorted<G, CW>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
                                             Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc, &iters,
                                             &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr))
                     return false;
@@ -778,16 +788,17 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         } else {
             for (int j = t; j < GG; j += NT) {
                 v1[j] = 0.f;
-                if (P.beta_out) P.beta_out[(size_t)b * GG + j] = 0.f;   // no OT for an empty crop (dm_loss.py:49)
+                if (P.beta_out && live(j)) P.beta_out[(size_t)b * gg + gidx(j)] = 0.f;   // no OT for an empty crop (dm_loss.py:49)
             }
             __syncthreads();
         }
         // 5. d loss / d pred_density = w_count * (w_ot * ot_grad + w_tv * tv_grad + count_grad)
         const float ktv = tc * invB;
         for (int j = t; j < GG; j += NT) {
+            if (!live(j)) continue;
             const float d = pd[j] * inv_pc - td[j] * inv_tc;
             const float gtv = ktv * (sgnf(d) * inv_pc - tvk * inv_pc * inv_pc);
-            P.grad_density[(size_t)b * GG + j] = P.w_count * (P.w_ot * v1[j] + wtv * gtv + gcount);
+            P.grad_density[(size_t)b * gg + gidx(j)] = P.w_count * (P.w_ot * v1[j] + wtv * gtv + gcount);
         }
     }
     if (P.prof && t == 0) { P.prof[b * 16 + 7] = clock64(); P.prof[b * 16 + 4] = iters; }
@@ -872,10 +883,18 @@ template <int G> int launch(const Params& P0, hipStream_t st)
 
 }  // namespace
 
+// the LDS grid a density grid g runs on (dead cells pad it to an instantiated size), 0 = unsupported
+static int lds_grid(int g)
+{
+    static const int grids[] = {8, 16, 24, 28, 32, 40, 48, 56, 64};
+    for (int G : grids) if (g <= G) return G;
+    return 0;
+}
+
 extern "C" size_t ebc_dace_workspace_bytes(int B, int total_points, int size, int reduction)
 {
-    const int g = size / reduction;
-    return sizeof(float) * ((size_t)(2 * g + 6) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
+    const int G = reduction > 0 ? lds_grid(size / reduction) : 0;
+    return sizeof(float) * ((size_t)(2 * (G ? G : 64) + 6) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
 }
 
 extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,
@@ -905,11 +924,22 @@ extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density,
     P.reg = reg; P.stop_thr = stop_thr; P.max_iter = max_iter; P.eval_freq = eval_freq;
     P.grad_class = grad_class; P.grad_density = grad_density; P.crop_stats = crop_stats;
     P.beta_out = beta_out; P.status = status; P.ws_factors = (float*)workspace;
-    P.total_points = (int)((workspace_bytes - 256) / (sizeof(float) * (2 * (size_t)g + 6)));
+    const int G = lds_grid(g);
+    if (g <= 0 || !G) return EBC_E_UNSUPPORTED;                 // density grids up to 64 x 64 (LDS-resident state)
+    P.g = g;
+    P.total_points = (int)((workspace_bytes - 256) / (sizeof(float) * (2 * (size_t)G + 6)));
     int rc;
-    if (g == 28) rc = launch<28>(P, st);
-    else if (g == 56) rc = launch<56>(P, st);
-    else return EBC_E_UNSUPPORTED;
+    switch (G) {
+        case 8: rc = launch<8>(P, st); break;
+        case 16: rc = launch<16>(P, st); break;
+        case 24: rc = launch<24>(P, st); break;
+        case 28: rc = launch<28>(P, st); break;
+        case 32: rc = launch<32>(P, st); break;
+        case 40: rc = launch<40>(P, st); break;
+        case 48: rc = launch<48>(P, st); break;
+        case 56: rc = launch<56>(P, st); break;
+        default: rc = launch<64>(P, st); break;
+    }
     if (rc) return rc;
     hipLaunchKernelGGL(dace_finalize_kernel, dim3(1), dim3(256), 0, st, crop_stats, B, count_mode,
                        weight_count_loss, weight_ot, weight_tv, losses);

@@ -31,17 +31,17 @@ from torch import Tensor, nn
 from . import _lib
 
 _INFO_DM = ("loss", "ot_loss", "tv_loss", "count_loss", "ce_loss")
-_GRIDS = (28, 56)
+MAX_GRID = 64       # density grids g = input_size / reduction up to 64 x 64 (the kernel's LDS-resident state)
 M_EPS = 1e-16      # bregman_pytorch.py:8
 
 
 def _check_geometry(input_size: int, reduction: int) -> None:
     assert input_size % reduction == 0, f"input_size {input_size} is not a multiple of reduction {reduction}"
     g = input_size // reduction
-    if g not in _GRIDS or reduction % 4:
+    if g > MAX_GRID or reduction % 4:
         raise NotImplementedError(
             f"ebc_amd DMCount kernel: density grid input_size/reduction = {g} (reduction {reduction}); "
-            f"built for grids {_GRIDS} with reduction % 4 == 0 (224/448 crops at reduction 8, 448 at 16)")
+            f"built for grids up to {MAX_GRID} with reduction % 4 == 0")
 
 
 class _Internals:
@@ -169,8 +169,8 @@ class DACELoss(nn.Module):
         assert pred_density.shape == (B, 1, h, w), f"Expected pred_density [B,1,H,W], got {pred_density.shape}"
         assert h == w, "square crops only"
         assert len(target_points) == B, f"Expected target_points to have length {B}, but got {len(target_points)}"
-        if h not in _GRIDS:
-            raise NotImplementedError(f"ebc_amd DACE kernel: density grid {h}x{w}; built for {_GRIDS}")
+        if h != w or h > MAX_GRID:
+            raise NotImplementedError(f"ebc_amd DACE kernel: density grid {h}x{w}; built for square grids up to {MAX_GRID}")
         reduced = tuple(target_density.shape[-2:]) == (h, w)
         size = h * self.reduction
         if not reduced:

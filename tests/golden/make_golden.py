@@ -125,21 +125,22 @@ def pack_points(points):
     return flat, offs
 
 
-def loss_case(ref, size: int, counts, seed: int):
-    """F1: DACE(dmcount) loss + Sinkhorn internals on a ragged crop batch."""
+def loss_case(ref, size: int, counts, seed: int, reduction: int = 8, p_limit: int = 200 * 784):
+    """F1: DACE(dmcount) loss + Sinkhorn internals on a ragged crop batch (any input_size % reduction == 0;
+    transport plans P kept for crops with n * g^2 <= p_limit)."""
     g = np.random.Generator(np.random.PCG64(seed))
     B = len(counts)
-    h = size // 8
+    h = size // reduction
     points = [(g.random((n, 2)) * size).astype(np.float32) for n in counts]
     density = np.stack([syn.point_map(p, size, size)[None] for p in points])
     pred_class = g.standard_normal((B, 5, h, h)).astype(np.float32)
     pred_density = (g.random((B, 1, h, h)) * 1.5).astype(np.float32)
     pc = torch.tensor(pred_class, requires_grad=True)
     pd = torch.tensor(pred_density, requires_grad=True)
-    loss_fn = ref.losses.DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=size)
+    loss_fn = ref.losses.DACELoss(BINS, reduction, weight_count_loss=1.0, count_loss="dmcount", input_size=size)
     loss, info = loss_fn(pc, pd, torch.from_numpy(density), [torch.from_numpy(p) for p in points])
     loss.backward()
-    out = dict(size=size, counts=np.asarray(counts), pred_class=pred_class, pred_density=pred_density,
+    out = dict(size=size, reduction=reduction, counts=np.asarray(counts), pred_class=pred_class, pred_density=pred_density,
                grad_pred_class=pc.grad.numpy(), grad_pred_density=pd.grad.numpy())
     flat, offs = pack_points(points)
     out["points"], out["offsets"] = flat, offs
@@ -169,11 +170,22 @@ def loss_case(ref, size: int, counts, seed: int):
         sd = pdt[b][0].view(-1); sc = sd.sum()
         grad = sc / (sc * sc + 1e-8) * log["beta"] - (sd * log["beta"]).sum() / (sc * sc + 1e-8)
         grads.append(grad.numpy()); wds.append(float(torch.sum(dist * P)))
-        if len(p) <= 200:
+        if len(p) * h * h <= p_limit:
             out[f"P_{b}"] = P.numpy()
     out.update(beta=np.stack(betas), v=np.stack(vs), err=np.stack(errs), ot_grad=np.stack(grads), wd=np.asarray(wds))
     out["u_flat"] = np.concatenate(us) if us else np.zeros(0, np.float32)
     return out
+
+
+LOSS_GRIDS = [(224, 16, [0, 5, 40, 300, 2], 303), (224, 32, [17, 0, 120], 304), (448, 16, [60, 1, 800], 305),
+              (448, 32, [9, 250], 306), (384, 8, [33, 0, 500, 4], 307), (512, 8, [70, 3], 308)]
+
+
+def loss_grids(ref):
+    """F1g: the loss at the other geometries the reference allows (reduction 16 / 32, other crop sizes):
+    density grids 14, 7, 28, 14, 48 and 64."""
+    for size, red, counts, seed in LOSS_GRIDS:
+        save(f"f1g_loss_{size}_r{red}.npz", **loss_case(ref, size, counts, seed, reduction=red, p_limit=40000))
 
 
 def _capture_sinkhorn(ref):
@@ -530,6 +542,8 @@ def main():
             save("f7_resnet50.npz", **resnet_case(ref))
         if "f8" in want:
             save("f8_vgg19_ae.npz", **vgg_case(ref))
+        if "f1g" in want:
+            loss_grids(ref)
         return
     prompt_table(ref)
     bpe_merges()
@@ -547,6 +561,7 @@ def main():
     save("f3_e2e_l12.npz", **e2e_case(ref, layers=12))
     save("f7_resnet50.npz", **resnet_case(ref))
     save("f8_vgg19_ae.npz", **vgg_case(ref))
+    loss_grids(ref)
 
 
 if __name__ == "__main__":

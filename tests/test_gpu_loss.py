@@ -10,28 +10,35 @@ from ebc_amd import synthetic as syn
 pytestmark = pytest.mark.gpu
 
 
-def _run(pred_class, pred_density, target_density, points, size, count_loss="dmcount", reduced=False):
+def _run(pred_class, pred_density, target_density, points, size, count_loss="dmcount", reduced=False, red=8):
     from ebc_amd.losses import DACELoss
     dev = torch.device("cuda:0")
-    fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss=count_loss, input_size=size)
+    fn = DACELoss(BINS, red, weight_count_loss=1.0, count_loss=count_loss, input_size=size)
     pc = torch.tensor(pred_class, device=dev, requires_grad=True)
     pd = torch.tensor(pred_density, device=dev, requires_grad=True)
     td = torch.from_numpy(target_density).to(dev)
     if reduced:
-        td = ref.reshape_density(td, 8)
+        td = ref.reshape_density(td, red)
     loss, info = fn(pc, pd, td, [torch.from_numpy(p).to(dev) for p in points])
     loss.backward()
     torch.cuda.synchronize()
     return float(loss), {k: float(v) for k, v in info.items()}, pc.grad.cpu().numpy(), pd.grad.cpu().numpy()
 
 
-@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"])
+F1G = ["f1g_loss_224_r16.npz", "f1g_loss_224_r32.npz", "f1g_loss_448_r16.npz", "f1g_loss_448_r32.npz",
+       "f1g_loss_384_r8.npz", "f1g_loss_512_r8.npz"]
+
+
+@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"] + F1G)
 def test_dace_kernel_matches_reference_fixture(fixture):
+    """Every density grid the reference allows up to 64 (reduction 8 / 16 / 32; grids 7, 14, 28, 48, 56, 64 run
+    on padded LDS grids 8 / 16 / 28 / 48 / 56 / 64 with dead cells)."""
     d = golden(fixture)
     size = int(d["size"])
+    red = int(d["reduction"]) if "reduction" in d.files else 8
     pts = split_points(d)
     dens = np.stack([syn.point_map(p, size, size)[None] for p in pts])
-    loss, info, gc, gd = _run(d["pred_class"], d["pred_density"], dens, pts, size)
+    loss, info, gc, gd = _run(d["pred_class"], d["pred_density"], dens, pts, size, red=red)
     for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
         assert abs(info[k] - float(d["info_" + k])) <= 2e-5 * abs(float(d["info_" + k])) + 1e-4, (k, info[k])
     assert abs(info["ot_loss"]) < 1e-3

@@ -15,7 +15,22 @@ from oracle import ref
 from ebc_amd import synthetic as syn
 
 
-@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"])
+F1G = ["f1g_loss_224_r16.npz", "f1g_loss_224_r32.npz", "f1g_loss_448_r16.npz", "f1g_loss_448_r32.npz",
+       "f1g_loss_384_r8.npz", "f1g_loss_512_r8.npz"]
+
+
+def _red(d):
+    return int(d["reduction"]) if "reduction" in d.files else 8
+
+
+def ref_iters(err):
+    """Iterations bregman_pytorch.py:102-126 ran, from its err log (a check every 10; stop at err <= 1e-9)."""
+    e = err[err >= 0]
+    hit = np.nonzero(e <= 1e-9)[0]
+    return 10 * (int(hit[0]) + 1) if len(hit) else 100
+
+
+@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"] + F1G)
 def test_sinkhorn_oracle_matches_reference(fixture):
     d = golden(fixture)
     size = int(d["size"])
@@ -24,7 +39,7 @@ def test_sinkhorn_oracle_matches_reference(fixture):
     for b, p in enumerate(split_points(d)):
         if len(p) == 0:
             continue
-        r = ref.ot_crop(p, d["pred_density"][b, 0], size)
+        r = ref.ot_crop(p, d["pred_density"][b, 0], size, _red(d))
         assert rel_max(r["beta"], d["beta"][b]) < 2e-6
         assert rel_max(r["v"], d["v"][b]) < 2e-5
         assert rel_max(r["ot_grad"], d["ot_grad"][b]) < 2e-6
@@ -32,7 +47,7 @@ def test_sinkhorn_oracle_matches_reference(fixture):
         ne = len(r["err"])
         np.testing.assert_allclose(r["err"], d["err"][b][:ne], rtol=1e-4)
         assert abs(r["wd"] - d["wd"][b]) <= 1e-5 * abs(d["wd"][b]) + 1e-6
-        assert r["iters"] == 100 and not r["rolled_back"]   # never converges at these shapes
+        assert r["iters"] == ref_iters(d["err"][b]) and not r["rolled_back"]
 
 
 def test_sinkhorn_oracle_plan_small():
@@ -54,7 +69,7 @@ def test_sinkhorn_oracle_plan_small():
         assert rel_l2(P, d[key]) < 1e-5
 
 
-@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"])
+@pytest.mark.parametrize("fixture", ["f1_loss_224.npz", "f1_loss_448.npz"] + F1G)
 def test_dace_loss_oracle_matches_reference(fixture):
     d = golden(fixture)
     size = int(d["size"])
@@ -62,7 +77,7 @@ def test_dace_loss_oracle_matches_reference(fixture):
     dens = np.stack([syn.point_map(p, size, size)[None] for p in pts])
     pc = torch.tensor(d["pred_class"], requires_grad=True)
     pd = torch.tensor(d["pred_density"], requires_grad=True)
-    loss, info = ref.dace_loss(pc, pd, torch.from_numpy(dens), pts, BINS, input_size=size)
+    loss, info = ref.dace_loss(pc, pd, torch.from_numpy(dens), pts, BINS, reduction=_red(d), input_size=size)
     loss.backward()
     for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
         assert abs(float(info[k]) - float(d["info_" + k])) <= 1e-5 * abs(float(d["info_" + k])) + 1e-4, k
