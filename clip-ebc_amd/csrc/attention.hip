@@ -17,6 +17,7 @@
 // accumulators are directly the A operand of P.V with no LDS round trip (mfma.h).
 //   grid: B * H * ceil(L/(16 NW)) workgroups of NW waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
 #include <cstdlib>
+#include <string>
 
 #include "ebc_common.h"
 #include "kernels.h"
@@ -211,10 +212,10 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
 
 // ------------------------------------------------------------------------------ backward dQ
 template <class E, int NWV, int LFIX>
-__global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
-                                                          const typename E::T* __restrict__ out, const float* __restrict__ lse,
-                                                          float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                          int L_, int H, float scale)
+__device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                 const typename E::T* __restrict__ out, const float* __restrict__ lse,
+                                                 float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
+                                                 int L_, int H, float scale)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
     constexpr int QB = 16 * NWV;
     const int nqb = (L + QB - 1) / QB;
-    const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+    const int bh = bid / nqb, qb = bid % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
         dd += __shfl_xor(dd, 16, 64);
         dd += __shfl_xor(dd, 32, 64);
         dq = qv ? dd : 0.f;
-        if (fg == 0 && qv) delta[((size_t)b * H + h) * L + qme] = dd;
+        if (fg == 0 && qv && delta) delta[((size_t)b * H + h) * L + qme] = dd;
     }
     __syncthreads();
 
@@ -308,11 +309,40 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
     }
 }
 
-// ------------------------------------------------------------------------------ backward dK, dV
 template <class E, int NWV, int LFIX>
-__global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
-                                                           const float* __restrict__ lse, const float* __restrict__ delta,
-                                                           typename E::T* __restrict__ dqkv, int B, int L_, int H, float scale)
+__global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                          const typename E::T* __restrict__ out, const float* __restrict__ lse,
+                                                          float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
+                                                          int L_, int H, float scale)
+{
+    attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, delta, dqkv, B, L_, H, scale);
+}
+
+// ------------------------------------------------------------------------------ backward dK, dV
+// delta = rowsum(dO * O) of query q, summed in the dQ kernel's order (per 16-lane group fg: a 16-term fma
+// chain over columns 32 ks + 8 fg + j, then (p0 + p1) + (p2 + p3)), so both kernels see the same bits
+template <class E>
+__device__ __forceinline__ float attn_delta_row(const typename E::T* drow, const typename E::T* orow) {
+    float p[4];
+#pragma unroll
+    for (int fg = 0; fg < 4; ++fg) {
+        float dd = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const typename E::Frag df = load8<E>(drow + 32 * ks + 8 * fg), of = load8<E>(orow + 32 * ks + 8 * fg);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dd = fmaf((float)df[j], (float)of[j], dd);
+        }
+        p[fg] = dd;
+    }
+    return (p[0] + p[1]) + (p[2] + p[3]);
+}
+
+template <class E, int NWV, int LFIX>
+__device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                  const typename E::T* __restrict__ out, const float* __restrict__ lse,
+                                                  const float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
+                                                  int L_, int H, float scale)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -324,7 +354,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
     float* dl = ls + LP;
     constexpr int QB = 16 * NWV;
     const int nkb = (L + QB - 1) / QB;
-    const int bh = blockIdx.x / nkb, kb = blockIdx.x % nkb;
+    const int bh = bid / nkb, kb = bid % nkb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
@@ -332,7 +362,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
     load_rows<E, NWV>(Ds, dout + (size_t)b * L * D + h * HD, D, L);
     for (int q = threadIdx.x; q < LP; q += blockDim.x) {              // lse pre-scaled by log2(e)
         ls[q] = q < L ? lse[((size_t)b * H + h) * L + q] * LOG2E : INFINITY;
-        dl[q] = q < L ? delta[((size_t)b * H + h) * L + q] : 0.f;
+        if (delta) dl[q] = q < L ? delta[((size_t)b * H + h) * L + q] : 0.f;
+        else dl[q] = q < L ? attn_delta_row<E>(dout + ((size_t)b * L + q) * D + h * HD, out + ((size_t)b * L + q) * D + h * HD) : 0.f;
     }
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
@@ -397,6 +428,27 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
     }
 }
 
+template <class E, int NWV, int LFIX>
+__global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                           const float* __restrict__ lse, const float* __restrict__ delta,
+                                                           typename E::T* __restrict__ dqkv, int B, int L_, int H, float scale)
+{
+    attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, nullptr, lse, delta, dqkv, B, L_, H, scale);
+}
+
+// dQ and dK/dV workgroups in ONE grid (the first ndq blocks take the dQ role): each dK/dV workgroup forms the
+// row statistic delta itself, so the two roles are independent and run side by side -- two workgroups per CU
+// at 8 waves, the 2 x B x H x ceil(L / 128) workgroups filling the CUs that one role's grid leaves idle
+template <class E, int NWV, int LFIX>
+__global__ __launch_bounds__(64 * NWV) void attn_bwd_fused_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                             const typename E::T* __restrict__ out, const float* __restrict__ lse,
+                                                             typename E::T* __restrict__ dqkv, int ndq, int B, int L_, int H,
+                                                             float scale)
+{
+    if ((int)blockIdx.x < ndq) attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale);
+    else attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x - ndq, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale);
+}
+
 int attn_waves(int L) {
     static const int forced = getenv("EBC_ATTN_NW") ? atoi(getenv("EBC_ATTN_NW")) : 0;
     if (forced == 8 || forced == 16) return forced;
@@ -455,9 +507,38 @@ template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
+template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, const void* dout, const void* out, const float* lse,
+                                                           void* dqkv, int B, int L, int H, hipStream_t st)
+{
+    using C = AttnCfg<E>;
+    const size_t lds = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
+        attr = true;
+    }
+    const int ndq = B * H * ((L + 16 * NW - 1) / (16 * NW));
+    const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 1, 0, 0, 0, B, L, H, st) : -1;
+    hipLaunchKernelGGL((attn_bwd_fused_kernel<E, NW, LFIX>), dim3(2 * ndq), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
+                       (const typename E::T*)dout, (const typename E::T*)out, lse, (typename E::T*)dqkv, ndq, B, L, H, 0.125f);
+    probe_stop(pi, st);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+// EBC_ATTN_BWD=split: the two backward kernels one after the other (delta through global memory)
+bool attn_bwd_split() {
+    static const bool split = getenv("EBC_ATTN_BWD") && std::string(getenv("EBC_ATTN_BWD")) == "split";
+    return split;
+}
+
 template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
                                   void* dqkv, int B, int L, int H, hipStream_t st)
 {
+    if (!attn_bwd_split() && E::BYTES == 2) {
+        return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st)
+                            : attn_bwd_fused_nw<E, 8, 0>(qkv, dout, out, lse, dqkv, B, L, H, st);
+    }
     if (attn_waves(L) == 16)
         return L == L_VPT32 ? attn_bwd_nw<E, 16, L_VPT32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st)
                             : attn_bwd_nw<E, 16, 0>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
