@@ -274,6 +274,102 @@ __global__ __launch_bounds__(256) void bn_relu_kernel(const T* __restrict__ z, c
     st8(out + p * C + c, v);
 }
 
+// ---- ModifiedResNet encoder blocks (image_encoder.py:10-115, blocks.py:56-101), NHWC rows [B*H*W][C]
+// out[b][y][x] = mean of the 2x2 window of relu(z*scale + shift) (the Bottleneck's conv2 -> bn2 -> relu2 ->
+// AvgPool2d(2) when stride 2); 8 channels per thread
+template <class T>
+__global__ __launch_bounds__(256) void bn_relu_avgpool_kernel(const T* __restrict__ z, const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, T* __restrict__ out, int B,
+                                                              int H, int W, int C)
+{
+    const int C8 = C / 8, Ho = H / 2, Wo = W / 2;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long)B * Ho * Wo * C8) return;
+    const long po = e / C8;
+    const int c = (int)(e - po * C8) * 8;
+    const int b = (int)(po / (Ho * Wo)), r = (int)(po - (long)b * Ho * Wo), yo = r / Wo, xo = r - yo * Wo;
+    const float4 s0 = ld4(scale + c), s1 = ld4(scale + c + 4), h0 = ld4(shift + c), h1 = ld4(shift + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    float v[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ld8(z + (((size_t)b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1)) * C + c, v[k]);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        // AvgPool2d: sum of the window in row-major order, then / 4 (aten avg_pool2d, count_include_pad)
+        const float a = fmaxf(fmaf(v[0][i], sc[i], sh[i]), 0.f), bb = fmaxf(fmaf(v[1][i], sc[i], sh[i]), 0.f);
+        const float cc = fmaxf(fmaf(v[2][i], sc[i], sh[i]), 0.f), d = fmaxf(fmaf(v[3][i], sc[i], sh[i]), 0.f);
+        o[i] = (((a + bb) + cc) + d) / 4.0f;
+    }
+    st8(out + po * C + c, o);
+}
+
+// out = AvgPool2d(2)(x) on NHWC rows (the downsample branch's "-1" pool); TI -> TO, 8 channels per thread
+template <class TI, class TO>
+__global__ __launch_bounds__(256) void avgpool2_kernel(const TI* __restrict__ x, TO* __restrict__ out, int B, int H, int W,
+                                                       int C)
+{
+    const int C8 = C / 8, Ho = H / 2, Wo = W / 2;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long)B * Ho * Wo * C8) return;
+    const long po = e / C8;
+    const int c = (int)(e - po * C8) * 8;
+    const int b = (int)(po / (Ho * Wo)), r = (int)(po - (long)b * Ho * Wo), yo = r / Wo, xo = r - yo * Wo;
+    float v[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ld8(x + (((size_t)b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1)) * C + c, v[k]);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (((v[0][i] + v[1][i]) + v[2][i]) + v[3][i]) / 4.0f;
+    st8(out + po * C + c, o);
+}
+
+// AvgPool2d(2) backward: gx[b][y][x] = g[b][y/2][x/2] / 4 (TI -> TO), 8 channels per thread
+template <class TI, class TO>
+__global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const TI* __restrict__ g, TO* __restrict__ gx, int B, int H, int W,
+                                                           int C)
+{
+    const int C8 = C / 8, Ho = H / 2, Wo = W / 2;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long)B * H * W * C8) return;
+    const long p = e / C8;
+    const int c = (int)(e - p * C8) * 8;
+    const int b = (int)(p / (H * W)), r = (int)(p - (long)b * H * W), y = r / W, x = r - y * W;
+    float v[8];
+    ld8(g + (((size_t)b * Ho + y / 2) * Wo + x / 2) * C + c, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] *= 0.25f;
+    st8(gx + p * C + c, v);
+}
+
+// y = relu(z*scale + shift + identity), identity = idt*iscale + ishift (the downsample branch's BatchNorm) or
+// idt itself (iscale == NULL): bn3 -> += identity -> relu3 of the Bottleneck; 8 channels per thread
+template <class T>
+__global__ __launch_bounds__(256) void bn_add_relu_flat_kernel(const T* __restrict__ z, const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, const T* __restrict__ idt,
+                                                               const float* __restrict__ iscale,
+                                                               const float* __restrict__ ishift, T* __restrict__ y, long P,
+                                                               int C)
+{
+    const int C8 = C / 8;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= P * C8) return;
+    const long p = e / C8;
+    const int c = (int)(e - p * C8) * 8;
+    const size_t off = (size_t)p * C + c;
+    float zv[8], iv[8];
+    ld8(z + off, zv);
+    ld8(idt + off, iv);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float idn = iscale ? fmaf(iv[i], iscale[c + i], ishift[c + i]) : iv[i];
+        o[i] = fmaxf(fmaf(zv[i], scale[c + i], shift[c + i]) + idn, 0.f);
+    }
+    st8(y + off, o);
+}
+
 // column partials of sum(z) and sum(z*z) (BatchNorm batch statistics of a 1x1 conv output); the
 // bn_bwd_partial_kernel scheme: (C/8) x RL threads, UNR rows per load batch, row order kept
 template <class T, int UNR>
@@ -910,6 +1006,60 @@ extern "C" int ebc_bn_bwd_apply_flat(int dtype, const void* gy, const void* mask
                                                    (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale, shift,
                                                    coef, (T*)dz, gmask, P, C));
     }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+// ------------------------------------------------------------------ ModifiedResNet block helpers
+extern "C" int ebc_bn_relu_avgpool(int dtype, const void* z, const float* scale, const float* shift, void* out, int B, int H,
+                                   int W, int C, ebc_stream_t stream)
+{
+    if (!z || !scale || !shift || !out || B <= 0 || H % 2 || W % 2 || H <= 0 || W <= 0 || C % 8) return EBC_E_ARG;
+    const long n = (long)B * (H / 2) * (W / 2) * (C / 8);
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(bn_relu_avgpool_kernel<T>, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream,
+                                               (const T*)z, scale, shift, (T*)out, B, H, W, C));
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+// dtype_in / dtype_out: the element types of x and out (EBC_F32 or the compute dtype)
+extern "C" int ebc_avgpool2(int dtype_in, int dtype_out, const void* x, void* out, int B, int H, int W, int C,
+                            ebc_stream_t stream)
+{
+    if (!x || !out || B <= 0 || H % 2 || W % 2 || H <= 0 || W <= 0 || C % 8 || dtype_in != dtype_out) return EBC_E_ARG;
+    const long n = (long)B * (H / 2) * (W / 2) * (C / 8);
+    EBC_DTYPE_SWITCH(dtype_in, hipLaunchKernelGGL((avgpool2_kernel<T, T>), dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream,
+                                                  (const T*)x, (T*)out, B, H, W, C));
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+extern "C" int ebc_avgpool2_bwd(int dtype_in, int dtype_out, const void* g, void* gx, int B, int H, int W, int C,
+                                ebc_stream_t stream)
+{
+    if (!g || !gx || B <= 0 || H % 2 || W % 2 || H <= 0 || W <= 0 || C % 8) return EBC_E_ARG;
+    const long n = (long)B * H * W * (C / 8);
+    const hipStream_t st = (hipStream_t)stream;
+    if (dtype_in == dtype_out) {
+        EBC_DTYPE_SWITCH(dtype_in, hipLaunchKernelGGL((avgpool2_bwd_kernel<T, T>), dim3(nblk(n)), dim3(256), 0, st,
+                                                      (const T*)g, (T*)gx, B, H, W, C));
+    } else if (dtype_in == EBC_F32) {
+        EBC_DTYPE_SWITCH(dtype_out, hipLaunchKernelGGL((avgpool2_bwd_kernel<float, T>), dim3(nblk(n)), dim3(256), 0, st,
+                                                       (const float*)g, (T*)gx, B, H, W, C));
+    } else {
+        return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+extern "C" int ebc_bn_add_relu_flat(int dtype, const void* z, const float* scale, const float* shift, const void* idt,
+                                    const float* iscale, const float* ishift, void* y, long P, int C, ebc_stream_t stream)
+{
+    if (!z || !scale || !shift || !idt || !y || P <= 0 || C % 8 || (!iscale != !ishift)) return EBC_E_ARG;
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(bn_add_relu_flat_kernel<T>, dim3(nblk(P * (C / 8))), dim3(256), 0,
+                                               (hipStream_t)stream, (const T*)z, scale, shift, (const T*)idt, iscale,
+                                               ishift, (T*)y, P, C));
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

@@ -848,7 +848,8 @@ int dispatch_epi(const GemmArgs& g, int epi, int out_f32, void* ws, size_t wsb, 
     switch (epi) {
         case EPI_STORE: return dispatch_out<E, EPI_STORE>(g, out_f32, ws, wsb, st);
         case EPI_GELU: return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_GELU>(g, ws, wsb, st);
-        case EPI_RESID: return dispatch_tile<E, float, EPI_RESID>(g, ws, wsb, st);
+        case EPI_RESID: return out_f32 ? dispatch_tile<E, float, EPI_RESID>(g, ws, wsb, st)
+                                       : dispatch_tile<E, typename E::T, EPI_RESID>(g, ws, wsb, st);
         case EPI_GELU_BWD: return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_GELU_BWD>(g, ws, wsb, st);
     }
     return EBC_E_ARG;

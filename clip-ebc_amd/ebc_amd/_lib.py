@@ -99,6 +99,10 @@ SIGNATURES = {
     "ebc_bn_stats": (_I, [_I, _P, _P, _P, _Z, _L, _I, _P]),
     "ebc_bn_relu": (_I, [_I, _P, _P, _P, _P, _L, _I, _P]),
     "ebc_bn_bwd_apply_flat": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "ebc_bn_relu_avgpool": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_avgpool2": (_I, [_I, _I, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_avgpool2_bwd": (_I, [_I, _I, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_bn_add_relu_flat": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, EbcAugConst, _P]),
     "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "ebc_probe_begin": (_I, [_I]),

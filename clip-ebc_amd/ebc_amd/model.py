@@ -296,6 +296,9 @@ _DEC_WS: Dict[Tuple[torch.device, int], Tensor] = {}
 # default: measured 2.7 % slower per step on MI355X (r01, interleaved A/B in one process: the two
 # 1-workgroup-per-CU GEMMs contend for CUs and the data-gradient chain is the critical path).
 _USE_SIDE = __import__("os").environ.get("EBC_DEC_SIDE", "0") == "1"
+# EBC_RN50_ENCODER=torch runs clip_resnet50's whole ModifiedResNet on PyTorch-ROCm (MIOpen) instead of the
+# HIP Bottleneck blocks (ebc_amd/resnet.py _ResBlockFn); an A/B switch, not a fallback (both need the GPU)
+_RN50_TORCH_ENCODER = __import__("os").environ.get("EBC_RN50_ENCODER", "") == "torch"
 _SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
 
 
@@ -652,11 +655,14 @@ class CLIP_EBC(nn.Module):
         return self._forward_vpt_nhwc(x).permute(0, 3, 1, 2)
 
     def _forward_resnet(self, x: Tensor, cdt: torch.dtype) -> Union[Tensor, Tuple[Tensor, Tensor]]:
-        """models/clip/model.py:191-217 for the resnet50 backbone: the trainable ModifiedResNet on PyTorch-ROCm
-        (channels_last, the caller's autocast), then the HIP Bottleneck decoder and head."""
-        from .resnet import _BottleneckFn
-        feat = self.image_encoder(x.contiguous(memory_format=torch.channels_last))
-        feat = feat.permute(0, 2, 3, 1).float().contiguous()                # NHWC rows, f32
+        """models/clip/model.py:191-217 for the resnet50 backbone: the trainable ModifiedResNet (stem on PyTorch-ROCm,
+        its 16 Bottlenecks on HIP), then the HIP Bottleneck decoder and head."""
+        from .resnet import _BottleneckFn, encoder_forward
+        if _RN50_TORCH_ENCODER:                                              # A/B: the whole encoder on MIOpen
+            feat = self.image_encoder(x.contiguous(memory_format=torch.channels_last)).permute(0, 2, 3, 1)
+        else:                                                                # stem on MIOpen, 16 blocks on HIP
+            feat = encoder_forward(self.image_encoder, x, cdt, self.training)
+        feat = feat.float().contiguous()                                     # NHWC rows, f32
         up = self.encoder_reduction // self.reduction
         blk = self.image_decoder[0]
         with torch.autocast("cuda", enabled=False):

@@ -176,6 +176,228 @@ def _batch_norm_bwd(L, gamma: Tensor, state, dnext: Tensor, mask: Optional[Tenso
     return dg, db, coef
 
 
+def _ws(L, dev, dt, B, H, W, C, N, P, Cmax):
+    """Stream-owned scratch for one block: the 3x3 conv's (split-K counters + BN partials) and the flat BN kernels'
+    column partials over P rows of up to Cmax channels."""
+    from .model import _dec_workspace
+    rpb = 8 * max(1, 512 // max(1, Cmax // 8))
+    need = max(L.ebc_dec_workspace_bytes(dt, B, H, W, C, N), 16384 + (-(-P // rpb)) * 8 * Cmax)
+    return _dec_workspace(dev, need)
+
+
+class _ResBlockFn(torch.autograd.Function):
+    """One ModifiedResNet Bottleneck (blocks.py:56-101) on libebc_hip.so, NHWC rows in the compute dtype:
+    conv1 1x1 -> bn1 -> relu -> conv2 3x3 -> bn2 -> relu -> avgpool(stride) -> conv3 1x1 -> bn3 (+ identity:
+    x, or avgpool(stride) -> 1x1 -> bn for the downsample branch) -> relu.  x [B,H,W,Cin] -> y [B,H/s,W/s,4p]."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2, w3, wd, g1, b1, g2, b2, g3, b3, gd, bd, blk, cdtype, training):
+        with _lib.on(x):
+            return _ResBlockFn._forward(ctx, x, (w1, w2, w3, wd), blk, cdtype, training)
+
+    @staticmethod
+    def _forward(ctx, x, wts, blk, cdtype, training):
+        L = _lib.lib()
+        x = x.detach()
+        if x.dtype != cdtype or not x.is_contiguous():
+            x = x.to(cdtype).contiguous()
+        B, H, W, Cin = x.shape
+        s = blk.stride
+        Ho, Wo = H // s, W // s
+        P, Po = B * H * W, B * Ho * Wo
+        planes, Cout = wts[0].shape[0], wts[2].shape[0]
+        down = blk.downsample is not None
+        dev, dt, st = x.device, _lib.dtype_code(cdtype), _lib.stream(x)
+        ws = _ws(L, dev, dt, B, H, W, planes, planes, P, max(Cin, Cout, planes))
+        use_batch = training or not blk.bn1.track_running_stats
+        bns = (blk.bn1, blk.bn2, blk.bn3) + ((blk.downsample[2],) if down else ())
+        from .model import _bn_group
+
+        def colsum_for(bn):
+            return torch.empty(2 * bn.num_features + (_bn_group(bn) is not None), device=dev, dtype=torch.float64) \
+                if use_batch else None
+
+        def stats(z, bn, rows, C):
+            cs = colsum_for(bn)
+            if cs is not None:
+                _lib.check(L.ebc_bn_stats(dt, _lib.ptr(z), _lib.ptr(cs), _lib.ptr(ws), ws.numel(), rows, C, st), "ebc_bn_stats")
+            return _batch_norm_fwd(L, bn, cs, rows, C, training, dev, st)
+
+        def mat(w, n, k):
+            return w.detach().reshape(n, k).to(cdtype).contiguous()
+
+        W1, W3 = mat(wts[0], planes, Cin), mat(wts[2], Cout, planes)
+        Wd = mat(wts[3], Cout, Cin) if down else None
+        geo = (ctypes.c_long * 6)()
+        _lib.check(L.ebc_dec_geometry(dt, B, H, W, planes, geo), "ebc_dec_geometry")
+        Q = geo[4]
+        wk2 = torch.empty(planes, 3, 3, planes, device=dev, dtype=cdtype)
+        wf2 = torch.empty(planes, 3, 3, planes, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_dec_prep_weights(dt, _lib.ptr(wts[1].detach().float().contiguous()), _lib.ptr(wk2), _lib.ptr(wf2),
+                                          planes, planes, st), "ebc_dec_prep_weights")
+        # conv1 1x1 -> bn1 -> relu1, into the zero-padded conv2 input
+        z1 = torch.empty(P, planes, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(x), _lib.ptr(W1), _lib.ptr(z1), None, None, None, P, planes, Cin, st),
+                   "ebc_gemm(conv1)")
+        s1 = stats(z1, bns[0], P, planes)
+        h1pad = torch.empty(Q, planes, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_bn_relu_pad(dt, _lib.ptr(z1), _lib.ptr(s1[2]), _lib.ptr(s1[3]), _lib.ptr(h1pad), B, H, W, planes,
+                                     st), "ebc_bn_relu_pad")
+        # conv2 3x3 (BN statistics in the epilogue) -> bn2 -> relu2 -> avgpool(stride)
+        z2 = torch.empty(P, planes, device=dev, dtype=cdtype)
+        cs2 = colsum_for(bns[1])
+        _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(h1pad), _lib.ptr(wk2), _lib.ptr(z2), _lib.ptr(cs2), None, None,
+                                     _lib.ptr(ws), ws.numel(), B, H, W, planes, planes, st), "ebc_conv3x3_fwd")
+        s2 = _batch_norm_fwd(L, bns[1], cs2, P, planes, training, dev, st)
+        h2p = torch.empty(Po, planes, device=dev, dtype=cdtype)
+        if s > 1:
+            _lib.check(L.ebc_bn_relu_avgpool(dt, _lib.ptr(z2), _lib.ptr(s2[2]), _lib.ptr(s2[3]), _lib.ptr(h2p), B, H, W,
+                                             planes, st), "ebc_bn_relu_avgpool")
+        else:
+            _lib.check(L.ebc_bn_relu(dt, _lib.ptr(z2), _lib.ptr(s2[2]), _lib.ptr(s2[3]), _lib.ptr(h2p), P, planes, st),
+                       "ebc_bn_relu")
+        # conv3 1x1 -> bn3
+        z3 = torch.empty(Po, Cout, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(h2p), _lib.ptr(W3), _lib.ptr(z3), None, None, None, Po, Cout, planes, st),
+                   "ebc_gemm(conv3)")
+        s3 = stats(z3, bns[2], Po, Cout)
+        # identity: x, or avgpool(stride) -> 1x1 -> bn (downsample "-1", "0", "1")
+        xd = zd = sd = None
+        if down:
+            if s > 1:
+                xd = torch.empty(Po, Cin, device=dev, dtype=cdtype)
+                _lib.check(L.ebc_avgpool2(dt, dt, _lib.ptr(x), _lib.ptr(xd), B, H, W, Cin, st), "ebc_avgpool2")
+            else:
+                xd = x.view(P, Cin)
+            zd = torch.empty(Po, Cout, device=dev, dtype=cdtype)
+            _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(xd), _lib.ptr(Wd), _lib.ptr(zd), None, None, None, Po, Cout, Cin, st),
+                       "ebc_gemm(downsample)")
+            sd = stats(zd, bns[3], Po, Cout)
+        y = torch.empty(B, Ho, Wo, Cout, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_bn_add_relu_flat(dt, _lib.ptr(z3), _lib.ptr(s3[2]), _lib.ptr(s3[3]),
+                                          _lib.ptr(zd if down else x), _lib.ptr(sd[2]) if down else None,
+                                          _lib.ptr(sd[3]) if down else None, _lib.ptr(y), Po, Cout, st), "ebc_bn_add_relu_flat")
+        ctx.save_for_backward(x, z1, h1pad, z2, h2p, z3, y, W1, wf2, W3, *(() if not down else (xd, zd, Wd)))
+        ctx.states = (s1, s2, s3, sd)
+        ctx.gammas = tuple(bn.weight for bn in bns)
+        ctx.meta = (B, H, W, Cin, s, Ho, Wo, P, Po, planes, Cout, down, cdtype, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        with _lib.on(gy):
+            return _ResBlockFn._backward(ctx, gy)
+
+    @staticmethod
+    def _backward(ctx, gy):
+        from .model import _wgrad_rows
+        L = _lib.lib()
+        B, H, W, Cin, s, Ho, Wo, P, Po, planes, Cout, down, cdtype, xdt = ctx.meta
+        saved = ctx.saved_tensors
+        x, z1, h1pad, z2, h2p, z3, y, W1, wf2, W3 = saved[:10]
+        xd, zd, Wd = saved[10:] if down else (None, None, None)
+        s1, s2, s3, sd = ctx.states
+        g1, g2, g3 = ctx.gammas[:3]
+        dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream(y)
+        gy = gy.to(cdtype).contiguous().view(Po, Cout)
+        ws = _ws(L, dev, dt, B, H, W, planes, planes, P, max(Cin, Cout, planes))
+        geo = (ctypes.c_long * 6)()
+        _lib.check(L.ebc_dec_geometry(dt, B, H, W, planes, geo), "ebc_dec_geometry")
+        Q, Qs = geo[4], geo[5]
+        f32 = dict(device=dev, dtype=torch.float32)
+
+        def apply_flat(g, mask, z, st_, coef, gmask=None):
+            dz = torch.empty(z.shape, device=dev, dtype=cdtype)
+            _lib.check(L.ebc_bn_bwd_apply_flat(dt, _lib.ptr(g), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(st_[0]),
+                                               _lib.ptr(st_[1]), _lib.ptr(st_[2]), _lib.ptr(st_[3]), _lib.ptr(coef),
+                                               _lib.ptr(dz), _lib.ptr(gmask), z.shape[0], z.shape[1], st),
+                       "ebc_bn_bwd_apply_flat")
+            return dz
+
+        # bn3 (+ relu3 through y); without a downsample the identity's gradient is g = gy * (y > 0) itself (f32)
+        dg3, db3, coef3 = _batch_norm_bwd(L, g3, s3, gy, y, z3, ws, Po, Cout, dev, st)
+        gid = None if down else torch.empty(Po, Cout, **f32)
+        dz3 = apply_flat(gy, y, z3, s3, coef3, gid)
+        dw3 = _wgrad_rows(L, dz3, h2p, cdtype, dev, st)
+        dh2p = torch.empty(Po, planes, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dz3), _lib.ptr(W3.t().contiguous()), _lib.ptr(dh2p), None, None, None,
+                              Po, planes, Cout, st), "ebc_gemm(conv3 dX)")
+        del dz3
+        dwd = dgd = dbd = None
+        if down:
+            # downsample bn (same masked gradient) -> 1x1 -> avgpool: the identity's input gradient, f32
+            dgd, dbd, coefd = _batch_norm_bwd(L, ctx.gammas[3], sd, gy, y, zd, ws, Po, Cout, dev, st)
+            dzd = apply_flat(gy, y, zd, sd, coefd)
+            dwd = _wgrad_rows(L, dzd, xd, cdtype, dev, st)
+            dxd = torch.empty(Po, Cin, **f32)
+            _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(dzd), _lib.ptr(Wd.t().contiguous()), _lib.ptr(dxd), None, None, None,
+                                  Po, Cin, Cout, st), "ebc_gemm(downsample dX)")
+            del dzd
+            if s > 1:
+                gid = torch.empty(P, Cin, **f32)
+                _lib.check(L.ebc_avgpool2_bwd(_lib.EBC_F32, _lib.EBC_F32, _lib.ptr(dxd), _lib.ptr(gid), B, H, W, Cin, st),
+                           "ebc_avgpool2_bwd(downsample)")
+                del dxd
+            else:
+                gid = dxd
+        # avgpool -> relu2 -> bn2 (ReLU mask recomputed from z2) -> conv2's gradients
+        if s > 1:
+            dh2 = torch.empty(P, planes, device=dev, dtype=cdtype)
+            _lib.check(L.ebc_avgpool2_bwd(dt, dt, _lib.ptr(dh2p), _lib.ptr(dh2), B, H, W, planes, st), "ebc_avgpool2_bwd")
+            del dh2p
+        else:
+            dh2 = dh2p
+        dg2, db2, coef2 = _batch_norm_bwd(L, g2, s2, dh2, None, z2, ws, P, planes, dev, st)
+        dz2pad = torch.empty(Q, planes, device=dev, dtype=cdtype)
+        dz2T = torch.empty(planes, Qs, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_bn_bwd_apply(dt, _lib.ptr(dh2), None, _lib.ptr(z2), _lib.ptr(s2[0]), _lib.ptr(s2[1]),
+                                      _lib.ptr(s2[2]), _lib.ptr(s2[3]), _lib.ptr(coef2), _lib.ptr(dz2pad), _lib.ptr(dz2T),
+                                      B, H, W, planes, st), "ebc_bn_bwd_apply(bn2)")
+        del dh2
+        xT3 = torch.empty(3, planes, Qs, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_dec_transpose3(dt, _lib.ptr(h1pad), _lib.ptr(xT3), B, H, W, planes, st), "ebc_dec_transpose3")
+        dw2 = torch.empty(planes, planes, 3, 3, **f32)
+        _lib.check(L.ebc_conv3x3_wgrad(dt, _lib.ptr(dz2T), _lib.ptr(xT3), _lib.ptr(dw2), _lib.ptr(ws), ws.numel(),
+                                       B, H, W, planes, planes, st), "ebc_conv3x3_wgrad")
+        del xT3, dz2T
+        dh1 = torch.empty(P, planes, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(dz2pad), _lib.ptr(wf2), _lib.ptr(dh1), None, None, None, _lib.ptr(ws),
+                                     ws.numel(), B, H, W, planes, planes, st), "ebc_conv3x3_fwd(dgrad)")
+        del dz2pad
+        # bn1 (ReLU mask recomputed from z1) -> conv1: dx = dz1 W1 + the identity's gradient
+        dg1, db1, coef1 = _batch_norm_bwd(L, g1, s1, dh1, None, z1, ws, P, planes, dev, st)
+        dz1 = apply_flat(dh1, None, z1, s1, coef1)
+        del dh1
+        dw1 = _wgrad_rows(L, dz1, x.view(P, Cin), cdtype, dev, st)
+        dx = torch.empty(B, H, W, Cin, device=dev, dtype=cdtype)
+        _lib.check(L.ebc_gemm(dt, 2, 0, _lib.ptr(dz1), _lib.ptr(W1.t().contiguous()), _lib.ptr(dx), None, _lib.ptr(gid),
+                              None, P, Cin, planes, st), "ebc_gemm(conv1 dX + identity)")
+        ctx.states = None
+        return (dx.to(xdt) if xdt != cdtype else dx, dw1.view(planes, Cin, 1, 1), dw2, dw3.view(Cout, planes, 1, 1),
+                None if dwd is None else dwd.view(Cout, Cin, 1, 1), dg1, db1, dg2, db2, dg3, db3, dgd, dbd,
+                None, None, None)
+
+
+def encoder_forward(enc: "ModifiedResNet", x: Tensor, cdtype: torch.dtype, training: bool) -> Tensor:
+    """ModifiedResNet forward with the 16 Bottlenecks on libebc_hip.so: the 3-conv stem + avgpool on
+    PyTorch-ROCm (3- and 32-channel convolutions), then NHWC rows through `_ResBlockFn`.
+    Returns layer4's output as NHWC [B, h, w, 2048] in the compute dtype."""
+    h = x.type(enc.conv1.weight.dtype).contiguous(memory_format=torch.channels_last)
+    h = enc.relu1(enc.bn1(enc.conv1(h)))
+    h = enc.relu2(enc.bn2(enc.conv2(h)))
+    h = enc.avgpool(enc.relu3(enc.bn3(enc.conv3(h))))
+    h = h.permute(0, 2, 3, 1)
+    with torch.autocast("cuda", enabled=False):
+        for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
+            for blk in layer:
+                d = blk.downsample
+                h = _ResBlockFn.apply(h, blk.conv1.weight, blk.conv2.weight, blk.conv3.weight,
+                                      None if d is None else d[1].weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
+                                      blk.bn2.bias, blk.bn3.weight, blk.bn3.bias, None if d is None else d[2].weight,
+                                      None if d is None else d[2].bias, blk, cdtype, training)
+    return h
+
+
 class _BottleneckFn(torch.autograd.Function):
     """Bottleneck(C, C, expansion=1) decoder after the x`up` bilinear adapt (models/clip/model.py:195-197;
     models/utils.py:346-363): conv1x1-BN-ReLU, conv3x3-BN-ReLU, conv1x1-BN, + x, ReLU.

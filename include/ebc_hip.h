@@ -90,7 +90,8 @@ int ebc_sinkhorn(const float* a, const float* b, const float* C, int na, int nb,
  * (image_encoder.py:141, as im2col-GEMM) and the 1x1 projection (models/clip/model.py:91-95).
  *   epilogue 0 STORE:    C = acc + bias                      (C of dtype, or f32 if out_f32)
  *   epilogue 1 GELU:     aux = acc + bias; C = QuickGELU(aux) (blocks.py:17-19)
- *   epilogue 2 RESID:    C(f32) = resid(f32) + acc + bias     (residual stream, may be in place)
+ *   epilogue 2 RESID:    C = resid(f32) + acc + bias          (C f32: the residual stream, may be in place;
+ *                                                              C in dtype when !out_f32)
  *   epilogue 3 GELU_BWD: C = acc * QuickGELU'(aux)           (MLP backward, dX only)
  */
 enum { EBC_EPI_STORE = 0, EBC_EPI_GELU = 1, EBC_EPI_RESID = 2, EBC_EPI_GELU_BWD = 3 };
@@ -308,6 +309,18 @@ int ebc_bn_relu(int dtype, const void* z, const float* scale, const float* shift
 int ebc_bn_bwd_apply_flat(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
                           const float* rstd, const float* scale, const float* shift, const float* coef, void* dz,
                           float* gmask, long P, int C, ebc_stream_t stream);
+/* ModifiedResNet encoder blocks on HIP (models/clip/_clip/image_encoder.py:10-115, blocks.py:56-101: 1x1 -> 3x3 ->
+ * avgpool(stride) -> 1x1, downsample = avgpool + 1x1 + BN), NHWC rows [B*H*W][C], C % 8 == 0, H, W even:
+ *   ebc_bn_relu_avgpool:  out [B][H/2][W/2][C] = AvgPool2d(2)(relu(z*scale + shift))      (bn2 -> relu2 -> avgpool)
+ *   ebc_avgpool2:         out = AvgPool2d(2)(x), same element type                        (downsample "-1" pool)
+ *   ebc_avgpool2_bwd:     gx [B][H][W][C] = g[b][y/2][x/2] / 4 (g f32 or the compute dtype -> gx in dtype_out)
+ *   ebc_bn_add_relu_flat: y = relu(z*scale + shift + idt*iscale + ishift) (iscale == NULL: + idt)  (bn3 + identity) */
+int ebc_bn_relu_avgpool(int dtype, const void* z, const float* scale, const float* shift, void* out, int B, int H, int W,
+                        int C, ebc_stream_t stream);
+int ebc_avgpool2(int dtype_in, int dtype_out, const void* x, void* out, int B, int H, int W, int C, ebc_stream_t stream);
+int ebc_avgpool2_bwd(int dtype_in, int dtype_out, const void* g, void* gx, int B, int H, int W, int C, ebc_stream_t stream);
+int ebc_bn_add_relu_flat(int dtype, const void* z, const float* scale, const float* shift, const void* idt,
+                         const float* iscale, const float* ishift, void* y, long P, int C, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Measurement (bench.py): in-step kernel durations and profile windows.  Not on the reference's
