@@ -440,6 +440,32 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     return;
 #endif
 
+    if (g.splits > 1 && g.cnt == nullptr) {
+        // split-K without a last arriver (deep splits of the weight-gradient products): every split stores its
+        // f32 partial row-major into part[split][M][N] (columns as the epilogue maps them), a separate launch
+        // (splitk_reduce_kernel) sums the splits in split order -- deterministic, and the sum is spread over
+        // the whole GPU instead of re-read through one CU
+        float* P = g.part + (size_t)split * g.M * g.N;
+        const int mb = m0 + wm * WM + fr;
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+            const int m = mb + a * 16;
+            if (m >= g.M) break;
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                int n;
+                if constexpr (MODE == 0) {
+                    constexpr int NP = TN / 2;
+                    const int nb = n0 + wn * WN;
+                    n = (b / 2 < NP) ? nb + (b / 2) * 32 + fg * 8 + (b & 1) * 4 : nb + NP * 32 + fg * 4;
+                } else {
+                    n = n0 + wn * WN + b * 16 + 4 * fg;
+                }
+                *reinterpret_cast<f32x4*>(P + (size_t)m * g.N + n) = acc[a][b];
+            }
+        }
+        return;
+    }
     if (g.splits > 1) {
         // split-K: publish this split's f32 partial (lane-major: the reader has the same lane map,
         // so every access is a coalesced 16-B per lane), count the arrival; the last arriver sums
@@ -871,6 +897,71 @@ int launch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st)
     return EBC_E_UNSUPPORTED;
 }
 
+// Weight-gradient products (MODE 2 conv dW, and ebc_gemm_wgrad's 1x1 dW): small outputs, long K (pixels).
+// Tile and split-K are chosen on a cost model of the measured limits -- the L2 -> LDS fill (~70 GB/s per CU,
+// MI355X_MICROARCH.md), ~8 TFLOP/s of MFMA per CU, whole waves of CUs -- plus the split's reduction: a
+// last-arriver re-read through one CU for 2 splits, else f32 partials summed by a separate grid-wide launch.
+// (r02: the RN50 encoder's 64 x 576 x 107520 conv dW ran one 256x192 tile x 8 splits: 267 us, 30 TFLOP/s.)
+struct WPlan { int cfg, splits; bool partials; };
+double wplan_cost(const TileCfg& c, int occ, int eb, int M, int N, int K, int s) {
+    const long tiles = ntiles(M, N, c.bm, c.bn), wgs = tiles * s;
+    const double ks = (double)K / s;
+    const double fill = (double)(c.bm + c.bn) * ks * eb / 70e9, mma = 2.0 * c.bm * c.bn * ks / 8e12;
+    const long slots = (long)NUM_CU * occ;
+    const long rounds = (wgs + slots - 1) / slots;
+    const int per_cu = (int)std::min<long>(occ, (wgs + NUM_CU - 1) / NUM_CU);
+    double t = rounds * per_cu * std::max(fill, mma);
+    if (s == 2) t += (double)c.bm * c.bn * 4 / 70e9;                       // last arriver re-reads one partial
+    else if (s > 2) t += (double)(s + 1) * M * N * 4 / 4e12 + 4e-6;        // partials + reduce launch
+    return t;
+}
+WPlan wgrad_plan(bool sixteen, bool conv, int M, int N, int K) {
+    const int bk = sixteen ? 64 : 32, nk = K / bk, eb = sixteen ? 2 : 4;
+    // (cfg, CUs' worth of LDS: workgroups per CU)
+    static const int cand16_conv[][2] = {{3, 1}, {7, 1}, {13, 1}, {2, 3}};
+    static const int cand16_gemm[][2] = {{7, 1}, {3, 1}, {1, 2}, {2, 3}};
+    static const int cand32[][2] = {{2, 3}};
+    const int (*cand)[2] = !sixteen ? cand32 : (conv ? cand16_conv : cand16_gemm);
+    const int ncand = !sixteen ? 1 : 4;
+    WPlan best{2, 1, false};
+    double bt = 1e30;
+    for (int i = 0; i < ncand; ++i) {
+        const TileCfg* c = find_cfg(cand[i][0]);
+        if (N % c->bn) continue;
+        for (int sp = 1; sp <= 128; ++sp) {
+            if (nk % sp || nk / sp < 8) continue;
+            if (ntiles(M, N, c->bm, c->bn) * sp > 4L * NUM_CU) break;
+            const double t = wplan_cost(*c, cand[i][1], eb, M, N, K, sp);
+            if (t < bt * 0.98) { bt = t; best = WPlan{c->id, sp, sp > 2}; }
+        }
+    }
+    return best;
+}
+size_t wplan_ws(const WPlan& w, int M, int N) {
+    if (w.splits <= 1) return 0;
+    const TileCfg* c = find_cfg(w.cfg);
+    if (w.partials) return GEMM_CNT_BYTES + (size_t)w.splits * M * N * 4;
+    return GEMM_CNT_BYTES + (size_t)w.splits * ntiles(M, N, c->bm, c->bn) * c->bm * c->bn * 4;
+}
+// C[e] = sum over splits of part[split][e] (split order), f32, 4 per thread
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, float* __restrict__ C, long MN,
+                                                            int splits)
+{
+    const long e = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (e >= MN) return;
+    float4 acc = *reinterpret_cast<const float4*>(part + e);
+    for (int sp = 1; sp < splits; ++sp) {
+        const float4 v = *reinterpret_cast<const float4*>(part + (size_t)sp * MN + e);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *reinterpret_cast<float4*>(C + e) = acc;
+}
+int splitk_reduce(const float* part, float* C, long MN, int splits, hipStream_t st) {
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, st, part, C, MN, splits);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
 int forced_conv_cfg() { static const int v = env_int("EBC_CONV_CFG"); return v; }
 int conv_cfg(bool sixteen, int mode, int M, int N)
 {
@@ -902,12 +993,23 @@ template <class E>
 int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream_t st)
 {
     constexpr bool SIXTEEN = E::BYTES == 2;
-    const int cfg = conv_cfg(SIXTEEN, mode, g.M, g.N);
+    const bool planned = mode == 2 && !forced_conv_cfg() && !forced_conv_splits();
+    const WPlan wp = planned ? wgrad_plan(SIXTEEN, true, g.M, g.N, g.K) : WPlan{0, 1, false};
+    const int cfg = planned ? wp.cfg : conv_cfg(SIXTEEN, mode, g.M, g.N);
     const int BK = cfg >= 20 ? 32 : 128 / E::BYTES;           // 64-B K rows for the 4-stage rings
     const TileCfg* c = find_cfg(cfg);
     if (g.N % c->bn || g.K % BK) return EBC_E_UNSUPPORTED;
     if (mode == 2) g.kpi *= (128 / E::BYTES) / BK;             // geometry counts 128-B k-tiles
-    int splits = conv_splits(cfg, mode, g.M, g.N, g.K / BK);
+    if (planned && wp.partials) {
+        if (!ws || wsb < wplan_ws(wp, g.M, g.N)) return EBC_E_ARG;
+        g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
+        g.cnt = nullptr;
+        g.splits = wp.splits;
+        g.kslice = g.K / wp.splits;
+        EBC_TRY((launch_conv_tile<E, float, EPI_STORE, 2>(g, cfg, st)));
+        return splitk_reduce(g.part, reinterpret_cast<float*>(g.C), (long)g.M * g.N, wp.splits, st);
+    }
+    int splits = planned ? wp.splits : conv_splits(cfg, mode, g.M, g.N, g.K / BK);
     if (splits > 1) {
         const size_t tiles = (size_t)ntiles(g.M, g.N, c->bm, c->bn);
         const size_t need = GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
@@ -934,11 +1036,13 @@ namespace ebc {
 size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K)
 {
     const bool sixteen = dtype != EBC_F32;
+    size_t need = GEMM_CNT_BYTES;
+    if (mode == 1) need += (size_t)((M + 127) / 128) * 2 * N * 4;     // EPI_STATS partials (BM >= 128)
+    if (mode == 2 && !forced_conv_cfg() && !forced_conv_splits())
+        return std::max(need, wplan_ws(wgrad_plan(sixteen, true, M, N, K), M, N));
     const int cfg = conv_cfg(sixteen, mode, M, N);
     const TileCfg* c = find_cfg(cfg);
     const int bk = !sixteen ? 32 : (cfg >= 20 ? 32 : 64);
-    size_t need = GEMM_CNT_BYTES;
-    if (mode == 1) need += (size_t)((M + 127) / 128) * 2 * N * 4;     // EPI_STATS partials (BM >= 128)
     const int s = conv_splits(cfg, mode, M, N, K / bk);
     if (s > 1) need = std::max(need, GEMM_CNT_BYTES + (size_t)s * ntiles(M, N, c->bm, c->bn) * c->bm * c->bn * 4);
     return need;
@@ -1001,32 +1105,38 @@ int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void*
 }  // namespace ebc
 
 namespace {
-// weight-gradient GEMM: 128x64 tiles, K split so that the grid is about one wave of CUs
-int wgrad_splits(int M, int N, int K, int bk) {
-    const long tiles = ntiles(M, N, 128, 64);
-    const int nk = K / bk;
-    int s = 1;
-    for (int c = 2; c <= 16; ++c)
-        if (tiles * c <= NUM_CU * 6 / 5 && nk % c == 0 && nk / c >= 8) s = c;
-    return s;
-}
-size_t wgrad_ws(int M, int N, int K, int bk) {
-    const int s = wgrad_splits(M, N, K, bk);
-    return s > 1 ? GEMM_CNT_BYTES + (size_t)s * ntiles(M, N, 128, 64) * 128 * 64 * 4 : 0;
+// weight-gradient GEMM (1x1 conv dW over K = pixels): tile and split-K from wgrad_plan
+size_t wgrad_ws(int M, int N, int K, bool sixteen) {
+    return wplan_ws(wgrad_plan(sixteen, false, M, N, K), M, N);
 }
 template <class E>
 int wgrad_launch(GemmArgs g, void* ws, size_t wsb, hipStream_t st) {
-    constexpr int bk = 128 / E::BYTES;
-    int s = wgrad_splits(g.M, g.N, g.K, bk);
-    if (s > 1 && (!ws || wsb < wgrad_ws(g.M, g.N, g.K, bk) || ntiles(g.M, g.N, 128, 64) > (long)(GEMM_CNT_BYTES / 4)))
+    constexpr bool SIXTEEN = E::BYTES == 2;
+    const WPlan wp = wgrad_plan(SIXTEEN, false, g.M, g.N, g.K);
+    const TileCfg* c = find_cfg(wp.cfg);
+    const int s = wp.splits;
+    if (s > 1 && (!ws || wsb < wplan_ws(wp, g.M, g.N) || (!wp.partials && ntiles(g.M, g.N, c->bm, c->bn) > (long)(GEMM_CNT_BYTES / 4))))
         return EBC_E_ARG;
     if (s > 1) {
-        g.cnt = reinterpret_cast<int*>(ws);
+        g.cnt = wp.partials ? nullptr : reinterpret_cast<int*>(ws);
         g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
     }
     g.splits = s;
     g.kslice = g.K / s;
-    return launch_gemm<E, float, EPI_STORE, 128, 64, 2>(g, st);
+    g.group_m = 0;
+    int rc = EBC_E_UNSUPPORTED;
+    if constexpr (SIXTEEN) {
+        switch (wp.cfg) {
+            case 7: rc = launch_gemm<E, float, EPI_STORE, 256, 256, 2, 4, 2>(g, st); break;
+            case 3: rc = launch_gemm<E, float, EPI_STORE, 256, 192, 2, 4, 2>(g, st); break;
+            case 1: rc = launch_gemm<E, float, EPI_STORE, 128, 128, 2>(g, st); break;
+            default: rc = launch_gemm<E, float, EPI_STORE, 128, 64, 2>(g, st); break;
+        }
+    } else {
+        rc = launch_gemm<E, float, EPI_STORE, 128, 64, 2>(g, st);
+    }
+    if (rc || !(s > 1 && wp.partials)) return rc;
+    return splitk_reduce(g.part, reinterpret_cast<float*>(g.C), (long)g.M * g.N, s, st);
 }
 
 // out[c][r] = in[r][c]: 64x64 tiles through LDS, 8-element (16 B for 16-bit) vectors both ways
@@ -1064,7 +1174,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in
 extern "C" size_t ebc_gemm_wgrad_workspace_bytes(int dtype, int M, int N, int K)
 {
     if (M <= 0 || N <= 0 || K <= 0) return 0;
-    return wgrad_ws(M, N, K, dtype == EBC_F32 ? 32 : 64);
+    return wgrad_ws(M, N, K, dtype != EBC_F32);
 }
 
 extern "C" int ebc_gemm_wgrad(int dtype, const void* A, const void* B, float* C, int M, int N, int K,
@@ -1138,6 +1248,12 @@ extern "C" int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, in
 {
     if (M <= 0 || N <= 0 || K <= 0 || (mode != 1 && mode != 2)) return EBC_E_ARG;
     const bool sixteen = dtype != EBC_F32;
+    if (mode == 2 && !forced_conv_cfg() && !forced_conv_splits()) {
+        const WPlan wp = wgrad_plan(sixteen, true, M, N, K);
+        const TileCfg* c = find_cfg(wp.cfg);
+        if (out) { out[0] = c->bm; out[1] = c->bn; out[2] = wp.splits; }
+        return wp.cfg;
+    }
     const int cfg = conv_cfg(sixteen, mode, M, N);
     const TileCfg* c = find_cfg(cfg);
     if (out) {
