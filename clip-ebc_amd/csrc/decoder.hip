@@ -68,6 +68,11 @@ template <class T> __device__ __forceinline__ void st8(T* p, const float* v) {
     *reinterpret_cast<t8*>(p) = x;
 }
 __device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+// 8 consecutive per-channel f32 parameters (two 16-B loads; c a multiple of 8)
+__device__ __forceinline__ void ldp8(const float* p, float* v) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 __device__ __forceinline__ float4 fma4(float4 a, float4 b, float4 c) {
     return make_float4(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z), fmaf(a.w, b.w, c.w));
 }
@@ -358,14 +363,16 @@ __global__ __launch_bounds__(256) void bn_add_relu_flat_kernel(const T* __restri
     const long p = e / C8;
     const int c = (int)(e - p * C8) * 8;
     const size_t off = (size_t)p * C + c;
-    float zv[8], iv[8];
+    float zv[8], iv[8], sc[8], sh[8], isc[8], ish[8];
     ld8(z + off, zv);
     ld8(idt + off, iv);
+    ldp8(scale + c, sc); ldp8(shift + c, sh);
+    if (iscale) { ldp8(iscale + c, isc); ldp8(ishift + c, ish); }
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const float idn = iscale ? fmaf(iv[i], iscale[c + i], ishift[c + i]) : iv[i];
-        o[i] = fmaxf(fmaf(zv[i], scale[c + i], shift[c + i]) + idn, 0.f);
+        const float idn = iscale ? fmaf(iv[i], isc[i], ish[i]) : iv[i];
+        o[i] = fmaxf(fmaf(zv[i], sc[i], sh[i]) + idn, 0.f);
     }
     st8(y + off, o);
 }
@@ -510,13 +517,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_flat_kernel(const T* __restr
     ld8(gy + off, gv);
     ld8(z + off, zv);
     if (HAS_MY) ld8(my + off, mv);
+    float k0[8], k1[8], k2[8], mu[8], rs[8], sc[8], sh[8];
+    ldp8(coef + c, k0); ldp8(coef + C + c, k1); ldp8(coef + 2 * C + c, k2); ldp8(mean + c, mu); ldp8(rstd + c, rs);
+    if (!HAS_MY) { ldp8(scale + c, sc); ldp8(shift + c, sh); }
     float v[8], gm[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const int cc = c + i;
-        const float m = HAS_MY ? mv[i] : fmaf(zv[i], scale[cc], shift[cc]);
+        const float m = HAS_MY ? mv[i] : fmaf(zv[i], sc[i], sh[i]);
         gm[i] = m > 0.f ? gv[i] : 0.f;
-        v[i] = coef[cc] * (gm[i] - coef[C + cc] - (zv[i] - mean[cc]) * rstd[cc] * coef[2 * C + cc]);
+        v[i] = k0[i] * (gm[i] - k1[i] - (zv[i] - mu[i]) * rs[i] * k2[i]);
     }
     st8(dz + off, v);
     if (gmask) {
@@ -699,6 +708,29 @@ __global__ __launch_bounds__(256) void prep_weights_kernel(const float* __restri
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = sm[ov + i][cl * 9 + 8 - tap];
         st8(wf + ((size_t)(c0 + cl) * 9 + tap) * N + o0 + ov, x);
+    }
+}
+
+// 1x1 conv weight [N][K] f32 -> wk [N][K] and its transpose wt [K][N] in the compute dtype (the GEMM's forward
+// and data-gradient operands), 32x32 tiles through LDS
+template <class T>
+__global__ __launch_bounds__(256) void prep_weights_1x1_kernel(const float* __restrict__ w, T* __restrict__ wk,
+                                                               T* __restrict__ wt, int N, int K)
+{
+    __shared__ float sm[32][33];
+    const int n0 = blockIdx.x * 32, k0 = blockIdx.y * 32, t = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int nl = r * 8 + t / 32, kl = t % 32;
+        const float v = w[(size_t)(n0 + nl) * K + k0 + kl];
+        sm[nl][kl] = v;
+        wk[(size_t)(n0 + nl) * K + k0 + kl] = (T)v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int kl = r * 8 + t / 32, nl = t % 32;
+        wt[(size_t)(k0 + kl) * N + n0 + nl] = (T)sm[nl][kl];
     }
 }
 
@@ -1060,6 +1092,16 @@ extern "C" int ebc_bn_add_relu_flat(int dtype, const void* z, const float* scale
     EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(bn_add_relu_flat_kernel<T>, dim3(nblk(P * (C / 8))), dim3(256), 0,
                                                (hipStream_t)stream, (const T*)z, scale, shift, (const T*)idt, iscale,
                                                ishift, (T*)y, P, C));
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+extern "C" int ebc_prep_weights_1x1(int dtype, const float* w, void* wk, void* wt, int N, int K, ebc_stream_t stream)
+{
+    if (!w || !wk || !wt || N <= 0 || K <= 0 || N % 32 || K % 32) return EBC_E_ARG;
+    const dim3 grid((unsigned)(N / 32), (unsigned)(K / 32));
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(prep_weights_1x1_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, w,
+                                               (T*)wk, (T*)wt, N, K));
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

@@ -103,6 +103,7 @@ SIGNATURES = {
     "ebc_avgpool2": (_I, [_I, _I, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_avgpool2_bwd": (_I, [_I, _I, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_bn_add_relu_flat": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "ebc_prep_weights_1x1": (_I, [_I, _P, _P, _P, _I, _I, _P]),
     "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, EbcAugConst, _P]),
     "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "ebc_probe_begin": (_I, [_I]),

@@ -657,7 +657,7 @@ class CLIP_EBC(nn.Module):
     def _forward_resnet(self, x: Tensor, cdt: torch.dtype) -> Union[Tensor, Tuple[Tensor, Tensor]]:
         """models/clip/model.py:191-217 for the resnet50 backbone: the trainable ModifiedResNet (stem on PyTorch-ROCm,
         its 16 Bottlenecks on HIP), then the HIP Bottleneck decoder and head."""
-        from .resnet import _BottleneckFn, encoder_forward
+        from .resnet import _BottleneckFn, encoder_forward, flush_bn_counters
         if _RN50_TORCH_ENCODER:                                              # A/B: the whole encoder on MIOpen
             feat = self.image_encoder(x.contiguous(memory_format=torch.channels_last)).permute(0, 2, 3, 1)
         else:                                                                # stem on MIOpen, 16 blocks on HIP
@@ -671,6 +671,7 @@ class CLIP_EBC(nn.Module):
                                     cdt, self.training)
             logits, exp = _HeadFn.apply(y, self.projection.weight, self.projection.bias, self.logit_scale,
                                         self.text_features, self._anchors, cdt, True)
+        flush_bn_counters()
         return (logits, exp) if self.training else exp
 
     def forward(self, x: Tensor) -> Union[Tensor, Tuple[Tensor, Tensor]]:

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import ctypes
 from collections import OrderedDict
-from typing import Any, Optional, Tuple
+from typing import Any, List, Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -143,7 +143,10 @@ def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, 
     mean, rstd, scale, shift = (torch.empty(N, **f32) for _ in range(4))
     upd = use_batch and training and bn.track_running_stats
     if upd:
-        bn.num_batches_tracked.add_(1)
+        if bn.momentum is None:                    # cumulative average: the factor needs the updated count now
+            bn.num_batches_tracked.add_(1)
+        else:
+            _PENDING_NBT.append(bn.num_batches_tracked)
     mom = _bn_momentum(bn) if upd else 0.0
     _lib.check(L.ebc_bn_finalize(_lib.ptr(colsum) if use_batch else None, count, float(bn.eps), mom,
                                  _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()), _lib.ptr(mean),
@@ -174,6 +177,27 @@ def _batch_norm_bwd(L, gamma: Tensor, state, dnext: Tensor, mask: Optional[Tenso
         _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, g, _lib.ptr(rstd), None, None, _lib.ptr(coef), N, st),
                    "ebc_bn_bwd_finalize(sync)")
     return dg, db, coef
+
+
+def _prep_1x1(L, w: Tensor, cdtype: torch.dtype, st) -> Tuple[Tensor, Tensor]:
+    """1x1 conv weight [N, K, 1, 1] f32 -> ([N, K], [K, N]) in the compute dtype, one launch (ebc_prep_weights_1x1)."""
+    N, K = w.shape[0], w.shape[1]
+    wk = torch.empty(N, K, device=w.device, dtype=cdtype)
+    wt = torch.empty(K, N, device=w.device, dtype=cdtype)
+    _lib.check(L.ebc_prep_weights_1x1(_lib.dtype_code(cdtype), _lib.ptr(w.detach().float().contiguous()), _lib.ptr(wk),
+                                      _lib.ptr(wt), N, K, st), "ebc_prep_weights_1x1")
+    return wk, wt
+
+
+# BatchNorm num_batches_tracked increments of one forward, applied by ONE foreach launch (flush_bn_counters)
+# instead of one add kernel per BatchNorm (56 per clip_resnet50 step)
+_PENDING_NBT: List[Tensor] = []
+
+
+def flush_bn_counters() -> None:
+    if _PENDING_NBT:
+        torch._foreach_add_(_PENDING_NBT, 1)
+        _PENDING_NBT.clear()
 
 
 def _ws(L, dev, dt, B, H, W, C, N, P, Cmax):
@@ -223,11 +247,9 @@ class _ResBlockFn(torch.autograd.Function):
                 _lib.check(L.ebc_bn_stats(dt, _lib.ptr(z), _lib.ptr(cs), _lib.ptr(ws), ws.numel(), rows, C, st), "ebc_bn_stats")
             return _batch_norm_fwd(L, bn, cs, rows, C, training, dev, st)
 
-        def mat(w, n, k):
-            return w.detach().reshape(n, k).to(cdtype).contiguous()
-
-        W1, W3 = mat(wts[0], planes, Cin), mat(wts[2], Cout, planes)
-        Wd = mat(wts[3], Cout, Cin) if down else None
+        W1, W1t = _prep_1x1(L, wts[0], cdtype, st)
+        W3, W3t = _prep_1x1(L, wts[2], cdtype, st)
+        Wd, Wdt = _prep_1x1(L, wts[3], cdtype, st) if down else (None, None)
         geo = (ctypes.c_long * 6)()
         _lib.check(L.ebc_dec_geometry(dt, B, H, W, planes, geo), "ebc_dec_geometry")
         Q = geo[4]
@@ -277,7 +299,7 @@ class _ResBlockFn(torch.autograd.Function):
         _lib.check(L.ebc_bn_add_relu_flat(dt, _lib.ptr(z3), _lib.ptr(s3[2]), _lib.ptr(s3[3]),
                                           _lib.ptr(zd if down else x), _lib.ptr(sd[2]) if down else None,
                                           _lib.ptr(sd[3]) if down else None, _lib.ptr(y), Po, Cout, st), "ebc_bn_add_relu_flat")
-        ctx.save_for_backward(x, z1, h1pad, z2, h2p, z3, y, W1, wf2, W3, *(() if not down else (xd, zd, Wd)))
+        ctx.save_for_backward(x, z1, h1pad, z2, h2p, z3, y, W1t, wf2, W3t, *(() if not down else (xd, zd, Wdt)))
         ctx.states = (s1, s2, s3, sd)
         ctx.gammas = tuple(bn.weight for bn in bns)
         ctx.meta = (B, H, W, Cin, s, Ho, Wo, P, Po, planes, Cout, down, cdtype, x.dtype)
@@ -294,8 +316,8 @@ class _ResBlockFn(torch.autograd.Function):
         L = _lib.lib()
         B, H, W, Cin, s, Ho, Wo, P, Po, planes, Cout, down, cdtype, xdt = ctx.meta
         saved = ctx.saved_tensors
-        x, z1, h1pad, z2, h2p, z3, y, W1, wf2, W3 = saved[:10]
-        xd, zd, Wd = saved[10:] if down else (None, None, None)
+        x, z1, h1pad, z2, h2p, z3, y, W1t, wf2, W3t = saved[:10]
+        xd, zd, Wdt = saved[10:] if down else (None, None, None)
         s1, s2, s3, sd = ctx.states
         g1, g2, g3 = ctx.gammas[:3]
         dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream(y)
@@ -320,7 +342,7 @@ class _ResBlockFn(torch.autograd.Function):
         dz3 = apply_flat(gy, y, z3, s3, coef3, gid)
         dw3 = _wgrad_rows(L, dz3, h2p, cdtype, dev, st)
         dh2p = torch.empty(Po, planes, device=dev, dtype=cdtype)
-        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dz3), _lib.ptr(W3.t().contiguous()), _lib.ptr(dh2p), None, None, None,
+        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dz3), _lib.ptr(W3t), _lib.ptr(dh2p), None, None, None,
                               Po, planes, Cout, st), "ebc_gemm(conv3 dX)")
         del dz3
         dwd = dgd = dbd = None
@@ -330,7 +352,7 @@ class _ResBlockFn(torch.autograd.Function):
             dzd = apply_flat(gy, y, zd, sd, coefd)
             dwd = _wgrad_rows(L, dzd, xd, cdtype, dev, st)
             dxd = torch.empty(Po, Cin, **f32)
-            _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(dzd), _lib.ptr(Wd.t().contiguous()), _lib.ptr(dxd), None, None, None,
+            _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(dzd), _lib.ptr(Wdt), _lib.ptr(dxd), None, None, None,
                                   Po, Cin, Cout, st), "ebc_gemm(downsample dX)")
             del dzd
             if s > 1:
@@ -370,7 +392,7 @@ class _ResBlockFn(torch.autograd.Function):
         del dh1
         dw1 = _wgrad_rows(L, dz1, x.view(P, Cin), cdtype, dev, st)
         dx = torch.empty(B, H, W, Cin, device=dev, dtype=cdtype)
-        _lib.check(L.ebc_gemm(dt, 2, 0, _lib.ptr(dz1), _lib.ptr(W1.t().contiguous()), _lib.ptr(dx), None, _lib.ptr(gid),
+        _lib.check(L.ebc_gemm(dt, 2, 0, _lib.ptr(dz1), _lib.ptr(W1t), _lib.ptr(dx), None, _lib.ptr(gid),
                               None, P, Cin, planes, st), "ebc_gemm(conv1 dX + identity)")
         ctx.states = None
         return (dx.to(xdt) if xdt != cdtype else dx, dw1.view(planes, Cin, 1, 1), dw2, dw3.view(Cout, planes, 1, 1),
@@ -395,6 +417,7 @@ def encoder_forward(enc: "ModifiedResNet", x: Tensor, cdtype: torch.dtype, train
                                       None if d is None else d[1].weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
                                       blk.bn2.bias, blk.bn3.weight, blk.bn3.bias, None if d is None else d[2].weight,
                                       None if d is None else d[2].bias, blk, cdtype, training)
+    flush_bn_counters()
     return h
 
 
@@ -434,8 +457,8 @@ class _BottleneckFn(torch.autograd.Function):
 
         x = torch.empty(P, C, device=dev, dtype=cdtype)
         _lib.check(L.ebc_dec_upsample(dt, _lib.ptr(feat), _lib.ptr(x), B, h, w, C, up, st), "ebc_dec_upsample")
-        W1 = wts[0].detach().reshape(N, C).to(cdtype).contiguous()
-        W3 = wts[2].detach().reshape(N, N).to(cdtype).contiguous()
+        W1, W1t = _prep_1x1(L, wts[0], cdtype, st)
+        W3, W3t = _prep_1x1(L, wts[2], cdtype, st)
         wk2 = torch.empty(N, 3, 3, N, device=dev, dtype=cdtype)
         wf2 = torch.empty(N, 3, 3, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_dec_prep_weights(dt, _lib.ptr(wts[1].detach().float().contiguous()), _lib.ptr(wk2),
@@ -471,7 +494,7 @@ class _BottleneckFn(torch.autograd.Function):
         y = torch.empty(B, H, W, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_bn_add_relu(dt, _lib.ptr(z3), _lib.ptr(s3[2]), _lib.ptr(s3[3]), _lib.ptr(feat), up, _lib.ptr(y),
                                      B, H, W, N, st), "ebc_bn_add_relu")
-        ctx.save_for_backward(x, z1, h1pad, z2, h2, z3, y, W1, wf2, W3, *gammas)
+        ctx.save_for_backward(x, z1, h1pad, z2, h2, z3, y, W1t, wf2, W3t, *gammas)
         ctx.states = (s1, s2, s3)
         ctx.meta = (B, h, w, H, W, C, N, up, cdtype, P)
         return y
@@ -485,7 +508,7 @@ class _BottleneckFn(torch.autograd.Function):
     def _backward(ctx, gy):
         from .model import _dec_workspace, _wgrad_rows
         L = _lib.lib()
-        x, z1, h1pad, z2, h2, z3, y, W1, wf2, W3, g1, g2, g3 = ctx.saved_tensors
+        x, z1, h1pad, z2, h2, z3, y, W1t, wf2, W3t, g1, g2, g3 = ctx.saved_tensors
         s1, s2, s3 = ctx.states
         B, h, w, H, W, C, N, up, cdtype, P = ctx.meta
         dev, dt, st = y.device, _lib.dtype_code(cdtype), _lib.stream(y)
@@ -505,7 +528,7 @@ class _BottleneckFn(torch.autograd.Function):
         # conv3: dW3 = dz3^T h2, dh2 = dz3 W3
         dw3 = _wgrad_rows(L, dz3, h2, cdtype, dev, st)
         dh2 = torch.empty(P, N, device=dev, dtype=cdtype)
-        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dz3), _lib.ptr(W3.t().contiguous()), _lib.ptr(dh2), None, None, None,
+        _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dz3), _lib.ptr(W3t), _lib.ptr(dh2), None, None, None,
                               P, N, N, st), "ebc_gemm(conv3 dX)")
         del dz3
         # bn2 (+ relu through h2) -> padded / transposed dz2 for the 3x3 conv's gradients
@@ -537,7 +560,7 @@ class _BottleneckFn(torch.autograd.Function):
         del dh1
         # conv1: dW1 = dz1^T x, dx = dz1 W1 + the identity branch's gradient (f32, in place over gid)
         dw1 = _wgrad_rows(L, dz1, x, cdtype, dev, st)
-        _lib.check(L.ebc_gemm(dt, 2, 1, _lib.ptr(dz1), _lib.ptr(W1.t().contiguous()), _lib.ptr(gid), None,
+        _lib.check(L.ebc_gemm(dt, 2, 1, _lib.ptr(dz1), _lib.ptr(W1t), _lib.ptr(gid), None,
                               _lib.ptr(gid), None, P, C, N, st), "ebc_gemm(conv1 dX + identity)")
         dfeat = torch.empty(B, h, w, C, device=dev, dtype=torch.float32)
         _lib.check(L.ebc_dec_upsample_bwd(_lib.EBC_F32, _lib.ptr(gid), _lib.ptr(dfeat), B, h, w, C, up, st),

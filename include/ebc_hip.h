@@ -321,6 +321,9 @@ int ebc_avgpool2(int dtype_in, int dtype_out, const void* x, void* out, int B, i
 int ebc_avgpool2_bwd(int dtype_in, int dtype_out, const void* g, void* gx, int B, int H, int W, int C, ebc_stream_t stream);
 int ebc_bn_add_relu_flat(int dtype, const void* z, const float* scale, const float* shift, const void* idt,
                          const float* iscale, const float* ishift, void* y, long P, int C, ebc_stream_t stream);
+/* 1x1 conv weight [N][K] f32 (nn.Conv2d [N][K][1][1]) -> wk [N][K] and wt [K][N] in dtype (the GEMM operands of the
+ * forward and of the data gradient), one launch; N, K multiples of 32 */
+int ebc_prep_weights_1x1(int dtype, const float* w, void* wk, void* wt, int N, int K, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Measurement (bench.py): in-step kernel durations and profile windows.  Not on the reference's

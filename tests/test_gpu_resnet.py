@@ -56,7 +56,7 @@ def _block(C, seed, dev):
 @pytest.mark.parametrize("dtype,B,h,C,up", [(torch.float32, 2, 7, 256, 2), (torch.float32, 3, 7, 256, 1),
                                             (torch.bfloat16, 2, 7, 256, 2), (torch.float16, 2, 8, 512, 2)])
 def test_bottleneck_fn_matches_torch(dtype, B, h, C, up):
-    from ebc_amd.resnet import _BottleneckFn
+    from ebc_amd.resnet import _BottleneckFn, flush_bn_counters
     dev = torch.device("cuda")
     blk = _block(C, 3, dev)
     g = torch.Generator(device="cuda").manual_seed(5)
@@ -65,6 +65,7 @@ def test_bottleneck_fn_matches_torch(dtype, B, h, C, up):
     params = [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
               blk.bn2.bias, blk.bn3.weight, blk.bn3.bias]
     y = _BottleneckFn.apply(featp, *params, blk, up, dtype, True)
+    flush_bn_counters()
     gy = torch.randn(y.shape, device=dev, generator=g)
     y.float().backward(gy)
     torch.cuda.synchronize()
@@ -298,7 +299,7 @@ def _block_params(blk):
 def test_encoder_block_matches_torch(dtype, cin, planes, stride, B, H):
     """ModifiedResNet Bottleneck (blocks.py:56-101) on HIP vs the same module in float64 (training-mode BatchNorm):
     output, input gradient, every parameter gradient, running statistics."""
-    from ebc_amd.resnet import _ResBlockFn
+    from ebc_amd.resnet import _ResBlockFn, flush_bn_counters
     dev = torch.device("cuda")
     blk = _enc_block(cin, planes, stride, 7, dev)
     ref = _enc_block(cin, planes, stride, 7, dev).double()
@@ -306,6 +307,7 @@ def test_encoder_block_matches_torch(dtype, cin, planes, stride, B, H):
     x = torch.randn(B, H, H, cin, device=dev, generator=g)
     xh = x.to(dtype).clone().requires_grad_(True)
     y = _ResBlockFn.apply(xh, *_block_params(blk), blk, dtype, True)
+    flush_bn_counters()
     gy = torch.randn(y.shape, device=dev, generator=g)
     y.float().backward(gy)
     torch.cuda.synchronize()
