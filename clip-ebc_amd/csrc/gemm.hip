@@ -51,6 +51,9 @@ struct GemmArgs {
     float* stats = nullptr;  // EPI_STATS: [ceil(M/BM)][2][N] per-tile column sums / sums of squares
     int group_m = 0;         // > 1: tiles ordered in groups of group_m tile rows, column-major inside a group
     const void* aux2 = nullptr;   // EPI_ADD_RELU_GRAD: ReLU output y (mask y > 0): C = acc + gy * (y > 0)
+    // a launch covers output tiles [tile0, tile0 + ntile) (ntile 0: through the last); split-K partials and
+    // arrival counters are indexed from tile0
+    int tile0 = 0, ntile = 0;
 };
 
 // Slab rows are ROWB bytes (one BK-deep K slice): 128 (BK = 64 for 16-bit, 32 for f32) or 64
@@ -198,8 +201,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WGN, wn = wave % WGN;
     const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
-    const int wg = xcd_remap(blockIdx.x, ntm * ntn * g.splits);
-    const int tile = wg / g.splits, split = wg - tile * g.splits;   // a tile's splits are adjacent
+    const int wg = xcd_remap(blockIdx.x, (int)gridDim.x);
+    const int ltile = wg / g.splits, split = wg - ltile * g.splits;   // a tile's splits are adjacent
+    const int tile = g.tile0 + ltile;
     int tm = tile / ntn, tn = tile % ntn;
     if (g.group_m > 1) {
         // each XCD's contiguous run of tiles (xcd_remap) then covers a group_m-tall block of tile rows and a
@@ -474,7 +478,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         constexpr int PT = NW * TM * TN * 64;     // f32x4 per partial tile
         // one buffer resource over this tile's `splits` partials; aux 16 = sc1
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<f32x4*>(g.part) + (size_t)tile * g.splits * PT, 0, 0x7fffffff, 0x00020000);
+            reinterpret_cast<f32x4*>(g.part) + (size_t)ltile * g.splits * PT, 0, 0x7fffffff, 0x00020000);
         // MI355X_MICROARCH.md cross-CU hand-off, sc1 form: sc1 (write-through) 16-B stores, every
         // wave's vmcnt(0), a barrier, ONE agent-scope atomic add; the last adder's waves read with
         // sc1 loads after a barrier.  No agent fences (a buffer_wbl2 per workgroup costs ~microseconds).
@@ -488,7 +492,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         __shared__ int last;
-        if (tid == 0) last = atomicAdd(&g.cnt[tile], 1) == g.splits - 1;
+        if (tid == 0) last = atomicAdd(&g.cnt[ltile], 1) == g.splits - 1;
         __syncthreads();
         if (!last) return;
         // bit-reproducible sum whichever split arrives last: two splits add the other's partial (f32
@@ -510,7 +514,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
                 for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
             for (int sp = 0; sp < g.splits; ++sp) add_partial(sp);
         }
-        if (tid == 0) atomicExch(&g.cnt[tile], 0);   // re-armed for the next launch
+        if (tid == 0) atomicExch(&g.cnt[ltile], 0);   // re-armed for the next launch
     }
 
     if constexpr (MODE == 0) {
@@ -706,7 +710,9 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
         attr = true;
     }
     if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
-    const int nwg = ((g.M + BM - 1) / BM) * (g.N / BN) * g.splits;
+    const int tiles = g.ntile ? g.ntile : ((g.M + BM - 1) / BM) * (g.N / BN) - g.tile0;
+    if (tiles <= 0 || g.tile0 + tiles > ((g.M + BM - 1) / BM) * (g.N / BN)) return EBC_E_ARG;
+    const int nwg = tiles * g.splits;
     const int pi = probe_on() ? probe_start(EBC_PROBE_GEMM, EPI, BM, BN, MODE, g.M, g.N, g.K, st) : -1;
     hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
     probe_stop(pi, st);
@@ -978,6 +984,35 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
     return N % 96 == 0 ? 13 : 2;
 }
 int forced_conv_splits() { static const int v = env_int("EBC_CONV_SPLITS"); return v; }
+// Split-K tail for the implicit-GEMM convolutions (MODE 1, one 256-wide workgroup per CU): when T tiles are a few
+// more than whole waves (the ResNet-50 decoder: 784 = 3 x 256 + 16 tiles of 256x256), the T mod 256 last tiles
+// would run as a fourth, nearly empty wave of whole-K tiles.  Instead the whole waves run as one launch and the
+// tail tiles as a second with K split s ways (last arriver sums the f32 partials in split order), s from the
+// same fill / MFMA cost model as the weight-gradient plans plus the last arriver's re-read.  EBC_CONV_TAIL=0: off.
+struct TailPlan { int dp, tail, splits; };
+TailPlan tail_plan(int cfg, int M, int N, int K, int bk) {
+    static const int off = getenv("EBC_CONV_TAIL") && atoi(getenv("EBC_CONV_TAIL")) == 0;
+    if (off || (cfg != 3 && cfg != 7)) return TailPlan{0, 0, 1};
+    const TileCfg* c = find_cfg(cfg);
+    const long T = ntiles(M, N, c->bm, c->bn), R = T % NUM_CU, kit = K / bk;
+    if (T < NUM_CU || R == 0 || R > (long)(GEMM_CNT_BYTES / 4)) return TailPlan{0, 0, 1};
+    auto piece = [&](double k) { return std::max((c->bm + c->bn) * k * 2 / 70e9, 2.0 * c->bm * c->bn * k / 8e12); };
+    double best = piece(K);
+    int bs = 1;
+    for (int sp = 2; sp <= 64; ++sp) {
+        if (kit % sp || R * sp > NUM_CU || kit / sp < 8) continue;
+        const double t = piece((double)K / sp) + (double)sp * c->bm * c->bn * 4 / 70e9 + 4e-6;
+        if (t < best) { best = t; bs = sp; }
+    }
+    if (bs == 1) return TailPlan{0, 0, 1};
+    return TailPlan{(int)(T - R), (int)R, bs};
+}
+// conv workspace: [arrival counters][EPI_STATS per-tile-row partials (BM >= 128)][split-K tail partials]
+size_t conv_stats_bytes(int M, int N) { return (((size_t)((M + 127) / 128) * 2 * N * 4 + 255) / 256) * 256; }
+size_t tail_ws_bytes(int cfg, const TailPlan& p) {
+    const TileCfg* c = find_cfg(cfg);
+    return p.splits > 1 ? (size_t)p.tail * p.splits * c->bm * c->bn * 4 : 0;
+}
 int conv_splits(int cfg, int mode, int M, int N, int nk)
 {
     if (mode != 2) return 1;
@@ -1023,6 +1058,27 @@ int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream
     g.splits = splits;
     g.kslice = g.K / splits;
     using T = typename E::T;
+    if (mode == 1 && SIXTEEN && splits == 1) {
+        const TailPlan tp = tail_plan(cfg, g.M, g.N, g.K, BK);
+        const size_t off = GEMM_CNT_BYTES + conv_stats_bytes(g.M, g.N);
+        if (tp.splits > 1 && ws && wsb >= off + tail_ws_bytes(cfg, tp)) {
+            GemmArgs d = g, t = g;
+            d.ntile = tp.dp;
+            t.tile0 = tp.dp;
+            t.ntile = tp.tail;
+            t.splits = tp.splits;
+            t.kslice = g.K / tp.splits;
+            t.cnt = reinterpret_cast<int*>(ws);
+            t.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + off);
+            for (const GemmArgs* a : {&d, &t}) {
+                if (epi == EPI_STORE) EBC_TRY((launch_conv_tile<E, T, EPI_STORE, 1>(*a, cfg, st)));
+                else if (epi == EPI_STATS) EBC_TRY((launch_conv_tile<E, T, EPI_STATS, 1>(*a, cfg, st)));
+                else if (epi == EPI_ADD_RELU_GRAD) EBC_TRY((launch_conv_tile<E, T, EPI_ADD_RELU_GRAD, 1>(*a, cfg, st)));
+                else return EBC_E_UNSUPPORTED;
+            }
+            return EBC_OK;
+        }
+    }
     if (mode == 1 && epi == EPI_STORE) return launch_conv_tile<E, T, EPI_STORE, 1>(g, cfg, st);
     if (mode == 1 && epi == EPI_STATS) return launch_conv_tile<E, T, EPI_STATS, 1>(g, cfg, st);
     if (mode == 1 && epi == EPI_ADD_RELU_GRAD) return launch_conv_tile<E, T, EPI_ADD_RELU_GRAD, 1>(g, cfg, st);
@@ -1037,7 +1093,13 @@ size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K)
 {
     const bool sixteen = dtype != EBC_F32;
     size_t need = GEMM_CNT_BYTES;
-    if (mode == 1) need += (size_t)((M + 127) / 128) * 2 * N * 4;     // EPI_STATS partials (BM >= 128)
+    if (mode == 1) {
+        need += conv_stats_bytes(M, N);                                // EPI_STATS partials (BM >= 128)
+        if (sixteen) {
+            const int cfg = conv_cfg(sixteen, mode, M, N);
+            need += tail_ws_bytes(cfg, tail_plan(cfg, M, N, K, cfg >= 20 ? 32 : 64));
+        }
+    }
     if (mode == 2 && !forced_conv_cfg() && !forced_conv_splits())
         return std::max(need, wplan_ws(wgrad_plan(sixteen, true, M, N, K), M, N));
     const int cfg = conv_cfg(sixteen, mode, M, N);

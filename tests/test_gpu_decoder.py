@@ -124,3 +124,42 @@ def test_conv3x3_abi_matches_torch():
     assert rel_l2(out.float().cpu().numpy(), ref.numpy()) < 2e-3
     np.testing.assert_allclose(colsum[0].cpu().numpy(), ref.sum(0).numpy(), rtol=1e-2, atol=1e-1)
     np.testing.assert_allclose(colsum[1].cpu().numpy(), (ref ** 2).sum(0).numpy(), rtol=2e-3)
+
+
+@pytest.mark.parametrize("B,H,C,N", [(16, 28, 256, 768),    # 196 tiles of 256x192 < 256 CUs: one launch
+                                     (8, 56, 256, 2048),    # 784 tiles of 256x256: 768 whole + 16 split-K tail tiles
+                                     (8, 56, 128, 1024)])   # 392 tiles: 256 whole + 136 tail tiles
+def test_conv3x3_split_tail(B, H, C, N):
+    """ebc_conv3x3_fwd at shapes whose last wave of tiles would leave CUs idle (gemm.hip tail_plan): whole waves in
+    one launch, the tail tiles split-K in a second (last arriver sums the partials), with and without the BN
+    column-sum epilogue, vs torch conv2d."""
+    from ebc_amd import _lib
+    import ctypes
+    L = _lib.lib()
+    W = H
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(B, C, H, W, generator=g, device=dev).half()
+    wt = (torch.randn(N, C, 3, 3, generator=g, device=dev) / (3 * C ** 0.5)).half()
+    geo = (ctypes.c_long * 6)()
+    _lib.check(L.ebc_dec_geometry(_lib.EBC_F16, B, H, W, C, geo), "geo")
+    Hp, Wp, Q = geo[0], geo[1], geo[4]
+    xpad = torch.zeros(B, Hp, Wp, C, device=dev, dtype=torch.float16)
+    xpad[:, 1:H + 1, 1:W + 1] = x.permute(0, 2, 3, 1)
+    xpad = xpad.reshape(Q, C)
+    wk = wt.permute(0, 2, 3, 1).contiguous()
+    ref = F.conv2d(x.float(), wt.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, N).double()
+    ws = torch.zeros(L.ebc_dec_workspace_bytes(_lib.EBC_F16, B, H, W, C, N), dtype=torch.uint8, device=dev)
+    for stats in (True, False):
+        out = torch.empty(B * H * W, N, dtype=torch.float16, device=dev)
+        colsum = torch.empty(2, N, dtype=torch.float64, device=dev)
+        for _ in range(2):                         # twice: the arrival counters must come back re-armed
+            _lib.check(L.ebc_conv3x3_fwd(_lib.EBC_F16, _lib.ptr(xpad), _lib.ptr(wk), _lib.ptr(out),
+                                         _lib.ptr(colsum) if stats else None, None, None, _lib.ptr(ws), ws.numel(),
+                                         B, H, W, C, N, _lib.stream()), "conv")
+        torch.cuda.synchronize()
+        assert rel_l2(out.double(), ref) < 2e-3
+        if stats:
+            torch.testing.assert_close(colsum[0], ref.sum(0), rtol=1e-2, atol=2.0)
+            torch.testing.assert_close(colsum[1], (ref ** 2).sum(0), rtol=3e-3, atol=1.0)
+    assert int(ws[:16384].view(torch.int32).abs().sum()) == 0

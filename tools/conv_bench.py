@@ -25,18 +25,20 @@ def timeit(fn, reps=20):
 
 def main():
     L = _lib.lib()
-    B, H, W, C = int(os.environ.get("CB", 16)), 28, 28, 768
-    dt = _lib.EBC_F16
+    B, H, C = int(os.environ.get("CB", 16)), int(os.environ.get("CH", 28)), int(os.environ.get("CC", 768))
+    W = H
+    dt = _lib.EBC_BF16 if os.environ.get("CDT") == "bf16" else _lib.EBC_F16
+    tdt = torch.bfloat16 if dt == _lib.EBC_BF16 else torch.float16
     geo = (ctypes.c_long * 6)()
     _lib.check(L.ebc_dec_geometry(dt, B, H, W, C, geo), "geo")
     Q, Qs = geo[4], geo[5]
-    x = (torch.randn(Q, C, device="cuda") * 0.5).half()
-    wk = (torch.randn(C, 3, 3, C, device="cuda") / 80).half()
-    out = torch.empty(B * H * W, C, device="cuda", dtype=torch.float16)
+    x = (torch.randn(Q, C, device="cuda") * 0.5).to(tdt)
+    wk = (torch.randn(C, 3, 3, C, device="cuda") / 80).to(tdt)
+    out = torch.empty(B * H * W, C, device="cuda", dtype=tdt)
     colsum = torch.empty(2, C, device="cuda", dtype=torch.float64)
     ws = torch.zeros(L.ebc_dec_workspace_bytes(dt, B, H, W, C, C), device="cuda", dtype=torch.uint8)
-    dzT = (torch.randn(C, Qs, device="cuda") * 0.1).half()
-    xT3 = (torch.randn(3, C, Qs, device="cuda") * 0.5).half()
+    dzT = (torch.randn(C, Qs, device="cuda") * 0.1).to(tdt)
+    xT3 = (torch.randn(3, C, Qs, device="cuda") * 0.5).to(tdt)
     dw = torch.empty(C, 3, 3, C, device="cuda")
     st = _lib.stream()
     f = 2.0 * B * H * W * C * C * 9
@@ -46,8 +48,8 @@ def main():
                                           ws.numel(), B, H, W, C, C, st))
     t3 = timeit(lambda: L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws), ws.numel(),
                                             B, H, W, C, C, st))
-    cfg = os.environ.get("EBC_CONV_CFG", "auto")
-    print(f"cfg {cfg:>4}: fwd+stats {t1*1e6:7.1f} us {f/t1/1e12:6.0f} TF/s | fwd {t2*1e6:7.1f} us {f/t2/1e12:6.0f} TF/s"
+    cfg = os.environ.get("EBC_CONV_CFG", "auto") + " tail=" + os.environ.get("EBC_CONV_TAIL", "1")
+    print(f"B={B} H={H} C={C} cfg {cfg:>4}: fwd+stats {t1*1e6:7.1f} us {f/t1/1e12:6.0f} TF/s | fwd {t2*1e6:7.1f} us {f/t2/1e12:6.0f} TF/s"
           f" | wgrad {t3*1e6:7.1f} us {f/t3/1e12:6.0f} TF/s (algorithmic)")
 
 
