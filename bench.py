@@ -206,7 +206,6 @@ def setup(args, rank, world, local, device):
     B = args.crops_per_gpu
     npool = min(args.pool, args.warmup + args.steps)
     pool = [make_batch(B, rank, s, device, args.size) for s in range(npool)]
-    info_buf = torch.zeros(5, device=device)
 
     def step(i):
         img, pts, dens, _ = pool[i % len(pool)]
@@ -217,10 +216,10 @@ def setup(args, rank, world, local, device):
         scaler.scale(loss).backward()
         scaler.step(opt)
         scaler.update()
-        # one packed all-reduce of the 5 loss_info scalars (reference: 5 separate + .item(), train.py:62)
-        torch.stack([info[k] for k in ("loss", "ot_loss", "tv_loss", "count_loss", "ce_loss")], out=info_buf)
+        # one packed all-reduce of the 5 loss_info scalars (reference: 5 separate + .item(), train.py:62): the
+        # loss's own [5] term vector (loss, ot, tv, count, ce), no stack launch
         if world > 1:
-            dist.all_reduce(info_buf)
+            dist.all_reduce(loss_fn.last_terms)
     step.pool = pool
     return step
 

@@ -31,6 +31,8 @@ size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K);
 constexpr size_t CONV_WS_STATS_OFFSET = 16 * 1024;
 int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,
                   void* out, float* outf, float* mean, float* rstd, int M, int D, hipStream_t st);
+int layernorm_bwd_fill(int dtype, const float* dy, const float* x, int rpg, int gstride, int goff, const float* mean,
+                       const float* rstd, const float* gamma, float* dx_out, void* dx_out_t, int M, int D, hipStream_t st);
 int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg, int gstride, int goff,
                   const float* mean, const float* rstd, const float* gamma, const float* dx_in, float* dx_out,
                   void* dx_out_t, int M, int D, hipStream_t st);

@@ -241,20 +241,18 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
     Layout lay = carve(ws, B, L, G, layers, dtype, 1);
     if (lay.bytes > ws_bytes) return EBC_E_ARG;
     const int per_batch = vpt_bstride != 0;
-    const size_t es = dtype == EBC_F32 ? 4 : 2;
 
     // ln_post backward into the patch rows of dX_L; CLS / prompt rows get zero gradient
     float* dX = lay.dXa;
     float* dXo = lay.dXb;
-    if (hipMemsetAsync(dX, 0, (size_t)M * WIDTH * 4, st) != hipSuccess) return EBC_E_LAUNCH;
     if (lay.gws && hipMemsetAsync(lay.gws, 0, std::min<size_t>(lay.gws_bytes, 16 * 1024), st) != hipSuccess)
         return EBC_E_LAUNCH;
     auto gemm = [&](int epi, const void* A, const void* Bm, void* C, void* aux, int m, int n, int k) {
         return ebc::gemm_nt(dtype, epi, 0, A, Bm, C, nullptr, nullptr, aux, m, n, k, st, lay.gws, lay.gws_bytes);
     };
-    if (hipMemsetAsync(lay.dXt, 0, (size_t)M * WIDTH * es, st) != hipSuccess) return EBC_E_LAUNCH;
-    EBC_TRY(ebc::layernorm_bwd(dtype, 1, dfeat, lay.X[layers], G, L, 1 + NV, lay.mpost, lay.rpost, w->ln_post_g,
-                               nullptr, dX, lay.dXt, B * G, WIDTH, st));
+    // (the CLS / prompt rows of dX, dXt are written as zeros by the same launch: no memsets)
+    EBC_TRY(ebc::layernorm_bwd_fill(dtype, dfeat, lay.X[layers], G, L, 1 + NV, lay.mpost, lay.rpost, w->ln_post_g, dX,
+                                    lay.dXt, B * G, WIDTH, st));
     for (int l = layers - 1; l >= 0; --l) {
         const EbcVitLayer& p = w->layer[l];
         LayerSave& s = lay.s[l];

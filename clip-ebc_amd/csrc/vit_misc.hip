@@ -126,15 +126,33 @@ struct VptOut {
     int L, NV;
 };
 
-template <class T, class DY, int NV>
+template <class T, class DY, int NV, bool ZF = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, const float* __restrict__ x, RowMap map,
                                                      const float* mean_in, const float* rstd_in, const float* gamma,
                                                      const float* dx_in, float* dx_out, T* dx_out_t, int M, VptOut vo)
 {
     constexpr int D = 256 * NV;
     constexpr float inv = 1.0f / (float)D;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (r >= M) return;
+    int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if constexpr (ZF) {
+        // grid over every destination row (M = groups * gstride): rows outside the mapped groups get a zero
+        // gradient (ln_post: the CLS / prompt rows), the others run as mapped row r = their index in the groups
+        if (r >= M) return;
+        const int grp = r / map.gstride, l = r - grp * map.gstride;
+        if (l < map.goff || l >= map.goff + map.rpg) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int c = 4 * lane + 256 * i;
+                *reinterpret_cast<float4*>(dx_out + (size_t)r * D + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (dx_out_t) st4<T>(dx_out_t + (size_t)r * D + c, make_float4(0.f, 0.f, 0.f, 0.f));
+            }
+            return;
+        }
+        r = grp * map.rpg + l - map.goff;
+    } else {
+        if (r >= M) return;
+    }
     const size_t xr = map(r) * D;
     const float mean = mean_in[r], rstd = rstd_in[r];
     float4 g[NV], xh[NV];
@@ -564,6 +582,29 @@ static int ln_bwd_t(int dy_f32, const void* dy, const float* x, RowMap map, cons
     return EBC_OK;
 }
 
+// ln_post's backward (dy f32 over the patch rows, no incoming dx): also writes the zero gradient of every row
+// outside the groups, so dx_out / dx_out_t need no memset: one launch over all M / rpg * gstride rows
+int layernorm_bwd_fill(int dtype, const float* dy, const float* x, int rpg, int gstride, int goff, const float* mean,
+                       const float* rstd, const float* gamma, float* dx_out, void* dx_out_t, int M, int D, hipStream_t st)
+{
+    if (D != 768 || M <= 0 || rpg <= 0 || M % rpg || goff + rpg > gstride) return EBC_E_UNSUPPORTED;
+    const RowMap map{rpg, gstride, goff};
+    const VptOut vo{nullptr, 1, 0};
+    const int Mf = M / rpg * gstride;
+    const dim3 grid((Mf + 3) / 4);
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL((ln_bwd_kernel<float, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean, rstd,
+                                         gamma, nullptr, dx_out, (float*)dx_out_t, Mf, vo); break;
+        case EBC_F16: hipLaunchKernelGGL((ln_bwd_kernel<_Float16, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean,
+                                         rstd, gamma, nullptr, dx_out, (_Float16*)dx_out_t, Mf, vo); break;
+        case EBC_BF16: hipLaunchKernelGGL((ln_bwd_kernel<__bf16, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean,
+                                          rstd, gamma, nullptr, dx_out, (__bf16*)dx_out_t, Mf, vo); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
 int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg, int gstride, int goff,
                   const float* mean, const float* rstd, const float* gamma, const float* dx_in, float* dx_out,
                   void* dx_out_t, int M, int D, hipStream_t st)
@@ -683,8 +724,12 @@ static int head_bwd_t(int dtype_z, int dtype_dz, const void* Z, const float* tex
                       const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
                       float* dbias, float* dscale, int P, int HW, int NB, hipStream_t st)
 {
-    if (dbias && hipMemsetAsync(dbias, 0, CH * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
-    if (dscale && hipMemsetAsync(dscale, 0, sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
+    if (dbias && dscale == dbias + CH) {           // one buffer [CH + 1]: one memset
+        if (hipMemsetAsync(dbias, 0, (CH + 1) * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
+    } else {
+        if (dbias && hipMemsetAsync(dbias, 0, CH * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
+        if (dscale && hipMemsetAsync(dscale, 0, sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
+    }
     const dim3 grid((P + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
     const size_t lds = ((size_t)NB * CH + 4 * CH + 4) * 4;
 #define HB(TZ, TD) hipLaunchKernelGGL((head_bwd_kernel<TZ, TD, CH>), grid, dim3(256), lds, st, (const TZ*)Z, text, logit_scale, anchors, dlogits, dexp, gscale, (TD*)dZ, dbias, dscale, P, HW, NB)

@@ -89,6 +89,10 @@ def _run_dace(pred_class, pred_density, target_density, points, offsets, order, 
 
 
 class _DaceFn(torch.autograd.Function):
+    """Outputs: the total loss (0-dim, differentiable), the 5 loss terms and the per-crop stats (both
+    non-differentiable).  The backward gets the total's upstream gradient alone (no materialised zero gradients
+    for the other outputs) and scales both kernel-made gradients by it in one foreach launch."""
+
     @staticmethod
     def forward(ctx, pred_class, pred_density, target_density, points, offsets, order, bins_lo, bins_hi,
                 cfg, sink):
@@ -98,15 +102,18 @@ class _DaceFn(torch.autograd.Function):
             sink.append(internals)
         ctx.save_for_backward(grad_c, grad_d)
         ctx.dtypes = (pred_class.dtype, pred_density.dtype)
-        ctx.mark_non_differentiable(stats)
-        return losses, stats
+        ctx.set_materialize_grads(False)
+        terms = losses.detach()
+        ctx.mark_non_differentiable(terms, stats)
+        return losses[0], terms, stats
 
     @staticmethod
-    def backward(ctx, g_losses, g_stats):
+    def backward(ctx, g_loss, g_terms, g_stats):
+        if g_loss is None:
+            return (None,) * 10
         grad_c, grad_d = ctx.saved_tensors
-        s = g_losses[0]
-        return ((grad_c * s).to(ctx.dtypes[0]), (grad_d * s).to(ctx.dtypes[1]),
-                None, None, None, None, None, None, None, None)
+        gc, gd = torch._foreach_mul([grad_c, grad_d], g_loss)
+        return (gc.to(ctx.dtypes[0]), gd.to(ctx.dtypes[1]), None, None, None, None, None, None, None, None)
 
 
 def _pack_points(target_points: Sequence[Tensor], device) -> Tuple[Tensor, Tensor, Tensor, int]:
@@ -190,15 +197,17 @@ class DACELoss(nn.Module):
                float(dm.ot_loss.reg) if dm else 10.0, int(dm.ot_loss.num_of_iter_in_ot) if dm else 0,
                1e-9, 10, total, reduced)
         sink = [] if (dm is not None and dm.keep_internals) else None
-        losses, _ = _DaceFn.apply(pred_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
+        loss, d, _ = _DaceFn.apply(pred_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
         if sink:
             dm.internals = sink[0]
-        d = losses.detach()
+        # the 5 terms as one device vector in _INFO_DM order (loss, ot, tv, count, ce): a packed all-reduce
+        # needs no stack launch
+        self.last_terms = d
         if self.use_dm_loss:
             info = {k: d[i] for i, k in enumerate(_INFO_DM)}
         else:
             info = {"ce_loss": d[4], f"{self.count_loss}_loss": d[3], "loss": d[0]}
-        return losses[0], info
+        return loss, info
 
 
 def _dummy_class(B: int, h: int, w: int, dev) -> Tuple[Tensor, Tensor, Tensor]:
@@ -231,11 +240,10 @@ class DMLoss(nn.Module):
                float(self.weight_ot), float(self.weight_tv), float(self.ot_loss.reg),
                int(self.ot_loss.num_of_iter_in_ot), 1e-9, 10, total, reduced)
         sink = [] if self.keep_internals else None
-        losses, _ = _DaceFn.apply(zero_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
+        loss, d, _ = _DaceFn.apply(zero_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
         if sink:
             self.internals = sink[0]
-        d = losses.detach()
-        loss = losses[0] - losses[4]   # remove the dummy CE (log 1 = 0 anyway)
+        loss = loss - d[4]             # remove the dummy CE (log 1 = 0 anyway)
         info = {"loss": d[0] - d[4], "ot_loss": d[1], "tv_loss": d[2], "count_loss": d[3]}
         return loss, info
 
@@ -271,7 +279,7 @@ class OTLoss(nn.Module):
         cfg = (B, 1, self.input_size, self.reduction, _lib.EBC_COUNT_OT_ONLY, self.norm_cood, 1.0, 1.0, 0.0,
                float(self.reg), int(self.num_of_iter_in_ot), 1e-9, 10, total, True)
         sink = []
-        losses, stats = _DaceFn.apply(zero_class, pred_density, dummy_target, pts, offs, order, lo, hi, cfg, sink)
+        loss, _, stats = _DaceFn.apply(zero_class, pred_density, dummy_target, pts, offs, order, lo, hi, cfg, sink)
         it = sink[0]
         if self.keep_internals:
             self.internals = it
@@ -279,7 +287,7 @@ class OTLoss(nn.Module):
         has = torch.tensor([float(len(p) > 0) for p in target_points], device=dev).view(B, 1)
         ot_obj = (normed_pred_density.detach().float().reshape(B, -1) * it.beta * has).sum().reshape(1)
         wd = float(stats[:, 4].sum())
-        return losses[0].reshape(1), wd, ot_obj          # OT-only mode: losses[0] = losses[1] = sum of the crops' OT
+        return loss.reshape(1), wd, ot_obj               # OT-only mode: losses[0] = losses[1] = sum of the crops' OT
 
 
 def sinkhorn(a: Tensor, b: Tensor, C: Tensor, reg: float = 1e-1, maxIter: int = 1000, stopThr: float = 1e-9,

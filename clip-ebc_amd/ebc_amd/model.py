@@ -244,7 +244,11 @@ class _HeadFn(torch.autograd.Function):
         else:
             Y = (y.detach() if nhwc else y.detach().permute(0, 2, 3, 1)).to(cdtype).reshape(P, C).contiguous()
         E = weight.shape[0]                                        # CLIP joint width: 512 / 1024 (RN50)
-        Wc = weight.detach().reshape(E, C).to(cdtype).contiguous()
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            from .resnet import _prep_1x1
+            Wc, Wt = _prep_1x1(L, weight, cdtype, st)              # [E, C] and [C, E], one launch
+        else:
+            Wc, Wt = weight.detach().reshape(E, C).to(cdtype).contiguous(), None
         bf = bias.detach().float().contiguous()
         Z = torch.empty(P, E, device=y.device, dtype=torch.float32)
         _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(Y), _lib.ptr(Wc), _lib.ptr(Z), _lib.ptr(bf), None, None,
@@ -254,19 +258,19 @@ class _HeadFn(torch.autograd.Function):
         expo = torch.empty(B, 1, Hh, Ww, device=y.device, dtype=torch.float32)
         _lib.check(L.ebc_head_fwd(_lib.EBC_F32, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
                                   _lib.ptr(logits), _lib.ptr(expo), P, HW, NB, E, st), "ebc_head_fwd")
-        ctx.save_for_backward(Y, Wc, Z, ls, text, anchors)
+        ctx.save_for_backward(Y, Wc, Wt, Z, ls, text, anchors)
         ctx.meta = (B, C, Hh, Ww, cdtype, y.dtype, weight.shape, nhwc)
         return logits, expo
 
     @staticmethod
     def backward(ctx, dlogits, dexp):
-        with _lib.on(ctx.saved_tensors[2]):
+        with _lib.on(ctx.saved_tensors[3]):
             return _HeadFn._backward(ctx, dlogits, dexp)
 
     @staticmethod
     def _backward(ctx, dlogits, dexp):
         L = _lib.lib()
-        Y, Wc, Z, ls, text, anchors = ctx.saved_tensors
+        Y, Wc, Wt, Z, ls, text, anchors = ctx.saved_tensors
         st = _lib.stream(Z)
         B, C, Hh, Ww, cdtype, ydt, wshape, nhwc = ctx.meta
         P, HW, NB = B * Hh * Ww, Hh * Ww, text.shape[0]
@@ -276,12 +280,13 @@ class _HeadFn(torch.autograd.Function):
         dt = _lib.dtype_code(cdtype)
         E = Wc.shape[0]
         dZ = torch.empty(P, E, device=dev, dtype=cdtype)
-        dbias = torch.empty(E, device=dev, dtype=torch.float32)
-        dscale = torch.empty(1, device=dev, dtype=torch.float32)
+        dbs = torch.empty(E + 1, device=dev, dtype=torch.float32)     # dbias | dscale: one memset in ebc_head_bwd
+        dbias, dscale = dbs[:E], dbs[E:]
         _lib.check(L.ebc_head_bwd(_lib.EBC_F32, dt, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
                                   _lib.ptr(dl), _lib.ptr(de), None, _lib.ptr(dZ), _lib.ptr(dbias), _lib.ptr(dscale),
                                   P, HW, NB, E, st), "ebc_head_bwd")
-        Wt = Wc.t().contiguous()                                   # [C, E]
+        if Wt is None:
+            Wt = Wc.t().contiguous()                               # [C, E]
         dY = torch.empty(P, C, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dZ), _lib.ptr(Wt), _lib.ptr(dY), None, None, None,
                               P, C, E, st), "ebc_gemm(projection dX)")
@@ -424,7 +429,11 @@ class _DecoderFn(torch.autograd.Function):
             mean, rstd, scale, shift = (torch.empty(N, **f32) for _ in range(4))
             upd = use_batch and training and bn.track_running_stats
             if upd:
-                bn.num_batches_tracked.add_(1)
+                if bn.momentum is None:            # cumulative average: the factor needs the updated count now
+                    bn.num_batches_tracked.add_(1)
+                else:
+                    from .resnet import _PENDING_NBT
+                    _PENDING_NBT.append(bn.num_batches_tracked)
             mom = _bn_momentum(bn) if upd else 0.0
             _lib.check(L.ebc_bn_finalize(_lib.ptr(colsum), count, float(bn.eps), mom, _lib.ptr(gm.detach()),
                                          _lib.ptr(bt.detach()), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale),
@@ -442,6 +451,8 @@ class _DecoderFn(torch.autograd.Function):
         _lib.check(L.ebc_bn_add_relu(dt, _lib.ptr(z2), _lib.ptr(scale2), _lib.ptr(shift2), _lib.ptr(feat), up,
                                      _lib.ptr(y), B, H, W, N, st), "ebc_bn_add_relu")
         ctx.save_for_backward(xpad, hpad, y, wflip[0], g1, wflip[1], g2)
+        from .resnet import flush_bn_counters
+        flush_bn_counters()                        # both BatchNorms' num_batches_tracked in one launch
         ctx.outs = outs
         ctx.meta = (B, h, w, H, W, C, N, up, cdtype, Q, Qs, P)
         return y

@@ -19,6 +19,8 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from .losses import _INFO_DM
+
 try:
     from tqdm import tqdm
 except ImportError:                                   # pragma: no cover
@@ -57,7 +59,11 @@ def train(model: nn.Module, data_loader, loss_fn: nn.Module, optimizer: torch.op
             optimizer.step()
         if keys is None:
             keys = list(loss_info.keys())
-        packed = torch.stack([loss_info[k].detach().float().reshape(()) for k in keys])
+        terms = getattr(loss_fn, "last_terms", None)
+        if terms is not None and keys == list(_INFO_DM):
+            packed = terms                            # DACELoss's own [5] vector in keys' order: no stack launch
+        else:
+            packed = torch.stack([loss_info[k].detach().float().reshape(()) for k in keys])
         acc = packed if acc is None else acc + packed
         steps += 1
     if steps == 0:
