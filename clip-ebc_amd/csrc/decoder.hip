@@ -534,67 +534,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_flat_kernel(const T* __restr
     }
 }
 
-// The same, 64 rows x 64 channels per block, also writing dz transposed (dzT[c][p], row stride ldt, zero for
-// P <= p < ldt): the weight-gradient GEMM's K-contiguous operand without a separate transpose pass
-template <class T, bool HAS_MY>
-__global__ __launch_bounds__(256) void bn_bwd_apply_flat_t_kernel(const T* __restrict__ gy, const T* __restrict__ my,
-                                                                  const T* __restrict__ z, const float* __restrict__ mean,
-                                                                  const float* __restrict__ rstd,
-                                                                  const float* __restrict__ scale,
-                                                                  const float* __restrict__ shift,
-                                                                  const float* __restrict__ coef, T* __restrict__ dz,
-                                                                  T* __restrict__ dzT, long ldt, float* __restrict__ gmask,
-                                                                  long P, int C)
-{
-    __shared__ float sm[64][65];
-    const int t = threadIdx.x;
-    const long p0 = (long)blockIdx.x * 64;
-    const int c0 = blockIdx.y * 64;
-    const int rl = t >> 2, cl = (t & 3) * 16;
-    const long p = p0 + rl;
-    const bool live = p < P;
-    const size_t off = (size_t)(live ? p : P - 1) * C + c0 + cl;
-    float v[16];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int c = c0 + cl + 8 * h;
-        float gv[8], zv[8], mv[8], k0[8], k1[8], k2[8], mu[8], rs[8], sc[8], sh[8];
-        ld8(gy + off + 8 * h, gv);
-        ld8(z + off + 8 * h, zv);
-        if (HAS_MY) ld8(my + off + 8 * h, mv);
-        ldp8(coef + c, k0); ldp8(coef + C + c, k1); ldp8(coef + 2 * C + c, k2); ldp8(mean + c, mu); ldp8(rstd + c, rs);
-        if (!HAS_MY) { ldp8(scale + c, sc); ldp8(shift + c, sh); }
-        float gm[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float m = HAS_MY ? mv[i] : fmaf(zv[i], sc[i], sh[i]);
-            gm[i] = m > 0.f ? gv[i] : 0.f;
-            v[8 * h + i] = live ? k0[i] * (gm[i] - k1[i] - (zv[i] - mu[i]) * rs[i] * k2[i]) : 0.f;
-        }
-        if (live) {
-            st8(dz + off + 8 * h, v + 8 * h);
-            if (gmask) {
-                *reinterpret_cast<float4*>(gmask + off + 8 * h) = make_float4(gm[0], gm[1], gm[2], gm[3]);
-                *reinterpret_cast<float4*>(gmask + off + 8 * h + 4) = make_float4(gm[4], gm[5], gm[6], gm[7]);
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sm[rl][cl + i] = v[i];
-    __syncthreads();
-    {
-        const int cr = t >> 2, jl = (t & 3) * 16;           // channel row cr, 16 consecutive pixels
-        float w[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = sm[jl + i][cr];
-        if (p0 + jl < ldt) {
-            T* dst = dzT + (size_t)(c0 + cr) * ldt + p0 + jl;
-            st8(dst, w);
-            st8(dst + 8, w + 8);
-        }
-    }
-}
-
 // Tiles of 64 padded positions x 64 channels, staged through LDS so that both the NHWC-padded image
 // (rows of channels) and the transposed image (rows of positions) are written with contiguous rows.
 constexpr int TQ = 64, TC = 64;
@@ -1084,27 +1023,12 @@ extern "C" int ebc_bn_relu(int dtype, const void* z, const float* scale, const f
 
 extern "C" int ebc_bn_bwd_apply_flat(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
                                      const float* rstd, const float* scale, const float* shift, const float* coef,
-                                     void* dz, void* dzT, long ldt, float* gmask, long P, int C, ebc_stream_t stream)
+                                     void* dz, float* gmask, long P, int C, ebc_stream_t stream)
 {
     if (!gy || !z || !mean || !rstd || !coef || !dz || P <= 0 || C % 8 || (!mask_y && (!scale || !shift)))
         return EBC_E_ARG;
-    const hipStream_t st = (hipStream_t)stream;
-    if (dzT) {
-        if (C % 64 || ldt < P || ldt % 64) return EBC_E_ARG;
-        const dim3 g2((unsigned)(ldt / 64), (unsigned)(C / 64));
-        if (mask_y) {
-            EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_flat_t_kernel<T, true>), g2, dim3(256), 0, st,
-                                                       (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale, shift,
-                                                       coef, (T*)dz, (T*)dzT, ldt, gmask, P, C));
-        } else {
-            EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_flat_t_kernel<T, false>), g2, dim3(256), 0, st,
-                                                       (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale, shift,
-                                                       coef, (T*)dz, (T*)dzT, ldt, gmask, P, C));
-        }
-        EBC_CHECK_LAUNCH();
-        return EBC_OK;
-    }
     const unsigned grid = nblk(P * (C / 8));
+    const hipStream_t st = (hipStream_t)stream;
     if (mask_y) {
         EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_flat_kernel<T, true>), dim3(grid), dim3(256), 0, st,
                                                    (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale, shift,

@@ -317,28 +317,19 @@ def _dec_workspace(dev: torch.device, nbytes: int, slot: int = 0) -> Tensor:
     return ws
 
 
-def _wgrad_k(P: int) -> int:
-    """The weight-gradient GEMM's K (pixel) extent for P rows: P rounded up to 64, the bf16 K step and the
-    tile height of ebc_bn_bwd_apply_flat's transposed output (the extra columns are zero)."""
-    return -(-P // 64) * 64
-
-
-def _wgrad_rows(L, dZ: Tensor, Y: Tensor, cdtype: torch.dtype, dev: torch.device, st,
-                dZT: Optional[Tensor] = None) -> Tensor:
+def _wgrad_rows(L, dZ: Tensor, Y: Tensor, cdtype: torch.dtype, dev: torch.device, st) -> Tensor:
     """dW [E, C] f32 = dZ^T Y for row matrices dZ [P, E], Y [P, C] (a 1x1 conv's weight gradient over
-    K = B*H*W pixels): both operands K-contiguous (Y transposed here; dZ too unless its producer already
-    wrote dZT [E, _wgrad_k(P)]), then the split-K MFMA GEMM (K padded with zero columns)."""
+    K = B*H*W pixels): both operands transposed to K-contiguous, then the split-K MFMA GEMM (K padded with
+    zero columns to the GEMM's K step when P is not a multiple of it)."""
     dt = _lib.dtype_code(cdtype)
     P, E = dZ.shape
     C = Y.shape[1]
-    Pp = _wgrad_k(P)
+    kstep = 32 if cdtype == torch.float32 else 64
+    Pp = -(-P // kstep) * kstep
     alloc = torch.empty if Pp == P else torch.zeros
-    if dZT is None:
-        dZT = alloc(E, Pp, device=dev, dtype=cdtype)
-        _lib.check(L.ebc_transpose(dt, _lib.ptr(dZ), _lib.ptr(dZT), P, E, Pp, st), "ebc_transpose(dZ)")
-    elif tuple(dZT.shape) != (E, Pp):
-        raise ValueError(f"dZT {tuple(dZT.shape)} != {(E, Pp)}")
+    dZT = alloc(E, Pp, device=dev, dtype=cdtype)
     YT = alloc(C, Pp, device=dev, dtype=cdtype)
+    _lib.check(L.ebc_transpose(dt, _lib.ptr(dZ), _lib.ptr(dZT), P, E, Pp, st), "ebc_transpose(dZ)")
     _lib.check(L.ebc_transpose(dt, _lib.ptr(Y), _lib.ptr(YT), P, C, Pp, st), "ebc_transpose(Y)")
     dW = torch.empty(E, C, device=dev, dtype=torch.float32)
     ws = _dec_workspace(dev, L.ebc_gemm_wgrad_workspace_bytes(dt, E, C, Pp), slot=2)

@@ -312,7 +312,7 @@ class _ResBlockFn(torch.autograd.Function):
 
     @staticmethod
     def _backward(ctx, gy):
-        from .model import _wgrad_k, _wgrad_rows
+        from .model import _wgrad_rows
         L = _lib.lib()
         B, H, W, Cin, s, Ho, Wo, P, Po, planes, Cout, down, cdtype, xdt = ctx.meta
         saved = ctx.saved_tensors
@@ -329,22 +329,18 @@ class _ResBlockFn(torch.autograd.Function):
         f32 = dict(device=dev, dtype=torch.float32)
 
         def apply_flat(g, mask, z, st_, coef, gmask=None):
-            # dz rows for the data-gradient GEMM, dz^T (K-contiguous) for the weight-gradient GEMM
-            R, C = z.shape
-            dz = torch.empty(R, C, device=dev, dtype=cdtype)
-            dzT = torch.empty(C, _wgrad_k(R), device=dev, dtype=cdtype)
+            dz = torch.empty(z.shape, device=dev, dtype=cdtype)
             _lib.check(L.ebc_bn_bwd_apply_flat(dt, _lib.ptr(g), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(st_[0]),
                                                _lib.ptr(st_[1]), _lib.ptr(st_[2]), _lib.ptr(st_[3]), _lib.ptr(coef),
-                                               _lib.ptr(dz), _lib.ptr(dzT), dzT.shape[1], _lib.ptr(gmask), R, C, st),
+                                               _lib.ptr(dz), _lib.ptr(gmask), z.shape[0], z.shape[1], st),
                        "ebc_bn_bwd_apply_flat")
-            return dz, dzT
+            return dz
 
         # bn3 (+ relu3 through y); without a downsample the identity's gradient is g = gy * (y > 0) itself (f32)
         dg3, db3, coef3 = _batch_norm_bwd(L, g3, s3, gy, y, z3, ws, Po, Cout, dev, st)
         gid = None if down else torch.empty(Po, Cout, **f32)
-        dz3, dz3T = apply_flat(gy, y, z3, s3, coef3, gid)
-        dw3 = _wgrad_rows(L, dz3, h2p, cdtype, dev, st, dz3T)
-        del dz3T
+        dz3 = apply_flat(gy, y, z3, s3, coef3, gid)
+        dw3 = _wgrad_rows(L, dz3, h2p, cdtype, dev, st)
         dh2p = torch.empty(Po, planes, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dz3), _lib.ptr(W3t), _lib.ptr(dh2p), None, None, None,
                               Po, planes, Cout, st), "ebc_gemm(conv3 dX)")
@@ -353,9 +349,8 @@ class _ResBlockFn(torch.autograd.Function):
         if down:
             # downsample bn (same masked gradient) -> 1x1 -> avgpool: the identity's input gradient, f32
             dgd, dbd, coefd = _batch_norm_bwd(L, ctx.gammas[3], sd, gy, y, zd, ws, Po, Cout, dev, st)
-            dzd, dzdT = apply_flat(gy, y, zd, sd, coefd)
-            dwd = _wgrad_rows(L, dzd, xd, cdtype, dev, st, dzdT)
-            del dzdT
+            dzd = apply_flat(gy, y, zd, sd, coefd)
+            dwd = _wgrad_rows(L, dzd, xd, cdtype, dev, st)
             dxd = torch.empty(Po, Cin, **f32)
             _lib.check(L.ebc_gemm(dt, 0, 1, _lib.ptr(dzd), _lib.ptr(Wdt), _lib.ptr(dxd), None, None, None,
                                   Po, Cin, Cout, st), "ebc_gemm(downsample dX)")
@@ -393,10 +388,9 @@ class _ResBlockFn(torch.autograd.Function):
         del dz2pad
         # bn1 (ReLU mask recomputed from z1) -> conv1: dx = dz1 W1 + the identity's gradient
         dg1, db1, coef1 = _batch_norm_bwd(L, g1, s1, dh1, None, z1, ws, P, planes, dev, st)
-        dz1, dz1T = apply_flat(dh1, None, z1, s1, coef1)
+        dz1 = apply_flat(dh1, None, z1, s1, coef1)
         del dh1
-        dw1 = _wgrad_rows(L, dz1, x.view(P, Cin), cdtype, dev, st, dz1T)
-        del dz1T
+        dw1 = _wgrad_rows(L, dz1, x.view(P, Cin), cdtype, dev, st)
         dx = torch.empty(B, H, W, Cin, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 2, 0, _lib.ptr(dz1), _lib.ptr(W1t), _lib.ptr(dx), None, _lib.ptr(gid),
                               None, P, Cin, planes, st), "ebc_gemm(conv1 dX + identity)")
@@ -512,7 +506,7 @@ class _BottleneckFn(torch.autograd.Function):
 
     @staticmethod
     def _backward(ctx, gy):
-        from .model import _dec_workspace, _wgrad_k, _wgrad_rows
+        from .model import _dec_workspace, _wgrad_rows
         L = _lib.lib()
         x, z1, h1pad, z2, h2, z3, y, W1t, wf2, W3t, g1, g2, g3 = ctx.saved_tensors
         s1, s2, s3 = ctx.states
@@ -526,14 +520,13 @@ class _BottleneckFn(torch.autograd.Function):
         # bn3 (+ relu through the block output y); the identity branch keeps g = gy * (y > 0) in f32
         dg3, db3, coef3 = _batch_norm_bwd(L, g3, s3, gy, y, z3, ws, P, N, dev, st)
         dz3 = torch.empty(P, N, device=dev, dtype=cdtype)
-        dzT = torch.empty(N, _wgrad_k(P), device=dev, dtype=cdtype)
         gid = torch.empty(P, C, device=dev, dtype=torch.float32)
         mean3, rstd3, sc3, sh3 = s3[:4]
         _lib.check(L.ebc_bn_bwd_apply_flat(dt, _lib.ptr(gy), _lib.ptr(y), _lib.ptr(z3), _lib.ptr(mean3), _lib.ptr(rstd3),
-                                           _lib.ptr(sc3), _lib.ptr(sh3), _lib.ptr(coef3), _lib.ptr(dz3), _lib.ptr(dzT),
-                                           dzT.shape[1], _lib.ptr(gid), P, N, st), "ebc_bn_bwd_apply_flat(bn3)")
+                                           _lib.ptr(sc3), _lib.ptr(sh3), _lib.ptr(coef3), _lib.ptr(dz3), _lib.ptr(gid),
+                                           P, N, st), "ebc_bn_bwd_apply_flat(bn3)")
         # conv3: dW3 = dz3^T h2, dh2 = dz3 W3
-        dw3 = _wgrad_rows(L, dz3, h2, cdtype, dev, st, dzT)
+        dw3 = _wgrad_rows(L, dz3, h2, cdtype, dev, st)
         dh2 = torch.empty(P, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(dz3), _lib.ptr(W3t), _lib.ptr(dh2), None, None, None,
                               P, N, N, st), "ebc_gemm(conv3 dX)")
@@ -562,11 +555,11 @@ class _BottleneckFn(torch.autograd.Function):
         mean1, rstd1, sc1, sh1 = s1[:4]
         dz1 = torch.empty(P, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_bn_bwd_apply_flat(dt, _lib.ptr(dh1), None, _lib.ptr(z1), _lib.ptr(mean1), _lib.ptr(rstd1),
-                                           _lib.ptr(sc1), _lib.ptr(sh1), _lib.ptr(coef1), _lib.ptr(dz1), _lib.ptr(dzT),
-                                           dzT.shape[1], None, P, N, st), "ebc_bn_bwd_apply_flat(bn1)")
+                                           _lib.ptr(sc1), _lib.ptr(sh1), _lib.ptr(coef1), _lib.ptr(dz1), None, P, N, st),
+                   "ebc_bn_bwd_apply_flat(bn1)")
         del dh1
         # conv1: dW1 = dz1^T x, dx = dz1 W1 + the identity branch's gradient (f32, in place over gid)
-        dw1 = _wgrad_rows(L, dz1, x, cdtype, dev, st, dzT)
+        dw1 = _wgrad_rows(L, dz1, x, cdtype, dev, st)
         _lib.check(L.ebc_gemm(dt, 2, 1, _lib.ptr(dz1), _lib.ptr(W1t), _lib.ptr(gid), None,
                               _lib.ptr(gid), None, P, C, N, st), "ebc_gemm(conv1 dX + identity)")
         dfeat = torch.empty(B, h, w, C, device=dev, dtype=torch.float32)

@@ -301,15 +301,14 @@ int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int B, int h, i
  *   ebc_bn_relu:           out [P][C] T = relu(z*scale + shift)
  *   ebc_bn_bwd_apply_flat: dz [P][C] T = BatchNorm input gradient (coef from ebc_bn_bwd_finalize), g = gy * relu'(mask_y,
  *                          or z*scale+shift when mask_y == NULL); gmask != NULL also receives g [P][C] f32 (the
- *                          identity branch's gradient); dzT != NULL also receives dz transposed, dzT [C][ldt] (zero
- *                          for P <= p < ldt; C, ldt multiples of 64): ebc_gemm_wgrad's operand without ebc_transpose. */
+ *                          identity branch's gradient). */
 int ebc_dec_upsample(int dtype, const float* feat, void* x, int B, int h, int w, int C, int up, ebc_stream_t stream);
 int ebc_bn_stats(int dtype, const void* z, double* colsum, void* ws, size_t wsb, long P, int C, ebc_stream_t stream);
 int ebc_bn_relu(int dtype, const void* z, const float* scale, const float* shift, void* out, long P, int C,
                 ebc_stream_t stream);
 int ebc_bn_bwd_apply_flat(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
                           const float* rstd, const float* scale, const float* shift, const float* coef, void* dz,
-                          void* dzT, long ldt, float* gmask, long P, int C, ebc_stream_t stream);
+                          float* gmask, long P, int C, ebc_stream_t stream);
 /* ModifiedResNet encoder blocks on HIP (models/clip/_clip/image_encoder.py:10-115, blocks.py:56-101: 1x1 -> 3x3 ->
  * avgpool(stride) -> 1x1, downsample = avgpool + 1x1 + BN), NHWC rows [B*H*W][C], C % 8 == 0, H, W even:
  *   ebc_bn_relu_avgpool:  out [B][H/2][W/2][C] = AvgPool2d(2)(relu(z*scale + shift))      (bn2 -> relu2 -> avgpool)

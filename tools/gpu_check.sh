@@ -55,6 +55,7 @@ for what in "$@"; do
       db=$(find $O/${TAG}_rprof -name "*.db" | head -1)
       python3 $R/tools/kstats.py "$db" --window --per 10 --top 45 --csv $O/${TAG}_rkstats.csv > $O/${TAG}_rkstats.txt \
         || { echo "kstats failed"; exit 1; }
+      [ -n "$KCALLS" ] && python3 $R/tools/kstats.py "$db" --window --top 0 --calls "$KCALLS" > $O/${TAG}_rcalls.txt
       rm -rf $O/${TAG}_rprof
       head -40 $O/${TAG}_rkstats.txt ;;
     *) echo "unknown step $what"; exit 2 ;;

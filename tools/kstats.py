@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 rocpd database (``--kernel-trace`` output) as per-kernel stats.
 
-usage: python tools/kstats.py <results.db> [--csv out.csv] [--top N] [--per STEPS] [--window]
+usage: python tools/kstats.py <results.db> [--csv out.csv] [--top N] [--per STEPS] [--window] [--calls PATTERN]
 
 Prints calls / total / average / share per kernel name (templated names shortened), and with
 ``--per`` the per-step time of each kernel (total / STEPS).  ``--window`` keeps only the kernels that run
@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--per", type=float, default=0.0)
     ap.add_argument("--window", action="store_true")
+    ap.add_argument("--calls", default="", help="also list every launch whose name contains PATTERN (in time order, "
+                    "with its duration and the kernel that ran before it)")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     where = ""
@@ -52,6 +54,15 @@ def main():
         ps = f"{r['per_step_us']:9.1f}" if a.per else ""
         print(f"{r['pct']:6.2f} {r['calls']:6d} {r['avg_us']:9.2f} {ps:>9}  {r['kernel']}")
     print(f"total kernel time {total / 1e6:.3f} ms" + (f"  per step {total / 1e3 / a.per:.1f} us" if a.per else ""))
+    if a.calls:
+        seq = con.execute(f"select name, start, end, duration from kernels{where} order by start").fetchall()
+        t0 = seq[0][1] if seq else 0
+        print(f"\n== launches matching {a.calls!r}: start_us dur_us gap_us  previous kernel")
+        for i, (name, s0, e0, d) in enumerate(seq):
+            if a.calls in name:
+                prev = seq[i - 1] if i else None
+                gap = (s0 - prev[2]) / 1e3 if prev else 0.0
+                print(f"{(s0 - t0) / 1e3:10.1f} {d / 1e3:8.2f} {gap:7.2f}  {short(prev[0]) if prev else '-'}")
     if a.csv:
         with open(a.csv, "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=list(out[0].keys()))
