@@ -56,24 +56,32 @@ __device__ __forceinline__ int attn_off(int row, int col) {
     else return row * C::LDR + col;
 }
 
-template <class E, int NWV>
-__device__ __forceinline__ void load_rows(typename E::T* dst, const typename E::T* src, int ld, int L)
-{
-    // dst[s][0..63] = src[s*ld + 0..63] for s < L, zero for L <= s < LP
-    using C = AttnCfg<E>;
-    constexpr int PER = LP * C::CPR / (64 * NWV);          // 16-B chunks per thread (all loads first)
+// One tile of rows into LDS (dst[s][0..63] = src[s*ld + 0..63] for s < L, zero up to LP) in two halves, so that several tiles' (and the fragments') global loads are all in flight before
+// the first LDS store waits on one of them: fetch -> (other loads) -> store
+template <class E, int NWV> struct RowFetch {
+    static constexpr int PER = LP * AttnCfg<E>::CPR / (64 * NWV);
     uint4 v[PER];
+};
+template <class E, int NWV>
+__device__ __forceinline__ void rows_fetch(RowFetch<E, NWV>& f, const typename E::T* src, int ld, int L)
+{
+    using C = AttnCfg<E>;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
+    for (int k = 0; k < RowFetch<E, NWV>::PER; ++k) {
         const int e = threadIdx.x + k * 64 * NWV;
         const int s = e / C::CPR, c = e % C::CPR;
-        v[k] = s < L ? *reinterpret_cast<const uint4*>(src + (size_t)s * ld + c * (16 / C::EB)) : make_uint4(0, 0, 0, 0);
+        f.v[k] = s < L ? *reinterpret_cast<const uint4*>(src + (size_t)s * ld + c * (16 / C::EB)) : make_uint4(0, 0, 0, 0);
     }
+}
+template <class E, int NWV>
+__device__ __forceinline__ void rows_store(typename E::T* dst, const RowFetch<E, NWV>& f)
+{
+    using C = AttnCfg<E>;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
+    for (int k = 0; k < RowFetch<E, NWV>::PER; ++k) {
         const int e = threadIdx.x + k * 64 * NWV;
         const int s = e / C::CPR, c = e % C::CPR;
-        *reinterpret_cast<uint4*>(dst + attn_off<E>(s, c * (16 / C::EB))) = v[k];
+        *reinterpret_cast<uint4*>(dst + attn_off<E>(s, c * (16 / C::EB))) = f.v[k];
     }
 }
 
@@ -129,8 +137,10 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
-    load_rows<E, NWV>(Ks, base + D, D3, L);
-    load_rows<E, NWV>(Vs, base + 2 * D, D3, L);
+    // K, V and this wave's Q fragments: every global load issued before the first LDS store
+    RowFetch<E, NWV> fk, fv;
+    rows_fetch<E, NWV>(fk, base + D, D3, L);
+    rows_fetch<E, NWV>(fv, base + 2 * D, D3, L);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
     const int q0 = qb * QB + w * 16;
@@ -138,6 +148,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     typename E::Frag qf[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qme < L);
+    rows_store<E, NWV>(Ks, fk);
+    rows_store<E, NWV>(Vs, fv);
     __syncthreads();
 
     if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
@@ -229,31 +241,35 @@ __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* _
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
-    load_rows<E, NWV>(Ks, base + D, D3, L);
-    load_rows<E, NWV>(Vs, base + 2 * D, D3, L);
+    // K, V, and this wave's Q / dO / O fragments and lse: every global load before the first LDS store
+    RowFetch<E, NWV> fk, fv;
+    rows_fetch<E, NWV>(fk, base + D, D3, L);
+    rows_fetch<E, NWV>(fv, base + 2 * D, D3, L);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
     const int q0 = qb * QB + w * 16;
     const int qme = q0 + fr;
     const bool qv = qme < L;
-    typename E::Frag qf[2], df[2];
+    typename E::Frag qf[2], df[2], of[2];
     const T* drow = dout + ((size_t)b * L + qme) * D + h * HD;
+    const T* orow = out + ((size_t)b * L + qme) * D + h * HD;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
         qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qv);
         df[ks] = gload8<E>(drow + 32 * ks + 8 * fg, qv);
+        of[ks] = gload8<E>(orow + 32 * ks + 8 * fg, qv);
     }
     const float lq = qv ? lse[((size_t)b * H + h) * L + qme] : INFINITY;
+    rows_store<E, NWV>(Ks, fk);
+    rows_store<E, NWV>(Vs, fv);
     // delta = rowsum(dO * O) (FA2 D_i), computed here and published for the dK/dV kernel
     float dq;
     {
-        const T* orow = out + ((size_t)b * L + qme) * D + h * HD;
         float dd = 0.f;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const typename E::Frag of = gload8<E>(orow + 32 * ks + 8 * fg, qv);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) dd = fmaf((float)df[ks][j], (float)of[j], dd);
+            for (int j = 0; j < 8; ++j) dd = fmaf((float)df[ks][j], (float)of[ks][j], dd);
         }
         dd += __shfl_xor(dd, 16, 64);
         dd += __shfl_xor(dd, 32, 64);
@@ -358,14 +374,10 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
-    load_rows<E, NWV>(Qs, base, D3, L);
-    load_rows<E, NWV>(Ds, dout + (size_t)b * L * D + h * HD, D, L);
-    for (int q = threadIdx.x; q < LP; q += blockDim.x) {              // lse pre-scaled by log2(e)
-        ls[q] = q < L ? lse[((size_t)b * H + h) * L + q] * LOG2E : INFINITY;
-        if (delta) dl[q] = q < L ? delta[((size_t)b * H + h) * L + q] : 0.f;
-        else dl[q] = q < L ? attn_delta_row<E>(dout + ((size_t)b * L + q) * D + h * HD, out + ((size_t)b * L + q) * D + h * HD) : 0.f;
-    }
-
+    // Q, dO and this wave's K / V fragments: every global load before the first LDS store
+    RowFetch<E, NWV> fq, fd;
+    rows_fetch<E, NWV>(fq, base, D3, L);
+    rows_fetch<E, NWV>(fd, dout + (size_t)b * L * D + h * HD, D, L);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
     const int k0 = kb * QB + w * 16;
     const int kme = k0 + fr;
@@ -376,6 +388,14 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
         kf[ks] = gload8<E>(base + (size_t)kme * D3 + D + 32 * ks + 8 * fg, kv);
         vf[ks] = gload8<E>(base + (size_t)kme * D3 + 2 * D + 32 * ks + 8 * fg, kv);
     }
+    rows_store<E, NWV>(Qs, fq);
+    rows_store<E, NWV>(Ds, fd);
+    for (int q = threadIdx.x; q < LP; q += blockDim.x) {              // lse pre-scaled by log2(e)
+        ls[q] = q < L ? lse[((size_t)b * H + h) * L + q] * LOG2E : INFINITY;
+        if (delta) dl[q] = q < L ? delta[((size_t)b * H + h) * L + q] : 0.f;
+        else dl[q] = q < L ? attn_delta_row<E>(dout + ((size_t)b * L + q) * D + h * HD, out + ((size_t)b * L + q) * D + h * HD) : 0.f;
+    }
+
     __syncthreads();
 
     if (k0 >= L) return;                                       // no live key in this wave (no barrier follows)
