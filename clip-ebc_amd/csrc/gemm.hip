@@ -23,6 +23,18 @@
 
 using namespace ebc;
 
+// cache-policy bits of the operand LDS-DMA loads (experiment builds: tools/build_gemm_exp.sh)
+#ifndef EBC_GLDS_AUX
+#define EBC_GLDS_AUX 0
+#endif
+// MODE 0 epilogue of the 8-wave tiles: operand loads in this many row phases, scheduling fence per row group
+#ifndef EBC_EPI_PHASES
+#define EBC_EPI_PHASES 2
+#endif
+#ifndef EBC_EPI_SCHED
+#define EBC_EPI_SCHED 1
+#endif
+
 namespace {
 
 enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4, EPI_ADD_RELU_GRAD = 5 };
@@ -170,7 +182,10 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE>
+// SPL: the split-K epilogue paths are compiled in (only the instances a launch with g.splits > 1 runs: their
+// partial loads / stores beside the accumulators made the register allocator spill every 8-wave tile's epilogue,
+// 256x256: 150-430 registers, even on launches that never split)
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE, bool SPL>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
 {
     static_assert(S >= 2 && S <= 5, "stages");
@@ -279,13 +294,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         for (int i = 0; i < NLDF; ++i) {
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src[i] + (isa[i] ? oa : ob)),
-                EBC_LDS(dst + (wave * NLDF + i) * 1024), 16, 0, 0);
+                EBC_LDS(dst + (wave * NLDF + i) * 1024), 16, 0, EBC_GLDS_AUX);
         }
 #pragma unroll
         for (int j = 0; j < NT4; ++j) {
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src[NLDF + j] + (isa[NLDF + j] ? oa : ob)),
-                EBC_LDS(dst + NLDF * NW * 1024 + (wave * NT4 + j) * 256), 4, 0, 0);
+                EBC_LDS(dst + NLDF * NW * 1024 + (wave * NT4 + j) * 256), 4, 0, EBC_GLDS_AUX);
         }
     };
 
@@ -444,7 +459,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     return;
 #endif
 
-    if (g.splits > 1 && g.cnt == nullptr) {
+    if (SPL && g.splits > 1 && g.cnt == nullptr) {
         // split-K without a last arriver (deep splits of the weight-gradient products): every split stores its
         // f32 partial row-major into part[split][M][N] (columns as the epilogue maps them), a separate launch
         // (splitk_reduce_kernel) sums the splits in split order -- deterministic, and the sum is spread over
@@ -470,7 +485,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         }
         return;
     }
-    if (g.splits > 1) {
+    if (SPL && g.splits > 1) {
         // split-K: publish this split's f32 partial (lane-major: the reader has the same lane map,
         // so every access is a coalesced 16-B per lane), count the arrival; the last arriver sums
         // the others and runs the epilogue, the rest exit.  Agent-scope fences order the partial
@@ -497,13 +512,28 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         if (!last) return;
         // bit-reproducible sum whichever split arrives last: two splits add the other's partial (f32
         // addition commutes); more splits re-read every partial, this one's too, in split order
+        // loaded in row-group chunks of at most 64 registers: the whole partial at once (TM*TN*4 registers on top of
+        // the accumulators) spilled the 256-wide tiles' epilogues (256x256: 150-430 registers)
+        constexpr int PCH = [] { int c = TM; while (c > 1 && (TM % c || c * TN * 4 > 64)) --c; return c; }();
         auto add_partial = [&](int sp) {
+            static_for<0, TM / PCH>([&](auto cc) {
+                constexpr int a0 = decltype(cc)::value * PCH;
+                f32x4 t[PCH][TN];
 #pragma unroll
-            for (int a = 0; a < TM; ++a)
+                for (int a = 0; a < PCH; ++a)
 #pragma unroll
-                for (int b = 0; b < TN; ++b)
-                    acc[a][b] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                        rs, ((sp * PT) + ((wave * TM + a) * TN + b) * 64 + lane) * 16, 0, 16));
+                    for (int b = 0; b < TN; ++b)
+                        t[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                            rs, ((sp * PT) + ((wave * TM + a0 + a) * TN + b) * 64 + lane) * 16, 0, 16));
+#pragma unroll
+                for (int a = 0; a < PCH; ++a)
+#pragma unroll
+                    for (int b = 0; b < TN; ++b) acc[a0 + a][b] += t[a][b];
+                // keep the next chunk's loads below this one's adds (a sched_barrier alone did not: the DAG
+                // scheduler hoisted all 32 loads of a 256x256 partial)
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+            });
         };
         if (g.splits == 2) {
             add_partial(1 - split);
@@ -531,18 +561,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         typedef PA pa4 __attribute__((ext_vector_type(4)));
         const int mb = m0 + wm * WM + fr;
         const int nb = n0 + wn * WN;
-        pa8 p8[PRE ? TM : 1][NP > 0 ? NP : 1];
-        pa4 p4[PRE && ODD ? TM : 1];
-        if constexpr (PRE) {
-            const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
-#pragma unroll
-            for (int a = 0; a < TM; ++a) {
-                const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
-#pragma unroll
-                for (int q = 0; q < NP; ++q) p8[a][q] = *reinterpret_cast<const pa8*>(src + ro + q * 32 + fg * 8);
-                if constexpr (ODD) p4[a] = *reinterpret_cast<const pa4*>(src + ro + NP * 32 + fg * 4);
-            }
-        }
+        // 8-wave tiles run two waves per SIMD (256 registers each): their operands are loaded for half of the
+        // row groups at a time (the whole wave tile at once spilled: GELU' 256x192, 27 registers)
+        constexpr int PREG = PRE ? TM * (NP * (int)sizeof(pa8) + ODD * (int)sizeof(pa4)) / 4 : 0;
+        constexpr int PH = (NW >= 8 && PREG > 24 && TM % 2 == 0) ? EBC_EPI_PHASES : 1;
+        constexpr int TMP = TM / PH;
         float bv[NP > 0 ? NP : 1][8], bo[4];
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
@@ -569,24 +592,41 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             if (w == 8) store8<TO>(C + off, v);
             else store4<TO>(C + off, v);
         };
+        static_for<0, PH>([&](auto phc) {
+            constexpr int a0 = decltype(phc)::value * TMP;
+            pa8 p8[PRE ? TMP : 1][NP > 0 ? NP : 1];
+            pa4 p4[PRE && ODD ? TMP : 1];
+            if constexpr (PRE) {
+                const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-            const int m = mb + a * 16;
-            if (m >= g.M) break;                 // rows ascend with a
-            const size_t ro = (size_t)m * g.N + nb;
+                for (int a = 0; a < TMP; ++a) {
+                    const size_t ro = (size_t)min(mb + (a0 + a) * 16, g.M - 1) * g.N + nb;
 #pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                float v[8] = {acc[a][2 * q][0], acc[a][2 * q][1], acc[a][2 * q][2], acc[a][2 * q][3],
-                              acc[a][2 * q + 1][0], acc[a][2 * q + 1][1], acc[a][2 * q + 1][2], acc[a][2 * q + 1][3]};
-                if constexpr (PRE) finish(v, 8, bv[q], p8[a][q], ro + q * 32 + fg * 8);
-                else finish(v, 8, bv[q], 0, ro + q * 32 + fg * 8);
+                    for (int q = 0; q < NP; ++q) p8[a][q] = *reinterpret_cast<const pa8*>(src + ro + q * 32 + fg * 8);
+                    if constexpr (ODD) p4[a] = *reinterpret_cast<const pa4*>(src + ro + NP * 32 + fg * 4);
+                }
             }
-            if constexpr (ODD) {
-                float v[4] = {acc[a][TN - 1][0], acc[a][TN - 1][1], acc[a][TN - 1][2], acc[a][TN - 1][3]};
-                if constexpr (PRE) finish(v, 4, bo, p4[a], ro + NP * 32 + fg * 4);
-                else finish(v, 4, bo, 0, ro + NP * 32 + fg * 4);
+#pragma unroll
+            for (int a = 0; a < TMP; ++a) {
+                const int m = mb + (a0 + a) * 16;
+                if (m >= g.M) break;                 // rows ascend with a
+                const size_t ro = (size_t)m * g.N + nb;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    float v[8] = {acc[a0 + a][2 * q][0], acc[a0 + a][2 * q][1], acc[a0 + a][2 * q][2], acc[a0 + a][2 * q][3],
+                                  acc[a0 + a][2 * q + 1][0], acc[a0 + a][2 * q + 1][1], acc[a0 + a][2 * q + 1][2],
+                                  acc[a0 + a][2 * q + 1][3]};
+                    if constexpr (PRE) finish(v, 8, bv[q], p8[a][q], ro + q * 32 + fg * 8);
+                    else finish(v, 8, bv[q], 0, ro + q * 32 + fg * 8);
+                }
+                if constexpr (ODD) {
+                    float v[4] = {acc[a0 + a][TN - 1][0], acc[a0 + a][TN - 1][1], acc[a0 + a][TN - 1][2], acc[a0 + a][TN - 1][3]};
+                    if constexpr (PRE) finish(v, 4, bo, p4[a], ro + NP * 32 + fg * 4);
+                    else finish(v, 4, bo, 0, ro + NP * 32 + fg * 4);
+                }
+                if constexpr (EBC_EPI_SCHED && NW >= 8) __builtin_amdgcn_sched_barrier(0);
             }
-        }
+        });
     } else {
     // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i].
     // Staged through LDS in passes of EPR rows (row pitch BN+4 floats: conflict-free b128 writes),
@@ -695,8 +735,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     }   // staged epilogue (MODE 1 / 2)
 }
 
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0>
-int launch_gemm(const GemmArgs& g, hipStream_t st)
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE, bool SPL>
+int launch_gemm_k(const GemmArgs& g, hipStream_t st)
 {
     constexpr int WM = BM / WGM;
     constexpr int LDS = gemm_lds_bytes<BM, BN, S, ROWB, WM>();
@@ -704,7 +744,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
     constexpr int BK = ROWB / E::BYTES;
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE>,
+        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
             return EBC_E_LAUNCH;
         attr = true;
@@ -714,16 +754,29 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
     if (tiles <= 0 || g.tile0 + tiles > ((g.M + BM - 1) / BM) * (g.N / BN)) return EBC_E_ARG;
     const int nwg = tiles * g.splits;
     const int pi = probe_on() ? probe_start(EBC_PROBE_GEMM, EPI, BM, BN, MODE, g.M, g.N, g.K, st) : -1;
-    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
+    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
+}
+
+// Split-K launches exist for the weight gradients (MODE 2, and MODE 0 f32 stores), the conv GEMMs' tail tiles
+// (MODE 1) and forced MODE 0 store splits; every other product runs the split-free instance.
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0>
+int launch_gemm(const GemmArgs& g, hipStream_t st)
+{
+    if (g.splits > 1) {
+        if constexpr (MODE != 0 || EPI == EPI_STORE) return launch_gemm_k<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, true>(g, st);
+        else return EBC_E_UNSUPPORTED;
+    }
+    return launch_gemm_k<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, false>(g, st);
 }
 
 // Tile configurations (EBC_GEMM_CFG=<n> forces one; EBC_GEMM_SPLITS=<s> forces the split count):
 //   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   6: 256x128/8w
 //   7: 256x256/8w   (2-stage rings of 128-B K rows)
 //   8: 128x64 S3   9: 128x128 S3   10: 256x128/8w S3   11: 192x128/8w S3   12: 128x64 S4   13: 128x96 S3
+//   14: 128x192 S3
 //   20: 256x256/8w  21: 256x128/8w  22: 128x256/8w  24: 128x128/4w   (4-stage rings
 //       of 64-B K rows, 16-bit only; r01: a 256x192 4-stage ring measured 10-15 % slower than
 //       cfg 3's 2-stage 128-B ring on the decoder convs and the MLP, so no such config is built)
@@ -733,7 +786,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 struct TileCfg { int id, bm, bn; };
 constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {6, 256, 128},
                             {7, 256, 256}, {8, 128, 64}, {9, 128, 128}, {10, 256, 128}, {11, 192, 128}, {12, 128, 64},
-                            {13, 128, 96}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128}};
+                            {13, 128, 96}, {14, 128, 192}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128}};
 const TileCfg* find_cfg(int id) {
     for (const TileCfg& c : CFGS) if (c.id == id) return &c;
     return nullptr;
@@ -858,6 +911,7 @@ int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
             case 11: return launch_gemm<E, TO, EPI, 192, 128, 3, 4, 2>(g, st);
             case 12: return launch_gemm<E, TO, EPI, 128, 64, 4>(g, st);
             case 13: return launch_gemm<E, TO, EPI, 128, 96, 3>(g, st);
+            case 14: return launch_gemm<E, TO, EPI, 128, 192, 3>(g, st);
             case 20: return launch_gemm<E, TO, EPI, 256, 256, 4, 4, 2, 64>(g, st);
             case 21: return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64>(g, st);
             case 22: return launch_gemm<E, TO, EPI, 128, 256, 4, 2, 4, 64>(g, st);
@@ -1142,8 +1196,7 @@ size_t gemm_workspace_bytes(int dtype, int M, int N, int K)
     const TileCfg* c = find_cfg(cfg);
     if (!c || N % c->bn != 0) cfg = pick_cfg(M, N, K, true);
     c = find_cfg(cfg);
-    if (cfg < 20) return 0;
-    const int bk = 32;
+    const int bk = (cfg >= 20 && cfg < 30) ? 32 : 64;
     const int splits = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, bk);
     if (splits <= 1) return 0;
     const size_t tiles = (size_t)((M + c->bm - 1) / c->bm) * (N / c->bn);

@@ -62,8 +62,11 @@ def run(what, args, a):
         R = torch.randn(M, N, device="cuda")
         tile = (ctypes.c_int * 3)()
         cfg = L.ebc_gemm_tile_config(code, M, N, K, tile)
-        us = timeit(lambda: L.ebc_gemm(code, epi, 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), _lib.ptr(bias), _lib.ptr(R),
-                                       _lib.ptr(aux), M, N, K, st), a.reps)
+        wsb = L.ebc_gemm_workspace_bytes(code, M, N, K)
+        ws = torch.zeros(max(wsb, 1), device="cuda", dtype=torch.uint8)
+        us = timeit(lambda: _lib.check(L.ebc_gemm_ws(code, epi, 0, _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), _lib.ptr(bias),
+                                                     _lib.ptr(R), _lib.ptr(aux), M, N, K, _lib.ptr(ws) if wsb else None,
+                                                     wsb, st), "gemm"), a.reps)
         f = 2.0 * M * N * K
         print(f"gemm M={M} N={N} K={K} epi={epi} cfg={cfg} tile={tuple(tile)}: {us:.2f} us  {f / us / 1e6:.1f} TF/s")
     elif what == "attn":
