@@ -16,6 +16,7 @@
 // Operand orientation ("swapped" S^T = K Q^T) puts each query on one lane, so the probability
 // accumulators are directly the A operand of P.V with no LDS round trip (mfma.h).
 //   grid: B * H * ceil(L/(16 NW)) workgroups of NW waves; wave w owns 16 queries (fwd, dQ) or 16 keys (dKV).
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 
@@ -227,7 +228,7 @@ template <class E, int NWV, int LFIX>
 __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                  const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                  float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                 int L_, int H, float scale)
+                                                 int L_, int H, float scale, int nblk = 0)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -236,7 +237,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* _
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
     constexpr int QB = 16 * NWV;
-    const int nqb = (L + QB - 1) / QB;
+    // nblk > 0: only the first nblk query blocks of every (crop, head) are launched
+    const int nqb = nblk > 0 ? nblk : (L + QB - 1) / QB;
     const int bh = bid / nqb, qb = bid % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
@@ -358,7 +360,7 @@ template <class E, int NWV, int LFIX>
 __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                   const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                   const float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                  int L_, int H, float scale)
+                                                  int L_, int H, float scale, int nblk = 0)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -369,7 +371,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
     float* ls = reinterpret_cast<float*>(smem + 2 * C::TILE_BYTES);
     float* dl = ls + LP;
     constexpr int QB = 16 * NWV;
-    const int nkb = (L + QB - 1) / QB;
+    const int nkb = nblk > 0 ? nblk : (L + QB - 1) / QB;     // nblk > 0: only the first nblk key blocks
     const int bh = bid / nkb, kb = bid % nkb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
@@ -463,10 +465,10 @@ template <class E, int NWV, int LFIX>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_fused_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                              const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                              typename E::T* __restrict__ dqkv, int ndq, int B, int L_, int H,
-                                                             float scale)
+                                                             float scale, int nblk)
 {
-    if ((int)blockIdx.x < ndq) attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale);
-    else attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x - ndq, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale);
+    if ((int)blockIdx.x < ndq) attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk);
+    else attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x - ndq, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk);
 }
 
 int attn_waves(int L) {
@@ -528,7 +530,7 @@ template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void
     return EBC_OK;
 }
 template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, const void* dout, const void* out, const float* lse,
-                                                           void* dqkv, int B, int L, int H, hipStream_t st)
+                                                           void* dqkv, int B, int L, int H, hipStream_t st, int rows = 0)
 {
     using C = AttnCfg<E>;
     const size_t lds = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
@@ -537,10 +539,14 @@ template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, cons
         if (hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
         attr = true;
     }
-    const int ndq = B * H * ((L + 16 * NW - 1) / (16 * NW));
+    // rows > 0: dQ of queries and dK / dV of keys < rows are wanted (the rest of dqkv is left unwritten)
+    const int nblk = rows > 0 ? std::min((rows + 16 * NW - 1) / (16 * NW), (L + 16 * NW - 1) / (16 * NW))
+                              : (L + 16 * NW - 1) / (16 * NW);
+    const int ndq = B * H * nblk;
     const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 1, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_bwd_fused_kernel<E, NW, LFIX>), dim3(2 * ndq), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
-                       (const typename E::T*)dout, (const typename E::T*)out, lse, (typename E::T*)dqkv, ndq, B, L, H, 0.125f);
+                       (const typename E::T*)dout, (const typename E::T*)out, lse, (typename E::T*)dqkv, ndq, B, L, H, 0.125f,
+                       nblk);
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
@@ -553,11 +559,11 @@ bool attn_bwd_split() {
 }
 
 template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
-                                  void* dqkv, int B, int L, int H, hipStream_t st)
+                                  void* dqkv, int B, int L, int H, hipStream_t st, int rows)
 {
     if (!attn_bwd_split() && E::BYTES == 2) {
-        return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st)
-                            : attn_bwd_fused_nw<E, 8, 0>(qkv, dout, out, lse, dqkv, B, L, H, st);
+        return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows)
+                            : attn_bwd_fused_nw<E, 8, 0>(qkv, dout, out, lse, dqkv, B, L, H, st, rows);
     }
     if (attn_waves(L) == 16)
         return L == L_VPT32 ? attn_bwd_nw<E, 16, L_VPT32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st)
@@ -579,13 +585,13 @@ int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int 
     return EBC_E_ARG;
 }
 int attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
-                  void* dqkv, int B, int L, int H, hipStream_t st)
+                  void* dqkv, int B, int L, int H, hipStream_t st, int rows)
 {
-    if (L <= 0 || L > LP || B <= 0 || H <= 0) return EBC_E_UNSUPPORTED;
+    if (L <= 0 || L > LP || B <= 0 || H <= 0 || rows < 0) return EBC_E_UNSUPPORTED;
     switch (dtype) {
-        case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
-        case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
-        case EBC_BF16: return attn_bwd_t<EBF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+        case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows);
+        case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows);
+        case EBC_BF16: return attn_bwd_t<EBF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows);
     }
     return EBC_E_ARG;
 }

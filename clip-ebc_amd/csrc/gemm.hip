@@ -34,6 +34,12 @@ using namespace ebc;
 #ifndef EBC_EPI_SCHED
 #define EBC_EPI_SCHED 1
 #endif
+#ifndef EBC_RESID_PREFETCH
+#define EBC_RESID_PREFETCH 1
+#endif
+#ifndef EBC_GELU_PREFETCH
+#define EBC_GELU_PREFETCH 1
+#endif
 
 namespace {
 
@@ -66,6 +72,8 @@ struct GemmArgs {
     // a launch covers output tiles [tile0, tile0 + ntile) (ntile 0: through the last); split-K partials and
     // arrival counters are indexed from tile0
     int tile0 = 0, ntile = 0;
+    // MODE 0 row-mapped A operand: A row of output row r = (r / a_rpg) * a_gstride + a_goff + r % a_rpg (a_rpg 0: r)
+    int a_rpg = 0, a_gstride = 0, a_goff = 0;
 };
 
 // Slab rows are ROWB bytes (one BK-deep K slice): 128 (BK = 64 for 16-bit, 32 for f32) or 64
@@ -259,6 +267,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             } else if constexpr (MODE == 2) {
                 base = A + (size_t)gr * g.cQs + g.cG;
             } else {
+                if (g.a_rpg) gr = (gr / g.a_rpg) * g.a_gstride + g.a_goff + gr % g.a_rpg;
                 base = A + (size_t)gr * K;
             }
         } else {
@@ -375,6 +384,39 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         asm volatile("" ::: "memory");
     };
 
+    // 4-wave RESID tiles (one wave per SIMD: registers to spare): the f32 residual operand of the epilogue is
+    // loaded before the ring fills, so its latency hides under the first tiles' instead of being paid after the
+    // K loop (vmcnt retires loads in order: issued any later, a counted ring wait would block on it mid-loop)
+    constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && EBC_RESID_PREFETCH;
+    typedef float rp8_t __attribute__((ext_vector_type(8)));
+    typedef float rp4_t __attribute__((ext_vector_type(4)));
+    rp8_t rp8[PREF ? TM : 1][TN / 2 > 0 ? TN / 2 : 1];
+    rp4_t rp4[PREF && (TN & 1) ? TM : 1];
+    // 8-wave GELU' tiles (256 registers a wave): the first half of the rows' pre-activation operand the same way
+    constexpr bool PREF_G = MODE == 0 && EPI == EPI_GELU_BWD && NW >= 8 && TM % 2 == 0 && (TN & 1) == 0 &&
+                            EBC_GELU_PREFETCH;
+    typedef T gp8_t __attribute__((ext_vector_type(8)));
+    gp8_t gp8[PREF_G ? TM / 2 : 1][TN / 2 > 0 ? TN / 2 : 1];
+    if constexpr (PREF_G) {
+        const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
+        const T* aux = reinterpret_cast<const T*>(g.aux);
+#pragma unroll
+        for (int a = 0; a < TM / 2; ++a) {
+            const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
+#pragma unroll
+            for (int q = 0; q < TN / 2; ++q) gp8[a][q] = *reinterpret_cast<const gp8_t*>(aux + ro + q * 32 + fq * 8);
+        }
+    }
+    if constexpr (PREF) {
+        const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+            const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
+#pragma unroll
+            for (int q = 0; q < TN / 2; ++q) rp8[a][q] = *reinterpret_cast<const rp8_t*>(g.resid + ro + q * 32 + fq * 8);
+            if constexpr (TN & 1) rp4[a] = *reinterpret_cast<const rp4_t*>(g.resid + ro + (TN / 2) * 32 + fq * 4);
+        }
+    }
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
         if (s < nk) stage(s, s);
@@ -596,7 +638,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             constexpr int a0 = decltype(phc)::value * TMP;
             pa8 p8[PRE ? TMP : 1][NP > 0 ? NP : 1];
             pa4 p4[PRE && ODD ? TMP : 1];
-            if constexpr (PRE) {
+            if constexpr (PREF) {
+#pragma unroll
+                for (int a = 0; a < TMP; ++a) {
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) p8[a][q] = rp8[a0 + a][q];
+                    if constexpr (ODD) p4[a] = rp4[a0 + a];
+                }
+            } else if constexpr (PREF_G && a0 == 0 && TMP == TM / 2) {
+#pragma unroll
+                for (int a = 0; a < TMP; ++a)
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) p8[a][q] = __builtin_convertvector(gp8[a][q], pa8);
+            } else if constexpr (PRE) {
                 const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
 #pragma unroll
                 for (int a = 0; a < TMP; ++a) {
@@ -776,7 +830,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 //   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   6: 256x128/8w
 //   7: 256x256/8w   (2-stage rings of 128-B K rows)
 //   8: 128x64 S3   9: 128x128 S3   10: 256x128/8w S3   11: 192x128/8w S3   12: 128x64 S4   13: 128x96 S3
-//   14: 128x192 S3
+//   14: 128x192 S3   (r02: 8-wave 128x96 S3 / S4 measured within noise of the 4-wave tile: not built)
 //   20: 256x256/8w  21: 256x128/8w  22: 128x256/8w  24: 128x128/4w   (4-stage rings
 //       of 64-B K rows, 16-bit only; r01: a 256x192 4-stage ring measured 10-15 % slower than
 //       cfg 3's 2-stage 128-B ring on the decoder convs and the MLP, so no such config is built)
@@ -1204,12 +1258,15 @@ size_t gemm_workspace_bytes(int dtype, int M, int N, int K)
 }
 
 int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
-            const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws, size_t ws_bytes)
+            const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws, size_t ws_bytes,
+            int a_rpg, int a_gstride, int a_goff)
 {
     const int bk = dtype == EBC_F32 ? 32 : 64;
     if (M <= 0 || N <= 0 || K <= 0 || K % bk != 0 || N % 64 != 0 || !A || !B || !C) return EBC_E_ARG;
     if ((epi == EPI_RESID && !resid) || (epi == EPI_GELU_BWD && !aux)) return EBC_E_ARG;
+    if (a_rpg < 0 || (a_rpg > 0 && (a_goff < 0 || a_goff + a_rpg > a_gstride || epi != EPI_STORE))) return EBC_E_ARG;
     GemmArgs g{A, B, C, bias, resid, aux, M, N, K};
+    g.a_rpg = a_rpg; g.a_gstride = a_gstride; g.a_goff = a_goff;
     switch (dtype) {
         case EBC_F32: return dispatch_epi<EF32>(g, epi, 0, nullptr, 0, st);   // element type is already f32
         case EBC_F16: return dispatch_epi<EF16>(g, epi, out_f32, ws, ws_bytes, st);

@@ -10,7 +10,7 @@ int probe_start(int kind, int epi, int bm, int bn, int mode, int m, int n, int k
 void probe_stop(int idx, hipStream_t st);
 int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
             const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws = nullptr,
-            size_t ws_bytes = 0);
+            size_t ws_bytes = 0, int a_rpg = 0, int a_gstride = 0, int a_goff = 0);
 // split-K workspace the heuristic wants for this shape (0: no split); zero-filled counter block first
 size_t gemm_workspace_bytes(int dtype, int M, int N, int K);
 // implicit-GEMM 3x3 convolution geometry (gemm.hip MODE 1 / MODE 2)
@@ -61,8 +61,15 @@ int attn_delta(int dtype, const void* dO, const void* O, float* delta, int B, in
 int cast_f32(int dtype, const float* in, void* out, size_t n, hipStream_t st);
 int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st);
 // delta (FA2 D_i = rowsum(dO * O)) is computed by the dQ kernel and written to `delta` [B,H,L]
+// rows > 0: only dQ of the queries and dK / dV of the keys below `rows` are needed (16-bit: the launch covers
+// the first ceil(rows / 128) blocks of each (crop, head); the other dqkv rows are left unwritten)
 int attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
-                  void* dqkv, int B, int L, int H, hipStream_t st);
+                  void* dqkv, int B, int L, int H, hipStream_t st, int rows = 0);
+// LayerNorm backward of the mapped rows into a dense output: dx_out[r] = dx_in[map r] + LN'(dy[r]) with x, mean,
+// rstd at map r (layer 0's prompt rows: r = (b, j) -> b * gstride + goff + j)
+int layernorm_bwd_rows(int dtype, const void* dy, const float* x, int rpg, int gstride, int goff, const float* mean,
+                       const float* rstd, const float* gamma, const float* dx_in, float* dx_out, int M, int D,
+                       hipStream_t st);
 }  // namespace ebc
 
 #define EBC_TRY(x)                  \

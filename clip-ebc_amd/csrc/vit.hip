@@ -263,6 +263,19 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         { float* t = dX; dX = dXo; dXo = t; }
         // attention half: dO = dX1 . W_out;  dQKV = attn'(...);  dH = dQKV . W_qkv;  dX = dX1 + LN1'(dH)
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dXt, p.wt_out, lay.dO, nullptr, M, WIDTH, WIDTH));
+        if (l == 0 && NV > 0 && dvpt && dvpt[0]) {
+            // layer 0: the frozen encoder below (ln_pre, embeddings, conv1) takes no gradient, so only the prompt
+            // rows' input gradient is wanted -- dQ / dK / dV of the first query and key block (rows 1..NV), dH on
+            // the B*NV prompt rows (row-mapped A operand), ln_1's backward of those rows straight into the prompt
+            // rows (same values as the full backward's rows: every kept element is summed in the same order)
+            EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st, 1 + NV));
+            EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dQKV, p.wt_qkv, lay.dH, nullptr, nullptr, nullptr, B * NV,
+                                 WIDTH, QKVW, st, lay.gws, lay.gws_bytes, NV, L, 1));
+            float* rows = per_batch ? dvpt[0] : lay.vpt_rows;
+            EBC_TRY(ebc::layernorm_bwd_rows(dtype, lay.dH, lay.X[0], NV, L, 1, s.m1, s.r1, p.ln1_g, dX, rows, B * NV,
+                                            WIDTH, st));
+            break;
+        }
         EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st));
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dQKV, p.wt_qkv, lay.dH, nullptr, M, WIDTH, QKVW));
         // prompt rows (deep VPT; shallow VPT: layer 0 only): ln_1's backward routes their gradient to the

@@ -129,7 +129,8 @@ struct VptOut {
     int L, NV;
 };
 
-template <class T, class DY, int NV, bool ZF = false>
+// RD: rows-dense output (layer 0's prompt rows): x, dx_in, mean and rstd at the mapped row, dy and dx_out dense
+template <class T, class DY, int NV, bool ZF = false, bool RD = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, const float* __restrict__ x, RowMap map,
                                                      const float* mean_in, const float* rstd_in, const float* gamma,
                                                      const float* dx_in, float* dx_out, T* dx_out_t, int M, VptOut vo)
@@ -156,8 +157,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
     } else {
         if (r >= M) return;
     }
-    const size_t xr = map(r) * D;
-    const float mean = mean_in[r], rstd = rstd_in[r];
+    const size_t mrow = map(r), xr = mrow * D;
+    const float mean = mean_in[RD ? mrow : r], rstd = rstd_in[RD ? mrow : r];
+    const size_t orow = RD ? (size_t)r * D : xr;
     float4 g[NV], xh[NV], din[NV];
     float s1 = 0.f, s2 = 0.f;
     // the incoming gradient is loaded with the row operands (not after the reductions)
@@ -190,8 +192,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
                 o = make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-        *reinterpret_cast<float4*>(dx_out + xr + c) = o;
-        if (dx_out_t) st4<T>(dx_out_t + xr + c, o);
+        *reinterpret_cast<float4*>(dx_out + orow + c) = o;
+        if (!RD && dx_out_t) st4<T>(dx_out_t + xr + c, o);
     }
 }
 
@@ -667,6 +669,29 @@ int layernorm_bwd_vpt(int dtype, const void* dy, const float* x, const float* me
         case EBC_BF16: return ln_bwd_t<__bf16>(0, dy, x, map, mean, rstd, gamma, dx_in, dx_out, dx_out_t, M, vo, st);
     }
     return EBC_E_ARG;
+}
+
+int layernorm_bwd_rows(int dtype, const void* dy, const float* x, int rpg, int gstride, int goff, const float* mean,
+                       const float* rstd, const float* gamma, const float* dx_in, float* dx_out, int M, int D,
+                       hipStream_t st)
+{
+    if (D != 768 || M <= 0 || rpg <= 0 || M % rpg || goff < 0 || goff + rpg > gstride) return EBC_E_UNSUPPORTED;
+    const RowMap map{rpg, gstride, goff};
+    const VptOut vo{nullptr, 1, 0};
+    const dim3 grid((M + 3) / 4);
+    const int pi = probe_on() ? probe_start(EBC_PROBE_LN_BWD, 0, 0, 0, 0, M, 768, 0, st) : -1;
+    struct Stop { int i; hipStream_t s; ~Stop() { probe_stop(i, s); } } stop{pi, st};
+    switch (dtype) {
+        case EBC_F32: hipLaunchKernelGGL((ln_bwd_kernel<float, float, 3, false, true>), grid, dim3(256), 0, st, (const float*)dy,
+                                         x, map, mean, rstd, gamma, dx_in, dx_out, (float*)nullptr, M, vo); break;
+        case EBC_F16: hipLaunchKernelGGL((ln_bwd_kernel<_Float16, _Float16, 3, false, true>), grid, dim3(256), 0, st,
+                                         (const _Float16*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (_Float16*)nullptr, M, vo); break;
+        case EBC_BF16: hipLaunchKernelGGL((ln_bwd_kernel<__bf16, __bf16, 3, false, true>), grid, dim3(256), 0, st,
+                                          (const __bf16*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (__bf16*)nullptr, M, vo); break;
+        default: return EBC_E_ARG;
+    }
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
 }
 
 int vpt_sum(const float* rows, float* const* dst, int layers, int B, int NVPT, int D, hipStream_t st)
