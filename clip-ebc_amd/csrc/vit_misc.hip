@@ -337,7 +337,10 @@ __global__ __launch_bounds__(256) void vpt_grad_kernel(float* __restrict__ dX, T
 // ----------------------------------------------------------------------------- similarity head
 // One wave per pixel, CH channels (CH / 64 per lane, in float4 pieces 256 apart), NB <= 16 bins; the text
 // features are normalised in LDS.  CH = 512 (ViT-B/16) or 1024 (ResNet-50, models/clip/model.py:85-95).
-constexpr int PIX_PER_BLOCK = 16;
+// pixels per 4-wave block (r02, tools/kbench.py head): the forward is fastest with one pixel per wave (4: 15.7 us vs
+// 18.5 at 16, 16 crops); the backward with 8 per wave (32: 38.2 vs 42.2 us), since each block adds its d bias row to
+// the same CH addresses with atomics and fewer blocks contend less (4 per block: 86 us)
+constexpr int HEAD_FWD_PPB = 4, HEAD_BWD_PPB = 32;
 
 template <class TZ, int CH>
 __device__ __forceinline__ void load_pix(const TZ* z, float (&v)[CH / 64]) {
@@ -351,14 +354,23 @@ __device__ __forceinline__ void load_pix(const TZ* z, float (&v)[CH / 64]) {
 
 template <int CH>
 __device__ void load_text(const float* text, int NB, float* tn) {
-    // tn[k][c] = text[k][c] / max(||text[k]||, 1e-12)   (F.normalize, model.py:204)
+    // tn[k][c] = text[k][c] / max(||text[k]||, 1e-12)   (F.normalize, model.py:204): each text row read once, as
+    // float4 pieces held in registers across the norm (the per-element loop re-read it, 2 x CH/64 dependent loads)
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     for (int k = w; k < NB; k += blockDim.x / 64) {
+        float4 x[CH / 256];
         float s = 0.f;
-        for (int c = lane; c < CH; c += 64) { const float x = text[k * CH + c]; s += x * x; }
+#pragma unroll
+        for (int q = 0; q < CH / 256; ++q) {
+            x[q] = *reinterpret_cast<const float4*>(text + k * CH + 256 * q + 4 * lane);
+            s += (x[q].x * x[q].x + x[q].y * x[q].y) + (x[q].z * x[q].z + x[q].w * x[q].w);
+        }
         s = wave_sum(s);
         const float inv = 1.0f / fmaxf(sqrtf(s), 1e-12f);
-        for (int c = lane; c < CH; c += 64) tn[k * CH + c] = text[k * CH + c] * inv;
+#pragma unroll
+        for (int q = 0; q < CH / 256; ++q)
+            *reinterpret_cast<float4*>(tn + k * CH + 256 * q + 4 * lane) =
+                make_float4(x[q].x * inv, x[q].y * inv, x[q].z * inv, x[q].w * inv);
     }
     __syncthreads();
 }
@@ -383,15 +395,15 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z,
     constexpr int NV = CH / 64;
     extern __shared__ __attribute__((aligned(16))) float tn[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front,
+    constexpr int PPW = HEAD_FWD_PPB / 4;            // pixels per wave: every row load issued up front,
     float vv[PPW][NV];                                // before the text normalisation (latencies overlap)
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) load_pix<TZ, CH>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+    for (int j = 0; j < PPW; ++j) load_pix<TZ, CH>(Z + (size_t)min(blockIdx.x * HEAD_FWD_PPB + w + 4 * j, P - 1) * CH, vv[j]);
     const float s = expf(*logit_scale);
     load_text<CH>(text, NB, tn);
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-        const int p = blockIdx.x * PIX_PER_BLOCK + w + 4 * j;
+        const int p = blockIdx.x * HEAD_FWD_PPB + w + 4 * j;
         if (p >= P) break;
         float* v = vv[j];
         float ss = 0.f;
@@ -432,10 +444,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
     float* dbias_l = tn + NB * CH;       // [4 waves][CH]
     float* dsc_l = dbias_l + 4 * CH;     // [4]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    constexpr int PPW = PIX_PER_BLOCK / 4;            // pixels per wave: every row load issued up front,
+    constexpr int PPW = HEAD_BWD_PPB / 4;            // pixels per wave: every row load issued up front,
     float vv[PPW][NV];                                // before the text normalisation (latencies overlap)
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) load_pix<TZ, CH>(Z + (size_t)min(blockIdx.x * PIX_PER_BLOCK + w + 4 * j, P - 1) * CH, vv[j]);
+    for (int j = 0; j < PPW; ++j) load_pix<TZ, CH>(Z + (size_t)min(blockIdx.x * HEAD_BWD_PPB + w + 4 * j, P - 1) * CH, vv[j]);
     const float ls = *logit_scale, s = expf(ls);
     const float gs = gscale ? *gscale : 1.0f;
     load_text<CH>(text, NB, tn);
@@ -445,7 +457,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
     float dsc = 0.f;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-        const int p = blockIdx.x * PIX_PER_BLOCK + w + 4 * j;
+        const int p = blockIdx.x * HEAD_BWD_PPB + w + 4 * j;
         if (p >= P) break;
         float* v = vv[j];
         float ss = 0.f;
@@ -733,7 +745,7 @@ template <int CH>
 static int head_fwd_t(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
                       float* logits, float* expo, int P, int HW, int NB, hipStream_t st)
 {
-    const dim3 grid((P + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
+    const dim3 grid((P + HEAD_FWD_PPB - 1) / HEAD_FWD_PPB);
     const size_t lds = (size_t)NB * CH * 4;
     switch (dtype_z) {
         case EBC_F32: hipLaunchKernelGGL((head_fwd_kernel<float, CH>), grid, dim3(256), lds, st, (const float*)Z, text, logit_scale, anchors, logits, expo, P, HW, NB); break;
@@ -765,7 +777,7 @@ static int head_bwd_t(int dtype_z, int dtype_dz, const void* Z, const float* tex
         if (dbias && hipMemsetAsync(dbias, 0, CH * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
         if (dscale && hipMemsetAsync(dscale, 0, sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
     }
-    const dim3 grid((P + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
+    const dim3 grid((P + HEAD_BWD_PPB - 1) / HEAD_BWD_PPB);
     const size_t lds = ((size_t)NB * CH + 4 * CH + 4) * 4;
 #define HB(TZ, TD) hipLaunchKernelGGL((head_bwd_kernel<TZ, TD, CH>), grid, dim3(256), lds, st, (const TZ*)Z, text, logit_scale, anchors, dlogits, dexp, gscale, (TD*)dZ, dbias, dscale, P, HW, NB)
     // the dZ element type is the caller's buffer type (dtype_dz), independent of Z's

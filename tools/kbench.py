@@ -4,6 +4,7 @@ usage: python tools/kbench.py gemm M N K EPI [--reps R] [--dtype f16|bf16]   (EP
        python tools/kbench.py multi gemm:M,N,K,EPI attn:B ... [--rounds R]   (several classes, interleaved rounds)
        python tools/kbench.py attn B [--reps R]                              (fwd + bwd at L = 229, 12 heads)
        python tools/kbench.py conv B [--reps R]                              (decoder 3x3 conv fwd + BN stats, 768 ch)
+       python tools/kbench.py head B [--reps R]                              (similarity head fwd + bwd, f32 Z)
 Prints the HIP-event average per launch.  Operands are random (DVFS: zero-filled data reads high).
 """
 import argparse
@@ -83,6 +84,25 @@ def run(what, args, a):
                                                 _lib.ptr(delta), _lib.ptr(dqkv), B, Lq, H, st), a.reps)
         f = 4.0 * B * H * Lq * Lq * 64
         print(f"attn B={B}: fwd {tf:.2f} us ({f / tf / 1e6:.0f} TF/s)  bwd {tb:.2f} us ({2 * f / tb / 1e6:.0f} TF/s)")
+    elif what == "head":
+        (B,) = args                                  # crops of 224 at reduction 8: 784 pixels each, embed 512, 5 bins
+        HW, CH, NB = 784, 512, 5
+        P = B * HW
+        f32, f16 = _lib.dtype_code(torch.float32), _lib.dtype_code(torch.float16)
+        Z = torch.randn(P, CH, device="cuda")
+        text = torch.randn(NB, CH, device="cuda")
+        ls = torch.full((1,), 4.6, device="cuda")
+        anchors = torch.tensor([0.0, 1.0, 2.0, 3.0, 4.2], device="cuda")
+        logits = torch.empty(B, NB, HW, device="cuda")
+        expo = torch.empty(B, 1, HW, device="cuda")
+        dl, de = torch.randn_like(logits), torch.randn_like(expo)
+        dZ = torch.empty(P, CH, device="cuda", dtype=torch.float16)
+        dbias, dscale = torch.zeros(CH, device="cuda"), torch.zeros(1, device="cuda")
+        p = _lib.ptr
+        tf = timeit(lambda: L.ebc_head_fwd(f32, p(Z), p(text), p(ls), p(anchors), p(logits), p(expo), P, HW, NB, CH, st), a.reps)
+        tb = timeit(lambda: L.ebc_head_bwd(f32, f16, p(Z), p(text), p(ls), p(anchors), p(dl), p(de), None, p(dZ), p(dbias),
+                                           p(dscale), P, HW, NB, CH, st), a.reps)
+        print(f"head B={B}: fwd {tf:.2f} us ({P * CH * 4 / tf / 1e3:.0f} GB/s)  bwd {tb:.2f} us ({P * CH * 6 / tb / 1e3:.0f} GB/s)")
     elif what == "conv":
         (B,) = args
         H = W = 28
