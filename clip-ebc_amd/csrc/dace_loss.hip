@@ -38,6 +38,10 @@ namespace {
 constexpr int NT = EBC_DACE_NT;          // threads per workgroup (16 waves, 4 per SIMD)
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
+#ifndef EBC_SORTED_W16_MIN_POINTS
+#define EBC_SORTED_W16_MIN_POINTS 250
+#endif
+constexpr int SORTED_W16_MIN_POINTS = EBC_SORTED_W16_MIN_POINTS;   // crops from this many points: 16 lanes per block
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
 
 // G = the LDS grid (a multiple of 4 >= the crop's density grid g = size / reduction); cells with a row or
@@ -321,7 +325,7 @@ __device__ __forceinline__ float sum4_dpp(float x) {
 // Factor rows are CW wide: G (full rows) or Cfg::CW (the 12 cells from row_base: compact).
 // Returns false (nothing iterated) when a window is wider than 9 cells; the caller then runs
 // sinkhorn_crop.  On return the factors, u (u0), windows and point coordinates (spts) are sorted.
-template <int G, int CW>
+template <int G, int CW, int LPB>
 __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                                 const float* __restrict__ pts, float* Ey, float* Ex, float* u0, float* u1, int* win,
                                 int* key, float* spts, int* bk, const float* b, float* v0, float* v1, float* part,
@@ -412,9 +416,12 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
     };
     // row base of a home bucket coordinate (compact rows; the 4x4 block at 4*B reads offset 4*B - base)
     auto hbase = [&](int h) { return CW == G ? 0 : min(C::BS * h, G - CW); };
-    // 8 adjacent lanes per 4x4 block: lane kg takes candidates kg, kg+8, ... four at a time (all LDS
-    // reads before the FMAs); the 16 block sums meet by DPP and lane kg keeps cells 2kg, 2kg+1
-    constexpr int LPB = 8;
+    // LPB adjacent lanes per 4x4 block: lane kg takes candidates kg, kg+LPB, ... four at a time (all LDS
+    // reads before the FMAs); the 16 block sums meet by DPP and lane kg keeps CPL = 16 / LPB cells from cell
+    // CPL * kg.  LPB = 16 (one cell a lane) halves the heaviest block's candidate loop, which the phase barrier
+    // waits for, at the cost of one more butterfly stage: the caller takes it for crops with many points only
+    static_assert(LPB == 8 || (LPB == 16 && NBK * 16 <= NT), "lanes per block");
+    constexpr int CPL = 16 / LPB;
     const int kg = t & (LPB - 1);
     auto ktu_block = [&](int blk, const Ranges& R, const float* uu, float& k0, float& k1) {
         const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1, by = BY * 4, bx = BX * 4;
@@ -470,6 +477,31 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
         };
         const bool b2 = kg & 4, b1 = kg & 2, b0 = kg & 1;
         float c8[8], c4[4];
+        if constexpr (LPB == 16) {
+            // first fold the two 8-lane halves (row mirror: lane kg <-> 15 - kg), then the 8-lane butterfly on the
+            // half of the block's cells this lane keeps; lane kg ends with cell kg
+            const bool b3 = kg & 8;
+            float h8[8], h4[4], h2[2];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float send = b3 ? c16[k] : c16[k + 8];
+                h8[k] = (b3 ? c16[k + 8] : c16[k]) + dpp(send, std::integral_constant<int, 0x140>{});
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float send = b2 ? h8[k] : h8[k + 4];
+                h4[k] = (b2 ? h8[k + 4] : h8[k]) + dpp(send, std::integral_constant<int, 0x141>{});
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const float send = b1 ? h4[k] : h4[k + 2];
+                h2[k] = (b1 ? h4[k + 2] : h4[k]) + dpp(send, std::integral_constant<int, 0x4E>{});
+            }
+            const float send = b0 ? h2[0] : h2[1];
+            k0 = (b0 ? h2[1] : h2[0]) + dpp(send, std::integral_constant<int, 0xB1>{});
+            k1 = 0.f;
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const float send = b2 ? c16[k] : c16[k + 8];
@@ -490,7 +522,7 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
     // cell index of lane kg's first cell (cells 2kg, 2kg+1: row 2kg/4, columns 2kg%4, +1)
     auto cell0 = [&](int blk) {
         const int BY = blk / NB1, BX = blk - (blk / NB1) * NB1;
-        return (BY * 4 + (2 * kg) / 4) * G + BX * 4 + (2 * kg) % 4;
+        return (BY * 4 + (CPL * kg) / 4) * G + BX * 4 + (CPL * kg) % 4;
     };
     constexpr int BPP = NT / LPB;                             // blocks per pass
     constexpr bool ONE = NBK <= BPP;                          // one block per 8-lane group (G = 28)
@@ -516,13 +548,17 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
             if (!ONE) ranges(blk, R); else R = R0;
             const int j = cell0(blk);
             float k0, k1;
-            if (have_ktu) { k0 = part[j]; k1 = part[j + 1]; }
+            if (have_ktu) { k0 = part[j]; k1 = CPL == 2 ? part[j + 1] : 0.f; }
             else ktu_block(blk, R, u, k0, k1);
             tick(1);                                          // diagnostics: "v" = K^T u gather time
-            const float v0n = b[j] / (k0 + M_EPS), v1n = b[j + 1] / (k1 + M_EPS);
+            const float v0n = b[j] / (k0 + M_EPS);
             vn[j] = v0n;
-            vn[j + 1] = v1n;
-            bad |= (int)!isfinite(v0n) | (int)!isfinite(v1n);
+            bad |= (int)!isfinite(v0n);
+            if constexpr (CPL == 2) {
+                const float v1n = b[j + 1] / (k1 + M_EPS);
+                vn[j + 1] = v1n;
+                bad |= (int)!isfinite(v1n);
+            }
         }
         have_ktu = 0;
         if (bad) *fl = 1;
@@ -580,10 +616,13 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
                 float k0, k1;
                 ktu_block(blk, R, u, k0, k1);
                 part[j] = k0;
-                part[j + 1] = k1;
-                const float d0 = b[j] - k0 * v[j], d1 = b[j + 1] - k1 * v[j + 1];
+                const float d0 = b[j] - k0 * v[j];
                 e = fmaf(d0, d0, e);
-                e = fmaf(d1, d1, e);
+                if constexpr (CPL == 2) {
+                    part[j + 1] = k1;
+                    const float d1 = b[j + 1] - k1 * v[j + 1];
+                    e = fmaf(d1, d1, e);
+                }
             }
             err = block_sum(e, misc);
             err_last = err;
@@ -771,10 +810,18 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                 int* win = reinterpret_cast<int*>(u1 + n);
                 int* key = win + n;
                 float* spts = reinterpret_cast<float*>(key + n);
-                if (!sinkhorn_sorted<G, CW>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts,
-                                            Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc, &iters,
-                                            &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr))
-                    return false;
+                // 16 lanes per 4x4 block for crops with many points (r02, tools/loss_probe.py: 600 points 883 -> 743 us,
+                // 1000 points 1278 -> 950 us per 16-crop launch; the bench's light crops ran slower on it)
+                constexpr bool W16 = C::NBK * 16 <= NT;
+                const bool ok = (W16 && n >= SORTED_W16_MIN_POINTS)
+                    ? sinkhorn_sorted<G, CW, W16 ? 16 : 8>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr,
+                                                           P.eval_freq, pts, Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1,
+                                                           part, misc, &iters, &rolled, &err_last,
+                                                           P.prof ? P.prof + b * 16 : nullptr)
+                    : sinkhorn_sorted<G, CW, 8>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr,
+                                                P.eval_freq, pts, Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc,
+                                                &iters, &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr);
+                if (!ok) return false;
                 post(cw, Ey, Ex, u0, win, spts);
                 return true;
             };
