@@ -39,7 +39,7 @@ constexpr int NT = EBC_DACE_NT;          // threads per workgroup (16 waves, 4 p
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
 #ifndef EBC_SORTED_W16_MIN_POINTS
-#define EBC_SORTED_W16_MIN_POINTS 250
+#define EBC_SORTED_W16_MIN_POINTS 257
 #endif
 constexpr int SORTED_W16_MIN_POINTS = EBC_SORTED_W16_MIN_POINTS;   // crops from this many points: 16 lanes per block
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
@@ -536,7 +536,10 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
     int* flag = reinterpret_cast<int*>(misc) + 16;
     if (t < 2) flag[t] = 0;
     __syncthreads();
-    const int q = t & 3;
+    // K v: LPT lanes per point, each <= ceil(9 / LPT) window rows; the heavy-crop instantiation (LPB = 16) uses 2,
+    // so up to NT / 2 points take one pass instead of two
+    constexpr int LPT = LPB == 16 ? 2 : 4;
+    const int q = t & (LPT - 1);
     int to_eval = eval_freq;
     tick(-1);
     while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
@@ -566,8 +569,8 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
         if (t == 0) flag[(it + 1) & 1] = 0;
         tick(0);
         // phase B: u = a / (K v + eps)
-        for (int i0 = 0; i0 < n; i0 += NT / 4) {
-            const int i = i0 + (t >> 2);
+        for (int i0 = 0; i0 < n; i0 += NT / LPT) {
+            const int i = i0 + t / LPT;
             float acc = 0.f;
             if (i < n) {
                 const int w = win[i];
@@ -582,7 +585,7 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
                     float4 e[KW / 4];
 #pragma unroll
                     for (int c = 0; c < KW / 4; ++c) e[c] = *reinterpret_cast<const float4*>(exr + 4 * c);
-                    for (int r = q; r < ylen; r += 4) {
+                    for (int r = q; r < ylen; r += LPT) {
                         const float* vr = vn + (ylo + r) * G + x4;
                         float sum = 0.f;
 #pragma unroll
@@ -595,7 +598,8 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
                     }
                 }
             }
-            acc = sum4_dpp(acc);
+            if constexpr (LPT == 4) acc = sum4_dpp(acc);
+            else acc += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, acc), 0xB1, 0xF, 0xF, true));
             if (i < n && q == 0) {
                 const float val = a / (acc + M_EPS);
                 un[i] = val;
