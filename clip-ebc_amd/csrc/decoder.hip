@@ -245,6 +245,76 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __re
     shift[c] = beta[c] - (float)m * sc;
 }
 
+// The two halves of a BatchNorm statistics pass fused for the ranks that exchange nothing in between (plain
+// BatchNorm, or SyncBatchNorm in a world of one): per-tile column partials [nb][2C] -> f64 sums in reduce_partials'
+// exact order (row groups strided by 16, then the 16 groups in order) -> the finalize of bn_fwd_finalize_kernel /
+// bn_bwd_finalize_kernel, one launch instead of two.  64 channels (both halves of the partial row) per block.
+__device__ __forceinline__ void reduce_pair(const float* __restrict__ part, int nb, int C, double (*red)[16][64],
+                                            double& S, double& Q)
+{
+    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    double s = 0.0, q = 0.0;
+    if (c < C) {
+#pragma unroll 4
+        for (int i = rg; i < nb; i += 16) {
+            s += (double)part[(size_t)i * 2 * C + c];
+            q += (double)part[(size_t)i * 2 * C + C + c];
+        }
+    }
+    red[0][rg][cl] = s;
+    red[1][rg][cl] = q;
+    __syncthreads();
+    S = 0.0; Q = 0.0;
+    if (rg == 0 && c < C) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { S += red[0][k][cl]; Q += red[1][k][cl]; }
+    }
+}
+
+__global__ __launch_bounds__(1024) void reduce_fwd_finalize_kernel(const float* __restrict__ part, int nb, int C,
+                                                                   double count, float eps, float momentum,
+                                                                   const float* __restrict__ gamma,
+                                                                   const float* __restrict__ beta, float* mean,
+                                                                   float* rstd, float* scale, float* shift,
+                                                                   float* rmean, float* rvar, double* colsum_out)
+{
+    __shared__ double red[2][16][64];
+    double S, Q;
+    reduce_pair(part, nb, C, red, S, Q);
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (threadIdx.x >= 64 || c >= C) return;
+    if (colsum_out) { colsum_out[c] = S; colsum_out[C + c] = Q; }
+    const double m = S / count;
+    double var = Q / count - m * m;
+    var = var > 0.0 ? var : 0.0;
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * m);
+    if (rvar) rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * var * count / (count - 1.0));
+    const float rs = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * rs;
+    mean[c] = (float)m;
+    rstd[c] = rs;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)m * sc;
+}
+
+__global__ __launch_bounds__(1024) void reduce_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C,
+                                                                   double count, const float* __restrict__ gamma,
+                                                                   const float* __restrict__ rstd, float* dgamma,
+                                                                   float* dbeta, float* coef)
+{
+    __shared__ double red[2][16][64];
+    double sg, sgx;
+    reduce_pair(part, nb, C, red, sg, sgx);
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (threadIdx.x >= 64 || c >= C) return;
+    if (dgamma) dgamma[c] = (float)sgx;
+    if (dbeta) dbeta[c] = (float)sg;
+    coef[c] = gamma[c] * rstd[c];
+    coef[C + c] = (float)(sg / count);
+    coef[2 * C + c] = (float)(sgx / count);
+}
+
 // x[p][c] = bilinear x`up` upsample of feat, unpadded rows (the Bottleneck's conv1x1 input)
 template <class T>
 __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__ feat, T* __restrict__ x, long P, int H,
@@ -738,10 +808,14 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 // bn_bwd_partial rows per block: 8 rows per thread-row-lane (two 4-row load batches)
 inline int bn_partial_rows(int C) { return 8 * std::max(1, 512 / std::max(1, C / 8)); }
 
+// optional fused finalize (reduce_fwd_finalize_kernel / reduce_bwd_finalize_kernel) instead of reduce_partials
+struct FwdFin { float eps, momentum; const float *gamma, *beta; float *mean, *rstd, *scale, *shift, *rmean, *rvar; };
+struct BwdFin { const float* gamma; float *dgamma, *dbeta, *coef; };
+
 template <class T>
 int bn_bwd_reduce_t(const void* gy, const void* my, const void* z, const float* mean, const float* rstd,
                     const float* scale, const float* shift, double* sums, void* ws, size_t wsb, long P, int C,
-                    hipStream_t st)
+                    hipStream_t st, const BwdFin* fin = nullptr)
 {
     if (C % 8 || C / 8 > 512) return EBC_E_UNSUPPORTED;
     const int C8 = C / 8;
@@ -759,14 +833,19 @@ int bn_bwd_reduce_t(const void* gy, const void* my, const void* z, const float* 
     else
         hipLaunchKernelGGL((bn_bwd_partial_kernel<T, false, 4>), dim3((unsigned)nb), dim3(threads), lds, st,
                            (const T*)gy, (const T*)my, (const T*)z, mean, rstd, scale, shift, part, P, C, rpb);
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
-                       2 * C, sums);
+    if (fin)
+        hipLaunchKernelGGL(reduce_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
+                           C, (double)P, fin->gamma, rstd, fin->dgamma, fin->dbeta, fin->coef);
+    else
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
+                           2 * C, sums);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
 
 template <class T>
-int bn_stats_t(const void* z, double* colsum, void* ws, size_t wsb, long P, int C, hipStream_t st)
+int bn_stats_t(const void* z, double* colsum, void* ws, size_t wsb, long P, int C, hipStream_t st,
+               const FwdFin* fin = nullptr)
 {
     if (C % 8 || C / 8 > 512) return EBC_E_UNSUPPORTED;
     const int C8 = C / 8;
@@ -778,8 +857,13 @@ int bn_stats_t(const void* z, double* colsum, void* ws, size_t wsb, long P, int 
     float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + CONV_WS_STATS_OFFSET);
     hipLaunchKernelGGL((bn_stats_partial_kernel<T, 4>), dim3((unsigned)nb), dim3(C8 * RL), (size_t)RL * 2 * C * 4, st,
                        (const T*)z, part, P, C, rpb);
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
-                       2 * C, colsum);
+    if (fin)
+        hipLaunchKernelGGL(reduce_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
+                           C, (double)P, fin->eps, fin->momentum, fin->gamma, fin->beta, fin->mean, fin->rstd, fin->scale,
+                           fin->shift, fin->rmean, fin->rvar, colsum);
+    else
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
+                           2 * C, colsum);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -1007,6 +1091,40 @@ extern "C" int ebc_bn_stats(int dtype, const void* z, double* colsum, void* ws, 
         case EBC_F32: return bn_stats_t<float>(z, colsum, ws, wsb, P, C, st);
         case EBC_F16: return bn_stats_t<_Float16>(z, colsum, ws, wsb, P, C, st);
         case EBC_BF16: return bn_stats_t<__bf16>(z, colsum, ws, wsb, P, C, st);
+    }
+    return EBC_E_ARG;
+}
+
+extern "C" int ebc_bn_stats_finalize(int dtype, const void* z, void* ws, size_t wsb, long P, int C, float eps,
+                                     float momentum, const float* gamma, const float* beta, float* mean, float* rstd,
+                                     float* scale, float* shift, float* running_mean, float* running_var,
+                                     double* colsum_out, ebc_stream_t stream)
+{
+    if (!z || P <= 1 || C % 8 || !gamma || !beta || !mean || !rstd || !scale || !shift) return EBC_E_ARG;
+    if ((running_mean == nullptr) != (running_var == nullptr)) return EBC_E_ARG;
+    const FwdFin fin{eps, momentum, gamma, beta, mean, rstd, scale, shift, running_mean, running_var};
+    const hipStream_t st = (hipStream_t)stream;
+    switch (dtype) {
+        case EBC_F32: return bn_stats_t<float>(z, colsum_out, ws, wsb, P, C, st, &fin);
+        case EBC_F16: return bn_stats_t<_Float16>(z, colsum_out, ws, wsb, P, C, st, &fin);
+        case EBC_BF16: return bn_stats_t<__bf16>(z, colsum_out, ws, wsb, P, C, st, &fin);
+    }
+    return EBC_E_ARG;
+}
+
+extern "C" int ebc_bn_bwd_reduce_finalize(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
+                                          const float* rstd, const float* scale, const float* shift, const float* gamma,
+                                          float* dgamma, float* dbeta, float* coef, void* ws, size_t wsb, long P, int C,
+                                          ebc_stream_t stream)
+{
+    if (!gy || !z || !mean || !rstd || !gamma || !coef || P <= 0 || C % 4 || (!mask_y && (!scale || !shift)))
+        return EBC_E_ARG;
+    const BwdFin fin{gamma, dgamma, dbeta, coef};
+    const hipStream_t st = (hipStream_t)stream;
+    switch (dtype) {
+        case EBC_F32: return bn_bwd_reduce_t<float>(gy, mask_y, z, mean, rstd, scale, shift, nullptr, ws, wsb, P, C, st, &fin);
+        case EBC_F16: return bn_bwd_reduce_t<_Float16>(gy, mask_y, z, mean, rstd, scale, shift, nullptr, ws, wsb, P, C, st, &fin);
+        case EBC_BF16: return bn_bwd_reduce_t<__bf16>(gy, mask_y, z, mean, rstd, scale, shift, nullptr, ws, wsb, P, C, st, &fin);
     }
     return EBC_E_ARG;
 }

@@ -97,6 +97,8 @@ SIGNATURES = {
     "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ebc_dec_upsample": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ebc_bn_stats": (_I, [_I, _P, _P, _P, _Z, _L, _I, _P]),
+    "ebc_bn_stats_finalize": (_I, [_I, _P, _P, _Z, _L, _I, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "ebc_bn_bwd_reduce_finalize": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _L, _I, _P]),
     "ebc_bn_relu": (_I, [_I, _P, _P, _P, _P, _L, _I, _P]),
     "ebc_bn_bwd_apply_flat": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "ebc_bn_relu_avgpool": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _P]),

@@ -17,6 +17,7 @@ except conv2's input, which is the zero-padded image the implicit-GEMM 3x3 conv 
 from __future__ import annotations
 
 import ctypes
+import os
 from collections import OrderedDict
 from typing import Any, List, Optional, Tuple
 
@@ -128,14 +129,24 @@ class Bottleneck(nn.Module):
         self.downsample = nn.Identity()
 
 
-def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, training: bool, dev, st):
+# EBC_BN_FUSED=0: the three-launch BatchNorm statistics path everywhere (A/B and debugging)
+_FUSE_BN = os.environ.get("EBC_BN_FUSED", "1") != "0"
+
+
+def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, training: bool, dev, st, src=None):
     """BatchNorm2d statistics -> (mean, rstd, scale, shift, count, group, colsum); SyncBatchNorm all-reduces
-    [sum | sum of squares | this rank's count] in one f64 buffer (as model._DecoderFn)."""
+    [sum | sum of squares | this rank's count] in one f64 buffer (as model._DecoderFn).  src = (dtype code, z, ws):
+    the statistics of z are taken here -- without an exchange, column sums and finalize in one launch
+    (ebc_bn_stats_finalize), else ebc_bn_stats into colsum first."""
     from .model import _bn_group, _bn_momentum
     f32 = dict(device=dev, dtype=torch.float32)
     use_batch = colsum is not None
     pg = _bn_group(bn) if use_batch else None
     count = float(P)
+    fused = src is not None and use_batch and pg is None and _FUSE_BN
+    if src is not None and use_batch and not fused:
+        dt, z, ws = src
+        _lib.check(L.ebc_bn_stats(dt, _lib.ptr(z), _lib.ptr(colsum), _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_stats")
     if pg is not None:
         colsum[2 * N].fill_(float(P))
         torch.distributed.all_reduce(colsum, group=pg)
@@ -148,6 +159,14 @@ def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, 
         else:
             _PENDING_NBT.append(bn.num_batches_tracked)
     mom = _bn_momentum(bn) if upd else 0.0
+    if fused:
+        dt, z, ws = src
+        _lib.check(L.ebc_bn_stats_finalize(dt, _lib.ptr(z), _lib.ptr(ws), ws.numel(), P, N, float(bn.eps), mom,
+                                           _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()), _lib.ptr(mean),
+                                           _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),
+                                           _lib.ptr(bn.running_mean) if upd else None,
+                                           _lib.ptr(bn.running_var) if upd else None, None, st), "ebc_bn_stats_finalize")
+        return mean, rstd, scale, shift, count, pg, colsum
     _lib.check(L.ebc_bn_finalize(_lib.ptr(colsum) if use_batch else None, count, float(bn.eps), mom,
                                  _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()), _lib.ptr(mean),
                                  _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),
@@ -163,6 +182,13 @@ def _batch_norm_bwd(L, gamma: Tensor, state, dnext: Tensor, mask: Optional[Tenso
     from this rank's sums, the input-gradient coefficients from the all-reduced sums and count."""
     mean, rstd, scale, shift, count, pg, colsum = state
     f32 = dict(device=dev, dtype=torch.float32)
+    if pg is None and _FUSE_BN:                    # no exchange: column sums and finalize in one launch
+        dg, db, coef = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty(3, N, **f32)
+        _lib.check(L.ebc_bn_bwd_reduce_finalize(_lib.dtype_code(z.dtype), _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z),
+                                                _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),
+                                                _lib.ptr(gamma.detach()), _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef),
+                                                _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce_finalize")
+        return dg, db, coef
     sums = torch.empty(2 * N + (pg is not None), device=dev, dtype=torch.float64)
     _lib.check(L.ebc_bn_bwd_reduce(_lib.dtype_code(z.dtype), _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z),
                                    _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(sums),
@@ -242,10 +268,7 @@ class _ResBlockFn(torch.autograd.Function):
                 if use_batch else None
 
         def stats(z, bn, rows, C):
-            cs = colsum_for(bn)
-            if cs is not None:
-                _lib.check(L.ebc_bn_stats(dt, _lib.ptr(z), _lib.ptr(cs), _lib.ptr(ws), ws.numel(), rows, C, st), "ebc_bn_stats")
-            return _batch_norm_fwd(L, bn, cs, rows, C, training, dev, st)
+            return _batch_norm_fwd(L, bn, colsum_for(bn), rows, C, training, dev, st, src=(dt, z, ws))
 
         W1, W1t = _prep_1x1(L, wts[0], cdtype, st)
         W3, W3t = _prep_1x1(L, wts[2], cdtype, st)
@@ -467,10 +490,7 @@ class _BottleneckFn(torch.autograd.Function):
         z1 = torch.empty(P, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(x), _lib.ptr(W1), _lib.ptr(z1), None, None, None, P, N, C, st),
                    "ebc_gemm(conv1)")
-        cs1 = colsum_for(bns[0])
-        if cs1 is not None:
-            _lib.check(L.ebc_bn_stats(dt, _lib.ptr(z1), _lib.ptr(cs1), _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_stats")
-        s1 = _batch_norm_fwd(L, bns[0], cs1, P, N, training, dev, st)
+        s1 = _batch_norm_fwd(L, bns[0], colsum_for(bns[0]), P, N, training, dev, st, src=(dt, z1, ws))
         h1pad = torch.empty(Q, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_bn_relu_pad(dt, _lib.ptr(z1), _lib.ptr(s1[2]), _lib.ptr(s1[3]), _lib.ptr(h1pad), B, H, W, N,
                                      st), "ebc_bn_relu_pad")
@@ -487,10 +507,7 @@ class _BottleneckFn(torch.autograd.Function):
         z3 = torch.empty(P, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_gemm(dt, 0, 0, _lib.ptr(h2), _lib.ptr(W3), _lib.ptr(z3), None, None, None, P, N, N, st),
                    "ebc_gemm(conv3)")
-        cs3 = colsum_for(bns[2])
-        if cs3 is not None:
-            _lib.check(L.ebc_bn_stats(dt, _lib.ptr(z3), _lib.ptr(cs3), _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_stats")
-        s3 = _batch_norm_fwd(L, bns[2], cs3, P, N, training, dev, st)
+        s3 = _batch_norm_fwd(L, bns[2], colsum_for(bns[2]), P, N, training, dev, st, src=(dt, z3, ws))
         y = torch.empty(B, H, W, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_bn_add_relu(dt, _lib.ptr(z3), _lib.ptr(s3[2]), _lib.ptr(s3[3]), _lib.ptr(feat), up, _lib.ptr(y),
                                      B, H, W, N, st), "ebc_bn_add_relu")

@@ -304,6 +304,17 @@ int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int B, int h, i
  *                          identity branch's gradient). */
 int ebc_dec_upsample(int dtype, const float* feat, void* x, int B, int h, int w, int C, int up, ebc_stream_t stream);
 int ebc_bn_stats(int dtype, const void* z, double* colsum, void* ws, size_t wsb, long P, int C, ebc_stream_t stream);
+/* ebc_bn_stats + ebc_bn_finalize (count = P) in two launches instead of three, for BatchNorms whose statistics need no
+ * SyncBatchNorm exchange between the two (models/utils.py / _clip/image_encoder.py BatchNorm2d, train mode);
+ * colsum_out (may be NULL) receives the f64 sums ebc_bn_stats would. */
+int ebc_bn_stats_finalize(int dtype, const void* z, void* ws, size_t wsb, long P, int C, float eps, float momentum,
+                          const float* gamma, const float* beta, float* mean, float* rstd, float* scale, float* shift,
+                          float* running_mean, float* running_var, double* colsum_out, ebc_stream_t stream);
+/* ebc_bn_bwd_reduce + ebc_bn_bwd_finalize (count = P) in two launches instead of three (no SyncBatchNorm exchange) */
+int ebc_bn_bwd_reduce_finalize(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
+                               const float* rstd, const float* scale, const float* shift, const float* gamma,
+                               float* dgamma, float* dbeta, float* coef, void* ws, size_t wsb, long P, int C,
+                               ebc_stream_t stream);
 int ebc_bn_relu(int dtype, const void* z, const float* scale, const float* shift, void* out, long P, int C,
                 ebc_stream_t stream);
 int ebc_bn_bwd_apply_flat(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
