@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from collections import OrderedDict
 from typing import Any, Dict, List, Optional, Tuple, Union
 
@@ -364,6 +365,10 @@ def _bn_momentum(bn: nn.Module) -> float:
     return 1.0 / float(bn.num_batches_tracked.item())
 
 
+# EBC_BN_FUSED=0: the three-launch BatchNorm backward statistics path (A/B and debugging)
+_FUSE_BN = os.environ.get("EBC_BN_FUSED", "1") != "0"
+
+
 class _DecoderFn(torch.autograd.Function):
     """BasicBlock(768, 768) (models/utils.py:254-303) after the x`up` bilinear reduction adapt
     (models/clip/model.py:195-196), on libebc_hip.so: implicit-GEMM 3x3 convs, BatchNorm statistics in
@@ -472,12 +477,20 @@ class _DecoderFn(torch.autograd.Function):
         for i in (1, 0):
             z, mean, rstd, scale, shift, count, pg, colsum = ctx.outs[i]
             gm = (g1, g2)[i]
-            sums = torch.empty(2 * N + (pg is not None), device=dev, dtype=torch.float64)
-            _lib.check(L.ebc_bn_bwd_reduce(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
-                                           _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(sums),
-                                           _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce")
             dg, db, coef = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty(3, N, **f32)
-            if pg is not None:
+            fused = pg is None and count == float(P) and _FUSE_BN
+            if fused:
+                # no exchange: column sums and finalize in one launch (ebc_bn_bwd_reduce_finalize, count = P)
+                _lib.check(L.ebc_bn_bwd_reduce_finalize(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
+                                                        _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),
+                                                        _lib.ptr(gm.detach()), _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef),
+                                                        _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce_finalize")
+            else:
+                sums = torch.empty(2 * N + (pg is not None), device=dev, dtype=torch.float64)
+                _lib.check(L.ebc_bn_bwd_reduce(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
+                                               _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(sums),
+                                               _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce")
+            if not fused and pg is not None:
                 # SyncBatchNorm backward (torch nn/modules/_functions.py, C5): d gamma / d beta come from THIS
                 # rank's sums (DDP then averages them over the ranks); the input gradient uses the all-reduced
                 # sums and the all-reduced count
@@ -487,7 +500,7 @@ class _DecoderFn(torch.autograd.Function):
                 sums[2 * N:].copy_(colsum[2 * N:])                          # the forward's all-reduced count
                 _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
                                                  None, None, _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize(sync)")
-            else:
+            elif not fused:
                 _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
                                                  _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize")
             dzpad = torch.empty(Q, N, device=dev, dtype=cdtype)
