@@ -63,6 +63,11 @@ def parse(argv=None):
     ap.add_argument("--cpu-crops", type=int, default=16, help="crops per CPU-baseline step (BASELINE.md: 16)")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps after 3 warm-up (BASELINE.md)")
     ap.add_argument("--no-probe", action="store_true", help="skip the instrumented in-step kernel timing pass")
+    ap.add_argument("--no-trace", action="store_true",
+                    help="in-step durations from the HIP events only (no torch.profiler kernel trace; for runs under rocprofv3)")
+    ap.add_argument("--classes-out", default=None,
+                    help="write the kernel class of every instrumented launch of one step, in launch order, as JSON "
+                         "(tools/pmc_step.py maps rocprofv3 --pmc dispatches to classes with it)")
     ap.add_argument("--eval", action="store_true",
                     help="SURVEY §8(d) config 5 instead: sliding-window eval of 2048x3072 images (window = stride = 224, "
                          "140 tiles per image, tiles sharded over ranks); --steps images timed; --dtype fp32 is the "
@@ -230,9 +235,43 @@ def _attn_flops(B, L, H, d=64):
     return 4.0 * B * H * L * L * d
 
 
-def probe_steps(step, first, n, device, counts_of, cells=784):
-    """Run n extra steps with every instrumented launch bracketed by HIP events (ebc_probe_*); returns the
-    per-step kernel classes sorted by time, and the Sinkhorn roofline entry."""
+# kernel-name families of the probe kinds (the launch order of a family's kernels = the order of its probe records)
+_FAMILY = {"gemm": ("gemm_nt_kernel",), "dace_loss": ("dace_loss_kernel",),
+           "attn_fwd": ("attn_fwd_kernel",), "attn_bwd_dq": ("attn_bwd_dq_kernel", "attn_bwd_fused_kernel"),
+           "attn_bwd_dkv": ("attn_bwd_dkv_kernel",), "ln_fwd": ("ln_fwd_kernel",), "ln_bwd": ("ln_bwd_kernel",)}
+
+
+def family_of(name):
+    for fam, keys in _FAMILY.items():
+        if any(k in name for k in keys):
+            return fam
+    return None
+
+
+def trace_steps(step, first, n):
+    """Device timestamps of every kernel of n steps in launch order, [(name, duration_us)]: the runtime's kernel
+    activity records (torch.profiler / roctracer: the source rocprofv3 --kernel-trace reads), so a kernel's
+    duration is its own, with nothing inserted between launches (None when the profiler yields no kernels)."""
+    from torch.profiler import ProfilerActivity, profile
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for i in range(n):
+            step(first + i)
+        torch.cuda.synchronize()
+    evs = []
+    for e in prof.profiler.kineto_results.events():
+        if str(e.device_type()).endswith("CUDA") and e.duration_ns() > 0:
+            evs.append((e.start_ns(), e.name(), e.duration_ns() / 1e3))
+    evs.sort()
+    return [(nm, d) for _, nm, d in evs] or None
+
+
+def probe_steps(step, first, n, device, counts_of, cells=784, trace=True, classes_out=None):
+    """Per-step kernel classes (shape + epilogue of every instrumented launch, ebc_probe_*) sorted by time, and
+    the Sinkhorn roofline entry.  The classes come from n steps whose launches are bracketed by HIP events; their
+    durations from n further steps traced without anything between the launches (trace_steps), matched to the
+    classes by launch order per kernel family; the event durations (which include the gaps the events add) are
+    kept as `event_avg_us` and are the fallback when the trace does not match."""
     from ebc_amd import _lib
     L = _lib.lib()
     cap = 8192
@@ -245,9 +284,33 @@ def probe_steps(step, first, n, device, counts_of, cells=784):
     got = L.ebc_probe_end(recs, cap)
     if got < 0:
         raise RuntimeError("ebc_probe_end failed")
+    recs = list(recs[:min(got, cap)])
+    # the same launch sequence again, traced: per family, the k-th kernel of the family is the k-th probe record
+    if trace:
+        try:
+            trace = trace_steps(step, first + n, n)
+        except Exception as exc:                   # profiler unavailable: event durations only
+            print(f"bench.py: kernel trace unavailable ({exc}); in-step durations from HIP events", file=sys.stderr)
+            trace = None
+    traced = [None] * len(recs)
+    if trace:
+        by_fam = {}
+        for nm, d in trace:
+            f = family_of(nm)
+            if f:
+                by_fam.setdefault(f, []).append(d)
+        want = {}
+        for i, r in enumerate(recs):
+            want.setdefault(_lib.PROBE_KINDS.get(r.kind, ""), []).append(i)
+        for fam, idx in want.items():
+            got_d = by_fam.get(fam, [])
+            if len(got_d) == len(idx):
+                for i, d in zip(idx, got_d):
+                    traced[i] = d
     classes = {}
     dace = []
-    for r in recs[:min(got, cap)]:
+    keys = []
+    for ri, r in enumerate(recs):
         kind = _lib.PROBE_KINDS.get(r.kind, str(r.kind))
         if kind == "gemm":
             mode = {0: "", 1: " conv3x3", 2: " conv3x3-wgrad"}[r.mode]
@@ -256,19 +319,30 @@ def probe_steps(step, first, n, device, counts_of, cells=784):
             flops = 2.0 * r.m * r.n * r.k
         elif kind == "dace_loss":
             key, flops = f"dace_loss_kernel B={r.m} g={r.k}", 0.0
-            dace.append(r.ms)
+            dace.append(traced[ri] * 1e-3 if traced[ri] is not None else r.ms)
         elif kind.startswith("attn"):
             key, flops = f"{kind} B={r.m} L={r.n} heads={r.k}", _attn_flops(r.m, r.n, r.k)
         else:
             key, flops = f"{kind} rows={r.m}", 0.0
-        c = classes.setdefault(key, {"kernel": key, "launches": 0, "ms": 0.0, "flop_per_launch": flops})
+        keys.append(key)
+        c = classes.setdefault(key, {"kernel": key, "launches": 0, "ms": 0.0, "ev_ms": 0.0, "flop_per_launch": flops,
+                                     "traced": 0})
         c["launches"] += 1
-        c["ms"] += r.ms
+        c["ev_ms"] += r.ms
+        c["ms"] += traced[ri] * 1e-3 if traced[ri] is not None else r.ms
+        c["traced"] += traced[ri] is not None
+    if classes_out:
+        order = []
+        for ri, r in enumerate(recs[:len(recs) // n]):
+            order.append({"family": _lib.PROBE_KINDS.get(r.kind, str(r.kind)), "kernel": keys[ri]})
+        with open(classes_out, "w") as f:
+            json.dump({"steps_per_window_note": "one step; repeats every step", "launches": order}, f, indent=0)
     out = []
     for c in classes.values():
         avg_us = c["ms"] / c["launches"] * 1e3
         rec = {"kernel": c["kernel"], "per_step_us": round(c["ms"] / n * 1e3, 1), "launches_per_step": c["launches"] / n,
-               "avg_us": round(avg_us, 2)}
+               "avg_us": round(avg_us, 2), "event_avg_us": round(c["ev_ms"] / c["launches"] * 1e3, 2),
+               "timing": "kernel trace" if c["traced"] == c["launches"] else "hip events"}
         if c["flop_per_launch"]:
             rec["tflops"] = round(c["flop_per_launch"] / (avg_us * 1e-6) / 1e12, 1)
             rec["flop_per_launch"] = c["flop_per_launch"]
@@ -279,8 +353,9 @@ def probe_steps(step, first, n, device, counts_of, cells=784):
         # 4 n M (2 I + I/10) + 3*4*M + 8 n bytes per crop, M = 784 cells (28x28; 3136 at 448),
         # I = 100 iterations executed
         byts = []
+        s0 = first + n if all(t is not None for t in traced) else first     # the steps the durations come from
         for i in range(n):
-            cnt = counts_of(first + i)
+            cnt = counts_of(s0 + i)
             byts.append(sum(4 * c * cells * (2 * 100 + 10) + 3 * 4 * cells + 8 * c for c in cnt if c > 0))
         avg_b, avg_s = sum(byts) / len(byts), sum(dace) / len(dace) * 1e-3
         sink = {"bound": "hbm", "achieved": round(avg_b / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -472,7 +547,8 @@ def main():
     if not args.no_probe:
         first = args.warmup + args.steps
         kernels, sink = probe_steps(step, first, 3, device, lambda i: step.pool[i % len(step.pool)][3],
-                                    cells=(args.size // 8) ** 2)
+                                    cells=(args.size // 8) ** 2, trace=not args.no_trace,
+                                    classes_out=args.classes_out if rank == 0 else None)
     if rank == 0:
         peak = MFMA_PEAK_TF[args.dtype]
         rn = args.model == "clip_resnet50"

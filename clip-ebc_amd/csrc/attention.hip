@@ -484,11 +484,7 @@ template <class E, int NW, int LFIX> int attn_fwd_nw(const void* qkv, void* out,
 {
     using C = AttnCfg<E>;
     const size_t lds = 2 * C::TILE_BYTES;
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)attn_fwd_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
-        attr = true;
-    }
+    if (!ensure_lds<attn_fwd_kernel<E, NW, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
     const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_FWD, 0, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_fwd_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
@@ -509,12 +505,8 @@ template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void
 {
     using C = AttnCfg<E>;
     const size_t lds_dq = 2 * C::TILE_BYTES, lds_kv = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dq) != hipSuccess) return EBC_E_LAUNCH;
-        if (hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv) != hipSuccess) return EBC_E_LAUNCH;
-        attr = true;
-    }
+    if (!ensure_lds<attn_bwd_dq_kernel<E, NW, LFIX>>((int)lds_dq, st) || !ensure_lds<attn_bwd_dkv_kernel<E, NW, LFIX>>((int)lds_kv, st))
+        return EBC_E_LAUNCH;
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
     int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 0, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_bwd_dq_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds_dq, st, (const typename E::T*)qkv,
@@ -534,11 +526,7 @@ template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, cons
 {
     using C = AttnCfg<E>;
     const size_t lds = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<E, NW, LFIX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return EBC_E_LAUNCH;
-        attr = true;
-    }
+    if (!ensure_lds<attn_bwd_fused_kernel<E, NW, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
     // rows > 0: dQ of queries and dK / dV of keys < rows are wanted (the rest of dqkv is left unwritten)
     const int nblk = rows > 0 ? std::min((rows + 16 * NW - 1) / (16 * NW), (L + 16 * NW - 1) / (16 * NW))
                               : (L + 16 * NW - 1) / (16 * NW);
@@ -552,16 +540,11 @@ template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, cons
     return EBC_OK;
 }
 
-// EBC_ATTN_BWD=split: the two backward kernels one after the other (delta through global memory)
-bool attn_bwd_split() {
-    static const bool split = getenv("EBC_ATTN_BWD") && std::string(getenv("EBC_ATTN_BWD")) == "split";
-    return split;
-}
-
 template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
                                   void* dqkv, int B, int L, int H, hipStream_t st, int rows)
 {
-    if (!attn_bwd_split() && E::BYTES == 2) {
+    // 16-bit: dQ and dK/dV roles in one grid; f32 (parity mode): the two kernels one after the other
+    if (E::BYTES == 2) {
         return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows)
                             : attn_bwd_fused_nw<E, 8, 0>(qkv, dout, out, lse, dqkv, B, L, H, st, rows);
     }

@@ -905,12 +905,7 @@ template <int G> int launch(const Params& P0, hipStream_t st)
     P.lds_cap = (int)((LDS_MAX - C::FIXED_BYTES) / (sizeof(float) * C::PER_POINT));
     P.lds_cap_s = (int)((LDS_MAX - C::FIXED_BYTES_C) / (sizeof(float) * C::PER_POINT));
     P.lds_cap_c = (int)((LDS_MAX - C::FIXED_BYTES_C) / (sizeof(float) * C::PER_POINT_C));
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)dace_loss_kernel<G>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX) != hipSuccess)
-            return EBC_E_LAUNCH;
-        attr = true;
-    }
+    if (!ensure_lds<dace_loss_kernel<G>>(LDS_MAX, st)) return EBC_E_LAUNCH;
     static unsigned long long* dprof = nullptr;
     static const bool want_prof = getenv("EBC_DACE_PROF") != nullptr;
     if (want_prof && !dprof && P.B <= 1024) (void)hipMalloc(&dprof, 1024 * 16 * sizeof(unsigned long long));

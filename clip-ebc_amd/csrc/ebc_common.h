@@ -17,6 +17,28 @@
 
 namespace ebc {
 
+// A kernel that asks for more than 64 KiB of dynamic LDS must be opted in with hipFuncSetAttribute, and the attribute
+// is held per device: set it once per (kernel, device) for the device the launch stream belongs to (a process may
+// drive several devices from one thread).  `bytes` must be the kernel's largest request.
+template <auto KERNEL>
+inline bool ensure_lds(int bytes, hipStream_t st)
+{
+    if (bytes <= 64 * 1024) return true;
+    static unsigned long long done = 0;          // bit d: set on device d (benign race: setting twice is harmless)
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    const unsigned long long bit = 1ull << dev;
+    if (__atomic_load_n(&done, __ATOMIC_RELAXED) & bit) return true;
+    int cur = dev;
+    if (hipGetDevice(&cur) != hipSuccess) return false;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return false;
+    const hipError_t e = hipFuncSetAttribute((const void*)KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (e != hipSuccess) return false;
+    __atomic_fetch_or(&done, bit, __ATOMIC_RELAXED);
+    return true;
+}
+
 // Wave-wide reductions on DPP (VALU lane moves) instead of __shfl_xor, which hipcc lowers to six
 // ds_bpermute LDS round trips each followed by lgkmcnt(0): quad xor-1 / xor-2, row half-mirror and
 // row mirror leave every lane with its 16-lane row's total, row_bcast:15 / row_bcast:31 fold the

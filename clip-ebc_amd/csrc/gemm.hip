@@ -116,19 +116,28 @@ template <int I, int N, class F> __device__ __forceinline__ void static_for(F&& 
     }
 }
 
+// output stores (EBC_STORE_NT: non-temporal, experiment builds)
+#ifndef EBC_STORE_NT
+#define EBC_STORE_NT 0
+#endif
+template <class V> __device__ __forceinline__ void st_out(V* p, const V& v) {
+    if constexpr (EBC_STORE_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 template <class TO> __device__ __forceinline__ void store4(TO* p, const float* v);
 template <> __device__ __forceinline__ void store4<float>(float* p, const float* v) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    st_out(reinterpret_cast<f4*>(p), f4{v[0], v[1], v[2], v[3]});
 }
 template <> __device__ __forceinline__ void store4<_Float16>(_Float16* p, const float* v) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     h4 r = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-    *reinterpret_cast<h4*>(p) = r;
+    st_out(reinterpret_cast<h4*>(p), r);
 }
 template <> __device__ __forceinline__ void store4<__bf16>(__bf16* p, const float* v) {
     typedef __bf16 b4 __attribute__((ext_vector_type(4)));
     b4 r = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-    *reinterpret_cast<b4*>(p) = r;
+    st_out(reinterpret_cast<b4*>(p), r);
 }
 template <class T> __device__ __forceinline__ void load4(const T* p, float* v) {
 #pragma unroll
@@ -148,12 +157,12 @@ template <> __device__ __forceinline__ void store8<_Float16>(_Float16* p, const 
     typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     h8 r = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3],
             (_Float16)v[4], (_Float16)v[5], (_Float16)v[6], (_Float16)v[7]};
-    *reinterpret_cast<h8*>(p) = r;
+    st_out(reinterpret_cast<h8*>(p), r);
 }
 template <> __device__ __forceinline__ void store8<__bf16>(__bf16* p, const float* v) {
     typedef __bf16 b8 __attribute__((ext_vector_type(8)));
     b8 r = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3], (__bf16)v[4], (__bf16)v[5], (__bf16)v[6], (__bf16)v[7]};
-    *reinterpret_cast<b8*>(p) = r;
+    st_out(reinterpret_cast<b8*>(p), r);
 }
 template <class T> __device__ __forceinline__ void load8f(const T* p, float* v) {
     typedef T t8 __attribute__((ext_vector_type(8)));
@@ -193,12 +202,18 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // SPL: the split-K epilogue paths are compiled in (only the instances a launch with g.splits > 1 runs: their
 // partial loads / stores beside the accumulators made the register allocator spill every 8-wave tile's epilogue,
 // 256x256: 150-430 registers, even on launches that never split)
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE, bool SPL>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
+// NLW > 0: NLW extra "loader" waves issue every LDS-DMA piece of the ring and the WGM x WGN compute waves only
+// read fragments and issue MFMAs.  A wave's LDS-DMA issue rate bounds the per-CU fill (tools/lab/bw_lab.hip:
+// 4 streaming waves ~105 GB/s, 8 or more ~130 GB/s = the L1 <-> L2 rate, against ~84 GB/s when the 4 compute
+// waves also issue the loads between their MFMAs).
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE, bool SPL, int NLW>
+__global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArgs g)
 {
     static_assert(S >= 2 && S <= 5, "stages");
+    static_assert(NLW == 0 || (MODE == 0 && !SPL), "loader waves: MODE 0 split-free tiles (no block-wide epilogue barriers)");
     using T = typename E::T;
-    constexpr int NW = WGM * WGN;                // waves per workgroup
+    constexpr int NW = WGM * WGN;                // compute waves per workgroup
+    constexpr int NLDR = NLW ? NLW : NW;         // waves that issue the LDS-DMA pieces
     constexpr int EB = E::BYTES;
     constexpr int BK = ROWB / EB;                // K elements per slab row
     constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
@@ -210,18 +225,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     // glds wave-instructions per wave per stage: NLDF full 1-KiB pieces (16-B lanes), plus, when the
     // rows do not divide, NT4 256-B pieces (4-B lanes; there is no 8-B LDS-DMA) per wave, e.g. 256x192
     // tiles of 64-B rows: 3 x 1 KiB + 2 x 256 B
-    constexpr int NLDF = ROWS / (RPI * NW);
-    constexpr int REMR = ROWS - NLDF * RPI * NW;
+    constexpr int NLDF = ROWS / (RPI * NLDR);
+    constexpr int REMR = ROWS - NLDF * RPI * NLDR;
     constexpr int R4 = 256 / ROWB;               // rows per 256-B piece
-    constexpr int NT4 = REMR / (NW * R4);
+    constexpr int NT4 = REMR / (NLDR * R4);
     constexpr bool TAIL = REMR != 0;
     constexpr int NLD = NLDF + NT4;
-    static_assert(REMR == NT4 * NW * R4, "tail pieces");
+    static_assert(REMR == NT4 * NLDR * R4, "tail pieces");
     static_assert(WM % 16 == 0 && WN % 16 == 0, "tiling");
     static_assert(BK % 32 == 0, "k32 MFMA steps");
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lw = NLW ? wave - NW : wave;       // index among the waves that issue the loads
     const int wm = wave / WGN, wn = wave % WGN;
     const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
     const int wg = xcd_remap(blockIdx.x, (int)gridDim.x);
@@ -251,8 +267,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         const bool tail = TAIL && i >= NLDF;
         // full pieces: rows (wave*NLDF + i)*RPI + lane/CPR; tail piece j: 4-B lanes, rows
         // NLDF*RPI*NW + (wave*NT4 + j)*R4 + lane/(4*CPR)
-        const int row = tail ? NLDF * RPI * NW + (wave * NT4 + (i - NLDF)) * R4 + lane / (4 * CPR)
-                             : (wave * NLDF + i) * RPI + lane / CPR;
+        const int row = tail ? NLDF * RPI * NLDR + (lw * NT4 + (i - NLDF)) * R4 + lane / (4 * CPR)
+                             : (lw * NLDF + i) * RPI + lane / CPR;
         const int slot = tail ? (lane % (4 * CPR)) / 4 : lane % CPR;
         const int c = slot ^ swz_row<ROWB>(row);
         const T* base;
@@ -281,10 +297,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         }
         src[i] = base + c * (16 / EB) + (tail ? (lane & 3) * (4 / EB) : 0);
     }
-    auto stage = [&](int buf, int kt) {
-#if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 2)
-        return;                                   // experiment build: no global->LDS traffic
-#endif
+    auto stage_pieces = [&](int buf, int kt) {
         const int ktg = ktbase + kt;
         long oa, ob;
         if constexpr (MODE == 1) {
@@ -303,14 +316,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
         for (int i = 0; i < NLDF; ++i) {
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src[i] + (isa[i] ? oa : ob)),
-                EBC_LDS(dst + (wave * NLDF + i) * 1024), 16, 0, EBC_GLDS_AUX);
+                EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, EBC_GLDS_AUX);
         }
 #pragma unroll
         for (int j = 0; j < NT4; ++j) {
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src[NLDF + j] + (isa[NLDF + j] ? oa : ob)),
-                EBC_LDS(dst + NLDF * NW * 1024 + (wave * NT4 + j) * 256), 4, 0, EBC_GLDS_AUX);
+                EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, EBC_GLDS_AUX);
         }
+    };
+    // the compute waves stage the ring themselves unless loader waves do
+    auto stage = [&](int buf, int kt) {
+        if constexpr (NLW == 0) stage_pieces(buf, kt);
     };
 
     f32x4 acc[TM][TN];
@@ -370,24 +387,45 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
             }
         }
     };
-    auto sync_tile = [&](int next_kt, auto tailc) {
-        // tile next_kt landed (count the later tiles still in flight), every wave done reading the
-        // buffer that the refill below overwrites.  Outside the tail S-2 later tiles are in flight.
+    // tile next_kt landed (count the later tiles still in flight): the issuing wave's counted vmcnt
+    auto wait_tile = [&](int next_kt, auto tailc) {
         if constexpr (decltype(tailc)::value) {
             const int later = (nk - 1 - next_kt) < (S - 2) ? (nk - 1 - next_kt) : (S - 2);
             wait_vmcnt<NLD, S - 2>(later);
         } else {
             asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * NLD) : "memory");
         }
+    };
+    auto sync_tile = [&](int next_kt, auto tailc) {
+        // tile next_kt landed, every wave done reading the buffer that the refill below overwrites.
+        // Outside the tail S-2 later tiles are in flight.
+        if constexpr (NLW == 0) wait_tile(next_kt, tailc);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
+    if constexpr (NLW > 0) {
+        if (wave >= NW) {
+            // loader wave: the compute waves' ring schedule (one barrier per k-tile, the buffer of tile kt
+            // refilled with tile kt + S right after the barrier that retires its reads), then exit
+            for (int s = 0; s < S - 1; ++s)
+                if (s < nk) stage_pieces(s, s);
+            wait_tile(0, std::true_type{});
+            __builtin_amdgcn_s_barrier();
+            if (S - 1 < nk) stage_pieces(S - 1, S - 1);
+            for (int kt = 0; kt + 1 < nk; ++kt) {
+                wait_tile(kt + 1, std::true_type{});
+                __builtin_amdgcn_s_barrier();
+                if (kt + S < nk) stage_pieces(kt % S, kt + S);
+            }
+            return;
+        }
+    }
 
     // 4-wave RESID tiles (one wave per SIMD: registers to spare): the f32 residual operand of the epilogue is
     // loaded before the ring fills, so its latency hides under the first tiles' instead of being paid after the
     // K loop (vmcnt retires loads in order: issued any later, a counted ring wait would block on it mid-loop)
-    constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && EBC_RESID_PREFETCH;
+    constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && NW + NLW <= 8 && EBC_RESID_PREFETCH;
     typedef float rp8_t __attribute__((ext_vector_type(8)));
     typedef float rp4_t __attribute__((ext_vector_type(4)));
     rp8_t rp8[PREF ? TM : 1][TN / 2 > 0 ? TN / 2 : 1];
@@ -425,9 +463,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
     load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
     auto mma_all = [&](typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
-#if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 1)
-        return;                                   // experiment build: no MFMA (fragment reads die too)
-#endif
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -488,18 +523,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     int kt0 = 0;
     for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
     for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
-#if defined(EBC_GEMM_EXP) && (EBC_GEMM_EXP & 4)
-    // experiment build: no epilogue (a never-taken store keeps the K loop alive)
-    if (g.K == 12345) {
-        float s = 0.f;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int b = 0; b < TN; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
-        reinterpret_cast<float*>(g.C)[tid] = s;
-    }
-    return;
-#endif
 
     if (SPL && g.splits > 1 && g.cnt == nullptr) {
         // split-K without a last arriver (deep splits of the weight-gradient products): every split stores its
@@ -789,26 +812,21 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_kernel(GemmArgs g)
     }   // staged epilogue (MODE 1 / 2)
 }
 
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE, bool SPL>
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE, bool SPL, int NLW = 0>
 int launch_gemm_k(const GemmArgs& g, hipStream_t st)
 {
     constexpr int WM = BM / WGM;
     constexpr int LDS = gemm_lds_bytes<BM, BN, S, ROWB, WM>();
     static_assert(LDS <= 160 * 1024, "LDS");
     constexpr int BK = ROWB / E::BYTES;
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
-            return EBC_E_LAUNCH;
-        attr = true;
-    }
+    if (!ensure_lds<gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL, NLW>>(LDS, st)) return EBC_E_LAUNCH;
     if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
     const int tiles = g.ntile ? g.ntile : ((g.M + BM - 1) / BM) * (g.N / BN) - g.tile0;
     if (tiles <= 0 || g.tile0 + tiles > ((g.M + BM - 1) / BM) * (g.N / BN)) return EBC_E_ARG;
     const int nwg = tiles * g.splits;
     const int pi = probe_on() ? probe_start(EBC_PROBE_GEMM, EPI, BM, BN, MODE, g.M, g.N, g.K, st) : -1;
-    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL>), dim3(nwg), dim3(64 * WGM * WGN), LDS, st, g);
+    hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL, NLW>), dim3(nwg),
+                       dim3(64 * (WGM * WGN + NLW)), LDS, st, g);
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
@@ -816,21 +834,28 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
 
 // Split-K launches exist for the weight gradients (MODE 2, and MODE 0 f32 stores), the conv GEMMs' tail tiles
 // (MODE 1) and forced MODE 0 store splits; every other product runs the split-free instance.
-template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0>
+template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0, int NLW = 0>
 int launch_gemm(const GemmArgs& g, hipStream_t st)
 {
     if (g.splits > 1) {
-        if constexpr (MODE != 0 || EPI == EPI_STORE) return launch_gemm_k<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, true>(g, st);
+        if constexpr (NLW == 0 && (MODE != 0 || EPI == EPI_STORE))
+            return launch_gemm_k<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, true>(g, st);
         else return EBC_E_UNSUPPORTED;
     }
-    return launch_gemm_k<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, false>(g, st);
+    return launch_gemm_k<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, false, NLW>(g, st);
 }
+
+}  // namespace
+// tools/lab/gemm_lab.hip includes the kernel templates above without the dispatch and the C-ABI below
+#ifndef EBC_GEMM_LAB
+namespace {
 
 // Tile configurations (EBC_GEMM_CFG=<n> forces one; EBC_GEMM_SPLITS=<s> forces the split count):
 //   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   6: 256x128/8w
 //   7: 256x256/8w   (2-stage rings of 128-B K rows)
 //   8: 128x64 S3   9: 128x128 S3   10: 256x128/8w S3   11: 192x128/8w S3   12: 128x64 S4   13: 128x96 S3
 //   14: 128x192 S3   (r02: 8-wave 128x96 S3 / S4 measured within noise of the 4-wave tile: not built)
+//   15: 128x96 S3 + 4 loader waves   16: 128x96 S4 + 4 loader waves   (r03, tools/lab/gemm_lab.hip)
 //   20: 256x256/8w  21: 256x128/8w  22: 128x256/8w  24: 128x128/4w   (4-stage rings
 //       of 64-B K rows, 16-bit only; r01: a 256x192 4-stage ring measured 10-15 % slower than
 //       cfg 3's 2-stage 128-B ring on the decoder convs and the MLP, so no such config is built)
@@ -840,7 +865,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 struct TileCfg { int id, bm, bn; };
 constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {6, 256, 128},
                             {7, 256, 256}, {8, 128, 64}, {9, 128, 128}, {10, 256, 128}, {11, 192, 128}, {12, 128, 64},
-                            {13, 128, 96}, {14, 128, 192}, {20, 256, 256}, {21, 256, 128}, {22, 128, 256}, {24, 128, 128}};
+                            {13, 128, 96}, {14, 128, 192}, {15, 128, 96}, {16, 128, 96}, {20, 256, 256}, {21, 256, 128},
+                            {22, 128, 256}, {24, 128, 128}};
 const TileCfg* find_cfg(int id) {
     for (const TileCfg& c : CFGS) if (c.id == id) return &c;
     return nullptr;
@@ -890,7 +916,12 @@ int pick_cfg(int M, int N, int K, bool wide) {
     // with more than one wave of 128x96 tiles (32 crops per GPU, SURVEY config 4: M = 7328) the 2-stage ring
     // wins: two workgroups fit a CU (56 KB of LDS instead of 84), s5 sweep tools/gpu78.sh: c_proj + residual
     // 51.5 -> 44.2 us, out-proj 21.9 -> 18.9, dH2 44.2 -> 37.8, dH 33.2 -> 29.5
-    if (N % 96 == 0 && N < 2048 && K >= 768) return ntiles(M, N, 128, 96) > NUM_CU ? 5 : 13;
+    // r03 (tools/lab/gemm_lab.hip, interleaved, each launch right after the c_fc product as in the step): with 4
+    // loader waves issuing the LDS-DMA pieces (gemm_nt_kernel NLW) the compute waves only read fragments and
+    // issue MFMAs -- c_proj + residual 28.5 -> 26.6 us (4-stage ring), its dX 26.3 -> 24.0, dX of QKV 20.7 ->
+    // 19.6, out-proj + residual 14.7 -> 14.2 (3 stages); 7 loader waves or a 5-stage ring gained nothing more.
+    // More than one wave of tiles keeps the 2-stage 4-wave tile (two workgroups a CU).
+    if (N % 96 == 0 && N < 2048 && K >= 768) return ntiles(M, N, 128, 96) > NUM_CU ? 5 : (K >= 2304 ? 16 : 15);
     return 2;
 }
 // Tile order for the wide-N products (>= 12 tile columns): with the row-major order each XCD's 1/8 of the
@@ -966,6 +997,8 @@ int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
             case 12: return launch_gemm<E, TO, EPI, 128, 64, 4>(g, st);
             case 13: return launch_gemm<E, TO, EPI, 128, 96, 3>(g, st);
             case 14: return launch_gemm<E, TO, EPI, 128, 192, 3>(g, st);
+            case 15: return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, 0, 4>(g, st);
+            case 16: return launch_gemm<E, TO, EPI, 128, 96, 4, 2, 2, 128, 0, 4>(g, st);
             case 20: return launch_gemm<E, TO, EPI, 256, 256, 4, 4, 2, 64>(g, st);
             case 21: return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64>(g, st);
             case 22: return launch_gemm<E, TO, EPI, 128, 256, 4, 2, 4, 64>(g, st);
@@ -1436,3 +1469,4 @@ extern "C" int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, in
     }
     return cfg;
 }
+#endif  // EBC_GEMM_LAB

@@ -54,9 +54,11 @@ int vpt_grad(int dtype, float* dX, void* dXt, float* dvpt, int B, int L, int NVP
              hipStream_t st);
 int head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
              float* logits, float* expo, int P, int HW, int NB, int embed, hipStream_t st);
+// d bias / d logit_scale as per-block partials (ws: head_bwd_ws_bytes) summed in block order by a second launch
+size_t head_bwd_ws_bytes(int P, int embed);
 int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale, const float* anchors,
              const float* dlogits, const float* dexp, const float* gscale, void* dZ, float* dbias, float* dscale,
-             int P, int HW, int NB, int embed, hipStream_t st);
+             int P, int HW, int NB, int embed, void* ws, size_t wsb, hipStream_t st);
 int attn_delta(int dtype, const void* dO, const void* O, float* delta, int B, int L, int H, hipStream_t st);
 int cast_f32(int dtype, const float* in, void* out, size_t n, hipStream_t st);
 int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st);

@@ -158,23 +158,11 @@ extern "C" int ebc_sinkhorn(const float* a, const float* b, const float* C, int 
              (float*)workspace};
     const hipStream_t st = (hipStream_t)stream;
     if (klds) {
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute((const void*)sinkhorn_dense_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    LDS_MAX) != hipSuccess)
-                return EBC_E_LAUNCH;
-            attr = true;
-        }
+        if (!ensure_lds<sinkhorn_dense_kernel<true>>(LDS_MAX, st)) return EBC_E_LAUNCH;
         const size_t lds = uv_bytes(na, nb) + sizeof(float) * (size_t)na * nb;
         hipLaunchKernelGGL(sinkhorn_dense_kernel<true>, dim3(1), dim3(NT), lds, st, p);
     } else {
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute((const void*)sinkhorn_dense_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    LDS_MAX) != hipSuccess)
-                return EBC_E_LAUNCH;
-            attr = true;
-        }
+        if (!ensure_lds<sinkhorn_dense_kernel<false>>(LDS_MAX, st)) return EBC_E_LAUNCH;
         hipLaunchKernelGGL(sinkhorn_dense_kernel<false>, dim3(1), dim3(NT), uv_bytes(na, nb), st, p);
     }
     EBC_CHECK_LAUNCH();

@@ -113,33 +113,6 @@ Layout carve(void* ws, int B, int L, int G, int layers, int dtype, int training)
     return lay;
 }
 
-// Crop-split concurrency: the encoder's crops are independent, so the two halves of the batch run their
-// layers on two HIP streams (the caller's and a library-owned side stream, forked and joined with
-// events).  One half's GEMM store phases, attention and LayerNorms then overlap the other half's
-// MFMA main loops.  Opt-in (EBC_VIT_STREAMS=2): measured 2.9 % SLOWER per train step on MI355X (r01,
-// interleaved A/B, 3080 vs 3172 crops/s) -- the half-batch GEMMs lose more tile efficiency than the
-// overlap wins.
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-SideStream* side_stream() {
-    static SideStream ss[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    SideStream& r = ss[dev];
-    if (!r.s) {
-        if (hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        if (hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-        if (hipEventCreateWithFlags(&r.join, hipEventDisableTiming) != hipSuccess) return nullptr;
-    }
-    return &r;
-}
-int vit_streams() {
-    static const int v = [] { const char* e = getenv("EBC_VIT_STREAMS"); return e ? atoi(e) : 1; }();
-    return v;
-}
-
 bool check_weights(const EbcVitWeights* w) {
     return w && w->layers > 0 && w->layer && w->width == WIDTH && w->heads == HEADS && w->patch == 16 && w->num_vpt >= 0;
 }
@@ -211,20 +184,9 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
         EBC_TRY(gemm(EBC_EPI_RESID, 1, Gm, p.w_proj, Xn, p.b_proj, X1, nullptr, WIDTH, MLP));
         return EBC_OK;
     };
-    SideStream* ss = (vit_streams() >= 2 && B >= 2 && !lay.gws) ? side_stream() : nullptr;
-    if (ss) {
-        const int bh = (B + 1) / 2;
-        if (hipEventRecord(ss->fork, st) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
-            return EBC_E_LAUNCH;
-        for (int l = 0; l < layers; ++l) {                              // interleaved enqueue: both halves start early
-            EBC_TRY(block(l, 0, bh, st));
-            EBC_TRY(block(l, bh, B - bh, ss->s));
-        }
-        if (hipEventRecord(ss->join, ss->s) != hipSuccess || hipStreamWaitEvent(st, ss->join, 0) != hipSuccess)
-            return EBC_E_LAUNCH;
-    } else {
-        for (int l = 0; l < layers; ++l) EBC_TRY(block(l, 0, B, st));
-    }
+    // (the two crop halves on two streams, overlapping one half's GEMM store phases with the other's main loops,
+    // measured 2.9 % slower per train step, r01: the half-batch GEMMs lose more tile efficiency than the overlap wins)
+    for (int l = 0; l < layers; ++l) EBC_TRY(block(l, 0, B, st));
     // ln_post on the patch rows only (CLS and prompt rows are dropped, model.py:185-188)
     EBC_TRY(ebc::layernorm_fwd(EBC_F32, lay.X[layers], G, L, 1 + NV, w->ln_post_g, w->ln_post_b, feat, nullptr,
                                lay.mpost, lay.rpost, B * G, WIDTH, st));
@@ -232,7 +194,7 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
 }
 
 extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int dtype, void* ws, size_t ws_bytes,
-                                const float* dfeat, float* const* dvpt, long vpt_bstride, ebc_stream_t stream)
+                                const float* dfeat, float* const* dvpt, long vpt_bstride, int flags, ebc_stream_t stream)
 {
     if (!check_weights(w) || !ws || !dfeat) return EBC_E_ARG;
     hipStream_t st = (hipStream_t)stream;
@@ -263,7 +225,7 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         { float* t = dX; dX = dXo; dXo = t; }
         // attention half: dO = dX1 . W_out;  dQKV = attn'(...);  dH = dQKV . W_qkv;  dX = dX1 + LN1'(dH)
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dXt, p.wt_out, lay.dO, nullptr, M, WIDTH, WIDTH));
-        if (l == 0 && NV > 0 && dvpt && dvpt[0]) {
+        if (l == 0 && NV > 0 && dvpt && dvpt[0] && !(flags & EBC_VIT_BWD_FULL_LAYER0)) {
             // layer 0: the frozen encoder below (ln_pre, embeddings, conv1) takes no gradient, so only the prompt
             // rows' input gradient is wanted -- dQ / dK / dV of the first query and key block (rows 1..NV), dH on
             // the B*NV prompt rows (row-mapped A operand), ln_1's backward of those rows straight into the prompt
@@ -325,12 +287,17 @@ extern "C" int ebc_head_fwd(int dtype_z, const void* Z, const float* text, const
 {
     return ebc::head_fwd(dtype_z, Z, text, logit_scale, anchors, logits, expo, P, HW, NB, embed, (hipStream_t)stream);
 }
+extern "C" size_t ebc_head_bwd_workspace_bytes(int P, int embed)
+{
+    return ebc::head_bwd_ws_bytes(P, embed);
+}
 extern "C" int ebc_head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
                             const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
-                            float* dbias, float* dscale, int P, int HW, int NB, int embed, ebc_stream_t stream)
+                            float* dbias, float* dscale, int P, int HW, int NB, int embed, void* workspace,
+                            size_t workspace_bytes, ebc_stream_t stream)
 {
     return ebc::head_bwd(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW,
-                         NB, embed, (hipStream_t)stream);
+                         NB, embed, workspace, workspace_bytes, (hipStream_t)stream);
 }
 extern "C" int ebc_cast_f32(int dtype, const float* in, void* out, size_t n, ebc_stream_t stream)
 {

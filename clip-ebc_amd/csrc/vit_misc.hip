@@ -338,8 +338,8 @@ __global__ __launch_bounds__(256) void vpt_grad_kernel(float* __restrict__ dX, T
 // One wave per pixel, CH channels (CH / 64 per lane, in float4 pieces 256 apart), NB <= 16 bins; the text
 // features are normalised in LDS.  CH = 512 (ViT-B/16) or 1024 (ResNet-50, models/clip/model.py:85-95).
 // pixels per 4-wave block (r02, tools/kbench.py head): the forward is fastest with one pixel per wave (4: 15.7 us vs
-// 18.5 at 16, 16 crops); the backward with 8 per wave (32: 38.2 vs 42.2 us), since each block adds its d bias row to
-// the same CH addresses with atomics and fewer blocks contend less (4 per block: 86 us)
+// 18.5 at 16, 16 crops); the backward with 8 per wave (32: 38.2 vs 42.2 us; fewer blocks also mean fewer d bias
+// partial rows for head_bias_finalize_kernel to sum)
 constexpr int HEAD_FWD_PPB = 4, HEAD_BWD_PPB = 32;
 
 template <class TZ, int CH>
@@ -432,12 +432,13 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const TZ* __restrict__ Z,
 }
 
 // dZ = d/dZ of (logits, exp) given upstream dlogits [B,NB,HW], dexp [B,1,HW] (x *gscale if given);
-// also d bias (column sums of dZ) and d logit_scale, accumulated with atomics (zeroed by the launcher).
+// also this block's d bias (column sums of its dZ rows) and d logit_scale partial: part[block][0..CH) and
+// part[block][CH] (plain stores; head_bias_finalize_kernel sums the blocks in order -- bit-reproducible, where float
+// atomics from every block into the same CH addresses were neither reproducible nor free of contention).
 template <class TZ, class TD, int CH>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z, const float* text, const float* logit_scale,
                                                        const float* anchors, const float* dlogits, const float* dexp,
-                                                       const float* gscale, TD* dZ, float* dbias, float* dscale,
-                                                       int P, int HW, int NB)
+                                                       const float* gscale, TD* dZ, float* part, int P, int HW, int NB)
 {
     constexpr int NV = CH / 64;
     extern __shared__ __attribute__((aligned(16))) float tn[];
@@ -514,11 +515,32 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
         for (int j = 0; j < 4; ++j) dbias_l[w * CH + 256 * q + 4 * lane + j] = db[4 * q + j];
     if (lane == 0) dsc_l[w] = dsc;
     __syncthreads();
-    for (int c = threadIdx.x; c < CH; c += blockDim.x) {
-        const float t = dbias_l[c] + dbias_l[CH + c] + dbias_l[2 * CH + c] + dbias_l[3 * CH + c];
-        if (dbias) atomicAdd(dbias + c, t);
+    if (!part) return;
+    float* pr = part + (size_t)blockIdx.x * (CH + 1);
+    for (int c = threadIdx.x; c < CH; c += blockDim.x)
+        pr[c] = (dbias_l[c] + dbias_l[CH + c]) + (dbias_l[2 * CH + c] + dbias_l[3 * CH + c]);
+    if (threadIdx.x == 0) pr[CH] = (dsc_l[0] + dsc_l[1]) + (dsc_l[2] + dsc_l[3]);
+}
+
+// dbias[c] = sum over blocks of part[b][c] (c < CH), dscale = sum of part[b][CH], blocks in order
+template <int CH>
+__global__ __launch_bounds__(256) void head_bias_finalize_kernel(const float* __restrict__ part, int nblk, float* dbias,
+                                                                 float* dscale)
+{
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c > CH) return;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;             // four interleaved chains, combined in a fixed order
+    int b = 0;
+    for (; b + 4 <= nblk; b += 4) {
+        s0 += part[(size_t)b * (CH + 1) + c];
+        s1 += part[(size_t)(b + 1) * (CH + 1) + c];
+        s2 += part[(size_t)(b + 2) * (CH + 1) + c];
+        s3 += part[(size_t)(b + 3) * (CH + 1) + c];
     }
-    if (threadIdx.x == 0 && dscale) atomicAdd(dscale, dsc_l[0] + dsc_l[1] + dsc_l[2] + dsc_l[3]);
+    for (; b < nblk; ++b) s0 += part[(size_t)b * (CH + 1) + c];
+    const float s = (s0 + s1) + (s2 + s3);
+    if (c < CH) { if (dbias) dbias[c] = s; }
+    else if (dscale) *dscale = s;
 }
 
 // delta[b, h, q] = sum_d dO[b*L+q, h*64+d] * O[b*L+q, h*64+d]   (FA-style backward row statistic)
@@ -616,6 +638,7 @@ int layernorm_bwd_fill(int dtype, const float* dy, const float* x, int rpg, int 
     const VptOut vo{nullptr, 1, 0};
     const int Mf = M / rpg * gstride;
     const dim3 grid((Mf + 3) / 4);
+    const int pi = probe_on() ? probe_start(EBC_PROBE_LN_BWD, 0, 0, 0, 0, Mf, 768, 0, st) : -1;
     switch (dtype) {
         case EBC_F32: hipLaunchKernelGGL((ln_bwd_kernel<float, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean, rstd,
                                          gamma, nullptr, dx_out, (float*)dx_out_t, Mf, vo); break;
@@ -623,8 +646,9 @@ int layernorm_bwd_fill(int dtype, const float* dy, const float* x, int rpg, int 
                                          rstd, gamma, nullptr, dx_out, (_Float16*)dx_out_t, Mf, vo); break;
         case EBC_BF16: hipLaunchKernelGGL((ln_bwd_kernel<__bf16, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean,
                                           rstd, gamma, nullptr, dx_out, (__bf16*)dx_out_t, Mf, vo); break;
-        default: return EBC_E_ARG;
+        default: probe_stop(pi, st); return EBC_E_ARG;
     }
+    probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -769,17 +793,17 @@ int head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_s
 template <int CH>
 static int head_bwd_t(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
                       const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
-                      float* dbias, float* dscale, int P, int HW, int NB, hipStream_t st)
+                      float* dbias, float* dscale, int P, int HW, int NB, void* ws, size_t wsb, hipStream_t st)
 {
-    if (dbias && dscale == dbias + CH) {           // one buffer [CH + 1]: one memset
-        if (hipMemsetAsync(dbias, 0, (CH + 1) * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
-    } else {
-        if (dbias && hipMemsetAsync(dbias, 0, CH * sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
-        if (dscale && hipMemsetAsync(dscale, 0, sizeof(float), st) != hipSuccess) return EBC_E_LAUNCH;
-    }
-    const dim3 grid((P + HEAD_BWD_PPB - 1) / HEAD_BWD_PPB);
+    const int nblk = (P + HEAD_BWD_PPB - 1) / HEAD_BWD_PPB;
+    const bool sums = dbias || dscale;
+    float* part = sums ? reinterpret_cast<float*>(ws) : nullptr;
+    if (sums && (!ws || wsb < head_bwd_ws_bytes(P, CH))) return EBC_E_ARG;
+    const dim3 grid(nblk);
     const size_t lds = ((size_t)NB * CH + 4 * CH + 4) * 4;
-#define HB(TZ, TD) hipLaunchKernelGGL((head_bwd_kernel<TZ, TD, CH>), grid, dim3(256), lds, st, (const TZ*)Z, text, logit_scale, anchors, dlogits, dexp, gscale, (TD*)dZ, dbias, dscale, P, HW, NB)
+    constexpr int LDS_MAX = (16 * CH + 4 * CH + 4) * 4;      // NB <= 16 (embed 1024: 81 KiB)
+#define HB(TZ, TD) if (!ensure_lds<head_bwd_kernel<TZ, TD, CH>>(LDS_MAX, st)) return EBC_E_LAUNCH; \
+    hipLaunchKernelGGL((head_bwd_kernel<TZ, TD, CH>), grid, dim3(256), lds, st, (const TZ*)Z, text, logit_scale, anchors, dlogits, dexp, gscale, (TD*)dZ, part, P, HW, NB)
     // the dZ element type is the caller's buffer type (dtype_dz), independent of Z's
 #define HBZ(TZ)                                                   \
     switch (dtype_dz) {                                           \
@@ -797,18 +821,29 @@ static int head_bwd_t(int dtype_z, int dtype_dz, const void* Z, const float* tex
 #undef HBZ
 #undef HB
     EBC_CHECK_LAUNCH();
+    if (sums) {
+        hipLaunchKernelGGL(head_bias_finalize_kernel<CH>, dim3(CH / 256 + 1), dim3(256), 0, st, part, nblk, dbias, dscale);
+        EBC_CHECK_LAUNCH();
+    }
     return EBC_OK;
+}
+
+size_t head_bwd_ws_bytes(int P, int embed)
+{
+    return P > 0 ? (size_t)((P + HEAD_BWD_PPB - 1) / HEAD_BWD_PPB) * (embed + 1) * sizeof(float) : 0;
 }
 
 int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale, const float* anchors,
              const float* dlogits, const float* dexp, const float* gscale, void* dZ, float* dbias, float* dscale,
-             int P, int HW, int NB, int embed, hipStream_t st)
+             int P, int HW, int NB, int embed, void* ws, size_t wsb, hipStream_t st)
 {
-    if (NB <= 0 || NB > 16) return EBC_E_UNSUPPORTED;
+    if (NB <= 0 || NB > 16 || P <= 0) return EBC_E_UNSUPPORTED;
     if (embed == 512)
-        return head_bwd_t<512>(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW, NB, st);
+        return head_bwd_t<512>(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW, NB,
+                               ws, wsb, st);
     if (embed == 1024)
-        return head_bwd_t<1024>(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW, NB, st);
+        return head_bwd_t<1024>(dtype_z, dtype_dz, Z, text, logit_scale, anchors, dlogits, dexp, gscale, dZ, dbias, dscale, P, HW,
+                                NB, ws, wsb, st);
     return EBC_E_UNSUPPORTED;
 }
 

@@ -71,13 +71,14 @@ SIGNATURES = {
     "ebc_transpose": (_I, [_I, _P, _P, _I, _I, _L, _P]),
     "ebc_vit_workspace_bytes": (_Z, [_I, _I, _I, _I, _I, _I, _I]),
     "ebc_vit_forward": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_long, _I, _I, _P, _Z, _P, _P]),
-    "ebc_vit_backward": (_I, [_P, _I, _I, _I, _I, _P, _Z, _P, _P, ctypes.c_long, _P]),
+    "ebc_vit_backward": (_I, [_P, _I, _I, _I, _I, _P, _Z, _P, _P, ctypes.c_long, _I, _P]),
     "ebc_layernorm_fwd": (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "ebc_layernorm_bwd": (_I, [_I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "ebc_attention_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _P]),
     "ebc_attention_bwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "ebc_head_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
-    "ebc_head_bwd": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ebc_head_bwd": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _Z, _P]),
+    "ebc_head_bwd_workspace_bytes": (_Z, [_I, _I]),
     "ebc_cast_f32": (_I, [_I, _P, _P, _Z, _P]),
     "ebc_tile_gather": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "ebc_tile_assemble": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

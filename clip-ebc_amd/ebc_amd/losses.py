@@ -18,8 +18,9 @@ scalar) in `backward`.  The Sinkhorn internals of the last call (beta [B, g*g], 
 negative = NaN/Inf rollback, and the per-crop err of the last check) are kept on the DMLoss / OTLoss
 module when it is built with `keep_internals=True` (off by default: an extra [B, g*g] write).
 
-Geometry: the fused kernel is built for density grids g = input_size / reduction of 28 and 56 (224 or
-448 crops at reduction 8, 448 at 16); other sizes raise NotImplementedError at construction.
+Geometry: the fused kernel takes any density grid g = input_size / reduction up to 64 x 64 (reduction
+8 / 16 / 32 at any crop size up to 512 at reduction 8; fixtures F1 / F1g pin eight geometries); larger grids raise
+NotImplementedError at construction.
 """
 from __future__ import annotations
 
@@ -272,6 +273,13 @@ class OTLoss(nn.Module):
         assert len(target_points) == B, f"Expected target_points to have length {B}, but got {len(target_points)}"
         assert self.output_size == normed_pred_density.size(2)
         _, _, h, w = pred_density.shape
+        # the kernel forms the Sinkhorn source marginal from pred_density itself: a caller that normalises
+        # differently would get a loss, gradient and ot_obj from two different marginals, so refuse it
+        pd = pred_density.detach().float()
+        own = pd / (pd.sum(dim=(1, 2, 3), keepdim=True) + 1e-8)
+        if not torch.allclose(normed_pred_density.detach().float(), own, rtol=1e-4, atol=1e-7):
+            raise ValueError("OTLoss: normed_pred_density must be pred_density / (pred_density.sum((1, 2, 3)) + 1e-8) "
+                             "(losses/dm_loss.py:106-108), the marginal the fused kernel uses")
         dev = pred_density.device
         pts, offs, order, total = _pack_points(target_points, dev)
         zero_class, lo, hi = _dummy_class(B, h, w, dev)

@@ -153,6 +153,7 @@ class _EncoderCache:
         self.cls = cvt(enc.class_embedding, torch.float32)
         self.ln = [cvt(t, torch.float32) for t in (enc.ln_pre.weight, enc.ln_pre.bias, enc.ln_post.weight, enc.ln_post.bias)]
         self.enc, self.num_vpt, self.layers = enc, num_vpt, layers
+        self.bwd_flags = 0              # EBC_VIT_BWD_FULL_LAYER0 (1): tests compare the trimmed layer-0 backward
         self.keep = keep
         self.structs: Dict[Tuple[int, int], Tuple[EbcVitWeights, Tensor]] = {}
 
@@ -213,7 +214,7 @@ class _VitFn(torch.autograd.Function):
         arr = (_VP * cache.layers)(*([_p(v) for v in dvpt] + [None] * (cache.layers - len(dvpt))))
         w = cache.weights(H // PATCH, W // PATCH)
         rc = L.ebc_vit_backward(ctypes.byref(w), B, H, W, _lib.dtype_code(cache.dtype), _lib.ptr(ctx.ws), ctx.ws.numel(),
-                                _lib.ptr(dfeat.float().contiguous()), arr, ctx.bstride, _lib.stream(dfeat))
+                                _lib.ptr(dfeat.float().contiguous()), arr, ctx.bstride, cache.bwd_flags, _lib.stream(dfeat))
         _lib.check(rc, "ebc_vit_backward")
         ctx.ws = None
         return (None, None, None, None) + tuple(dvpt)
@@ -281,11 +282,13 @@ class _HeadFn(torch.autograd.Function):
         dt = _lib.dtype_code(cdtype)
         E = Wc.shape[0]
         dZ = torch.empty(P, E, device=dev, dtype=cdtype)
-        dbs = torch.empty(E + 1, device=dev, dtype=torch.float32)     # dbias | dscale: one memset in ebc_head_bwd
+        dbs = torch.empty(E + 1, device=dev, dtype=torch.float32)     # dbias | dscale
         dbias, dscale = dbs[:E], dbs[E:]
+        # per-block partial column sums, reduced in block order by a second launch (bit-reproducible)
+        ws = _dec_workspace(dev, L.ebc_head_bwd_workspace_bytes(P, E), slot=3)
         _lib.check(L.ebc_head_bwd(_lib.EBC_F32, dt, _lib.ptr(Z), _lib.ptr(text), _lib.ptr(ls), _lib.ptr(anchors),
                                   _lib.ptr(dl), _lib.ptr(de), None, _lib.ptr(dZ), _lib.ptr(dbias), _lib.ptr(dscale),
-                                  P, HW, NB, E, st), "ebc_head_bwd")
+                                  P, HW, NB, E, _lib.ptr(ws), ws.numel(), st), "ebc_head_bwd")
         if Wt is None:
             Wt = Wc.t().contiguous()                               # [C, E]
         dY = torch.empty(P, C, device=dev, dtype=cdtype)
@@ -298,19 +301,16 @@ class _HeadFn(torch.autograd.Function):
 
 # ----------------------------------------------------------------------------- decoder
 _DEC_WS: Dict[Tuple[torch.device, int], Tensor] = {}
-# EBC_DEC_SIDE=1 runs the weight-gradient GEMMs on a side stream beside the data-gradient chain.  Off by
-# default: measured 2.7 % slower per step on MI355X (r01, interleaved A/B in one process: the two
-# 1-workgroup-per-CU GEMMs contend for CUs and the data-gradient chain is the critical path).
-_USE_SIDE = __import__("os").environ.get("EBC_DEC_SIDE", "0") == "1"
 # EBC_RN50_ENCODER=torch runs clip_resnet50's whole ModifiedResNet on PyTorch-ROCm (MIOpen) instead of the
 # HIP Bottleneck blocks (ebc_amd/resnet.py _ResBlockFn); an A/B switch, not a fallback (both need the GPU)
 _RN50_TORCH_ENCODER = __import__("os").environ.get("EBC_RN50_ENCODER", "") == "torch"
-_SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
 
 
 def _dec_workspace(dev: torch.device, nbytes: int, slot: int = 0) -> Tensor:
-    """Stream-owned scratch of the decoder calls (slot 0: the caller's stream, slot 1: the side stream of the
-    weight-gradient GEMMs, slot 2: the projection's dW GEMM); its first 16 KiB (split-K counters) start zeroed."""
+    """Scratch of the decoder calls on the caller's stream (slot 0: convolutions, slot 1: the weight-gradient
+    GEMMs, slot 2: the projection's dW GEMM); its first 16 KiB (split-K counters) start zeroed and every kernel
+    leaves them zero.  (The weight gradients on a side stream beside the data-gradient chain measured 2.7 %
+    slower per step, r01: the data-gradient chain is the critical path.)"""
     ws = _DEC_WS.get((dev, slot))
     if ws is None or ws.numel() < nbytes:
         ws = torch.zeros(max(nbytes, 1 << 20), device=dev, dtype=torch.uint8)
@@ -337,16 +337,6 @@ def _wgrad_rows(L, dZ: Tensor, Y: Tensor, cdtype: torch.dtype, dev: torch.device
     _lib.check(L.ebc_gemm_wgrad(dt, _lib.ptr(dZT), _lib.ptr(YT), _lib.ptr(dW), E, C, Pp, _lib.ptr(ws), ws.numel(), st),
                "ebc_gemm_wgrad")
     return dW
-
-
-def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
-    """A second HIP stream: the decoder's weight-gradient GEMMs run on it beside the data-gradient chain
-    (nothing waits for dW until the end of the decoder backward)."""
-    s = _SIDE.get(dev)
-    if s is None:
-        s = torch.cuda.Stream(device=dev)
-        _SIDE[dev] = s
-    return s
 
 
 def _bn_group(bn: nn.Module):
@@ -467,9 +457,7 @@ class _DecoderFn(torch.autograd.Function):
         gy = gy.to(cdtype).contiguous()
         nbytes = L.ebc_dec_workspace_bytes(dt, B, H, W, C, N)
         ws = _dec_workspace(dev, nbytes)
-        ws_side = _dec_workspace(dev, nbytes, 1)
-        cur = torch.cuda.current_stream(dev)
-        side = _side_stream(dev) if _USE_SIDE else cur
+        ws_w = _dec_workspace(dev, nbytes, 1)
         f32 = dict(device=dev, dtype=torch.float32)
         grads = []
         dnext = gy                                    # gradient at the current BN output's ReLU
@@ -503,6 +491,8 @@ class _DecoderFn(torch.autograd.Function):
             elif not fused:
                 _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, _lib.ptr(gm.detach()), _lib.ptr(rstd),
                                                  _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef), N, st), "ebc_bn_bwd_finalize")
+            if colsum is None:                            # running statistics (eval mode): dz = gamma * rstd * g
+                coef[1:].zero_()
             dzpad = torch.empty(Q, N, device=dev, dtype=cdtype)
             dzT = torch.empty(N, Qs, device=dev, dtype=cdtype)
             _lib.check(L.ebc_bn_bwd_apply(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
@@ -512,13 +502,8 @@ class _DecoderFn(torch.autograd.Function):
             xT3 = torch.empty(3, C, Qs, device=dev, dtype=cdtype)
             _lib.check(L.ebc_dec_transpose3(dt, _lib.ptr(src), _lib.ptr(xT3), B, H, W, C, st), "ebc_dec_transpose3")
             dw = torch.empty(N, C, 3, 3, **f32)
-            # weight gradient on the side stream, overlapping the data-gradient chain below
-            side.wait_stream(cur)
-            for t_ in (dzT, xT3, dw):
-                t_.record_stream(side)
-            _lib.check(L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws_side),
-                                           ws_side.numel(), B, H, W, C, N, ctypes.c_void_p(side.cuda_stream)),
-                       "ebc_conv3x3_wgrad")
+            _lib.check(L.ebc_conv3x3_wgrad(dt, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws_w),
+                                           ws_w.numel(), B, H, W, C, N, st), "ebc_conv3x3_wgrad")
             del xT3, dzT
             wf = (wf1, wf2)[i]                                                    # [C][3][3][N]
             dx = torch.empty(P, C, device=dev, dtype=cdtype)
@@ -531,7 +516,6 @@ class _DecoderFn(torch.autograd.Function):
         dfeat = torch.empty(B, h, w, C, **f32)
         _lib.check(L.ebc_dec_upsample_bwd(dt, _lib.ptr(dnext), _lib.ptr(dfeat), B, h, w, C, up, st),
                    "ebc_dec_upsample_bwd")
-        cur.wait_stream(side)                          # dW ready before autograd hands it on
         (dw2, dg2, db2), (dw1, dg1, db1) = grads
         ctx.outs = None
         return dfeat, dw1, dg1, db1, dw2, dg2, db2, None, None, None, None
@@ -580,6 +564,7 @@ class CLIP_EBC(nn.Module):
             for p in self.image_encoder.parameters():
                 p.requires_grad = False
             self.num_vpt, self.deep_vpt, self.vpt_drop = num_vpt, deep_vpt, vpt_drop
+            _check_tokens(input_size, input_size, num_vpt)
             val = math.sqrt(6.0 / float(3 * PATCH + WIDTH))
             for idx in range(vit_layers if deep_vpt else 1):
                 setattr(self, f"vpt_{idx}", nn.Parameter(torch.empty(num_vpt, WIDTH).uniform_(-val, val)))
@@ -612,6 +597,7 @@ class CLIP_EBC(nn.Module):
         self._refresh_text()
         self._cache: Optional[_EncoderCache] = None
         self._cache_key = None
+        self.vit_bwd_flags = 0          # ebc_vit_backward flags (include/ebc_hip.h), for parity tests only
 
     # -- weights ---------------------------------------------------------------------------
     def _load_synthetic(self, seed, vit_layers, text_layers, input_size):
@@ -648,6 +634,7 @@ class CLIP_EBC(nn.Module):
         if self._cache is None or self._cache_key != key:
             self._cache = _EncoderCache(self.image_encoder, self.num_vpt, dtype, device)
             self._cache_key = key
+        self._cache.bwd_flags = int(self.vit_bwd_flags)
         return self._cache
 
     # -- forward ---------------------------------------------------------------------------
@@ -704,6 +691,7 @@ class CLIP_EBC(nn.Module):
         cdt = self._compute_dtype(x)
         if self.backbone == "resnet50":
             return self._forward_resnet(x, cdt)
+        _check_tokens(x.shape[-2], x.shape[-1], self.num_vpt)
         feat = self._forward_vpt_nhwc(x)
         up = self.encoder_reduction // self.reduction                      # model.py:195-196 (x2 for reduction 8)
         blk = self.image_decoder[0]
@@ -722,6 +710,20 @@ def _clip_ebc(backbone: str, bins, anchor_points, reduction=None, freeze_text_en
     return CLIP_EBC(backbone, bins, anchor_points, reduction=reduction, freeze_text_encoder=freeze_text_encoder,
                     prompt_type=prompt_type, input_size=input_size, num_vpt=num_vpt, deep_vpt=deep_vpt,
                     vpt_drop=vpt_drop, decoder_cfg=decoder_cfg, **kw)
+
+
+MAX_TOKENS = 256      # attention.hip LP: a (crop, head)'s whole K / V (or Q / dO) stays in LDS
+
+
+def _check_tokens(h: int, w: int, num_vpt: int) -> None:
+    """The ViT sequence (CLS + prompts + (h/16)(w/16) patches) must fit the attention kernels' LDS-resident tiles."""
+    tokens = 1 + num_vpt + (h // PATCH) * (w // PATCH)
+    if tokens > MAX_TOKENS:
+        raise NotImplementedError(
+            f"clip_vit_b_16 on {h}x{w} inputs with {num_vpt} prompts is a sequence of {tokens} tokens; the HIP attention "
+            f"kernels hold a whole (crop, head) sequence in LDS, up to {MAX_TOKENS} tokens (224x224 with 32 prompts: "
+            f"229).  The reference interpolates the positional embedding to any grid (image_encoder.py:183-198); use "
+            f"input_size <= 224 (sliding-window eval: window 224)")
 
 
 def get_model(backbone: str, input_size: int, reduction: int, bins: Optional[List[Tuple[float, float]]] = None,

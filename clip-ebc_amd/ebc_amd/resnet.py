@@ -188,7 +188,7 @@ def _batch_norm_bwd(L, gamma: Tensor, state, dnext: Tensor, mask: Optional[Tenso
                                                 _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),
                                                 _lib.ptr(gamma.detach()), _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef),
                                                 _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_bwd_reduce_finalize")
-        return dg, db, coef
+        return dg, db, _eval_coef(coef, colsum)
     sums = torch.empty(2 * N + (pg is not None), device=dev, dtype=torch.float64)
     _lib.check(L.ebc_bn_bwd_reduce(_lib.dtype_code(z.dtype), _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z),
                                    _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift), _lib.ptr(sums),
@@ -202,7 +202,17 @@ def _batch_norm_bwd(L, gamma: Tensor, state, dnext: Tensor, mask: Optional[Tenso
         sums[2 * N:].copy_(colsum[2 * N:])
         _lib.check(L.ebc_bn_bwd_finalize(_lib.ptr(sums), count, g, _lib.ptr(rstd), None, None, _lib.ptr(coef), N, st),
                    "ebc_bn_bwd_finalize(sync)")
-    return dg, db, coef
+    return dg, db, _eval_coef(coef, colsum)
+
+
+def _eval_coef(coef: Tensor, colsum: Optional[Tensor]) -> Tensor:
+    """BatchNorm normalised with its running statistics (eval mode, or track_running_stats with use of the running
+    estimates: no batch statistics, colsum None) has the input gradient gamma * rstd * g: the batch-mean terms
+    coef[1] = mean(g), coef[2] = mean(g * xhat) of the train-mode backward are zero (torch batch_norm_backward with
+    training=False); d gamma / d beta are the same column sums."""
+    if colsum is None:
+        coef[1:].zero_()
+    return coef
 
 
 def _prep_1x1(L, w: Tensor, cdtype: torch.dtype, st) -> Tuple[Tensor, Tensor]:

@@ -54,7 +54,9 @@ int ebc_version(void);
  * count_mode: EBC_COUNT_DMCOUNT / _MAE / _MSE (DACELoss count_loss="dmcount"/"mae"/"mse"), or
  *   EBC_COUNT_OT_ONLY: OTLoss.forward alone (losses/dm_loss.py:38-79): grad_density = the OT gradient
  *   (weight_count_loss * weight_ot times it), losses[1] = sum of the crops' OT losses, no TV / count terms.
- * size / reduction (the density grid g) must be 28 or 56 (224 or 448 crops at reduction 8, 448 at 16);
+ * size / reduction (the density grid g) may be any integer up to 64 (e.g. 28 / 14 / 7 for 224 crops at reduction
+ * 8 / 16 / 32, 56 / 28 / 14 for 448, 48 for 384 at 8, 64 for 512 at 8; the kernel runs on an LDS grid
+ * G in {8,16,24,28,32,40,48,56,64} >= g whose extra cells are dead); EBC_E_UNSUPPORTED above 64.
  * grid cell k sits at k * reduction + reduction / 2 (dm_loss.py:31).
  * norm_cood: OTLoss norm_cood (dm_loss.py:31-34,51): coordinates mapped to [-1, 1].
  * workspace: ebc_dace_workspace_bytes(...) bytes of device memory.
@@ -154,9 +156,13 @@ size_t ebc_vit_workspace_bytes(int B, int H, int W, int layers, int num_vpt, int
 int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B, int H, int W,
                     const float* const* vpt, long vpt_bstride, int dtype, int training,
                     void* workspace, size_t workspace_bytes, float* feat, ebc_stream_t stream);
-/* dfeat [B, G, 768] f32 -> dvpt[l] ([num_vpt,768] f32, summed over crops; per crop if vpt_bstride). */
+/* dfeat [B, G, 768] f32 -> dvpt[l] ([num_vpt,768] f32, summed over crops; per crop if vpt_bstride).
+ * Layer 0's backward stops at its prompt rows (the frozen embedding below takes no gradient: dQ/dK/dV of the first
+ * query/key block, dH and ln_1' of the prompt rows only); flags & EBC_VIT_BWD_FULL_LAYER0 runs it over every row
+ * instead, which must give bit-identical prompt gradients (a parity hook for tests/test_gpu_model.py). */
+enum { EBC_VIT_BWD_FULL_LAYER0 = 1 };
 int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int dtype, void* workspace,
-                     size_t workspace_bytes, const float* dfeat, float* const* dvpt, long vpt_bstride,
+                     size_t workspace_bytes, const float* dfeat, float* const* dvpt, long vpt_bstride, int flags,
                      ebc_stream_t stream);
 
 /* LayerNorm over 768 channels (models/clip/_clip/blocks.py:8-14, fp32 math, eps 1e-5).
@@ -178,12 +184,17 @@ int ebc_attention_bwd(int dtype, const void* qkv, const void* dout, const void* 
  * Z [P=B*HW, embed] projected features (NHWC rows) -> logits [B,NB,HW], exp [B,1,HW]; text [NB, embed];
  * embed = the CLIP joint width: 512 (ViT-B/16) or 1024 (ResNet-50), NB <= 16.
  * Backward: dZ (element type dtype_dz), d projection bias (column sums), d logit_scale; gscale (device scalar) scales the
- * upstream gradients (NULL = 1). */
+ * upstream gradients (NULL = 1).  d bias / d logit_scale are summed deterministically (per-block partials in `workspace`,
+ * ebc_head_bwd_workspace_bytes(P, embed) bytes, reduced in block order); workspace may be NULL when both are NULL.
+ * Replaces the autograd backward of model.py:198-217 (F.normalize, cosine logits x exp(logit_scale), softmax, expectation)
+ * and the projection bias's column sum. */
 int ebc_head_fwd(int dtype_z, const void* Z, const float* text, const float* logit_scale, const float* anchors,
                  float* logits, float* expo, int P, int HW, int NB, int embed, ebc_stream_t stream);
+size_t ebc_head_bwd_workspace_bytes(int P, int embed);
 int ebc_head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const float* logit_scale,
                  const float* anchors, const float* dlogits, const float* dexp, const float* gscale, void* dZ,
-                 float* dbias, float* dscale, int P, int HW, int NB, int embed, ebc_stream_t stream);
+                 float* dbias, float* dscale, int P, int HW, int NB, int embed, void* workspace, size_t workspace_bytes,
+                 ebc_stream_t stream);
 int ebc_cast_f32(int dtype, const float* in, void* out, size_t n, ebc_stream_t stream);
 
 /* Sliding-window evaluation (utils/eval_utils.py:26-96).  Tiles t = i*cols + j, rows/cols =

@@ -121,14 +121,15 @@ def dace_loss(pred_class: torch.Tensor, pred_density: torch.Tensor, target_densi
     B = pred_density.shape[0]
     pred_count = pred_density.view(B, -1).sum(dim=1)
     normed_pred = pred_density / (pred_count.view(-1, 1, 1, 1) + 1e-8)
-    target_count = torch.tensor([len(p) for p in points], dtype=torch.float32)
+    dev = pred_density.device                     # the oracle also runs on the GPU (AMP calibration, tests only)
+    target_count = torch.tensor([len(p) for p in points], dtype=torch.float32, device=dev)
     normed_target = target_density / (target_count.view(-1, 1, 1, 1) + 1e-8)
     grads = np.zeros((B,) + tuple(pred_density.shape[1:]), np.float32)
     pdn = pred_density.detach().cpu().numpy()
     for b, p in enumerate(points):
         if len(p) > 0:
             grads[b] = ot_crop(p, pdn[b, 0], input_size, reduction, norm_cood=norm_cood)["ot_grad"].reshape(pdn.shape[1:])
-    ot_loss = _OTGrad.apply(pred_density, torch.from_numpy(grads))
+    ot_loss = _OTGrad.apply(pred_density, torch.from_numpy(grads).to(dev))
     tv = ((normed_pred - normed_target).abs().sum(dim=(1, 2, 3)) * target_count).mean()
     cnt = (pred_count - target_count).abs().mean()
     dm = ot_loss * weight_ot + tv * weight_tv + cnt
@@ -163,8 +164,10 @@ def block(x, p, pre, heads=12):
     return x + F.linear(a, p[pre + "mlp.c_proj.weight"], p[pre + "mlp.c_proj.bias"])
 
 
-def vit_vpt_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, layers: int, num_vpt: int = 32) -> torch.Tensor:
-    """CLIP_EBC._forward_vpt (models/clip/model.py:142-189), deep VPT, vpt_drop=0."""
+def vit_vpt_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, layers: int, num_vpt: int = 32,
+                    deep_vpt: bool = True) -> torch.Tensor:
+    """CLIP_EBC._forward_vpt (models/clip/model.py:142-189), vpt_drop=0: deep VPT (vpt_l inserted before block l) or
+    shallow (vpt_0 before block 0, then each block's output prompt rows carried into the next, model.py:174-178)."""
     B, _, H, W = x.shape
     gh, gw = H // 16, W // 16
     e = "image_encoder."
@@ -172,10 +175,13 @@ def vit_vpt_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, layers: int, nu
     cls = p[e + "class_embedding"].view(1, 1, -1).expand(B, 1, 768)
     f = torch.cat([cls, f], dim=1) + p[e + "positional_embedding"]
     f = layer_norm(f, p[e + "ln_pre.weight"], p[e + "ln_pre.bias"])
+    vpt = p["vpt_0"].unsqueeze(0).expand(B, -1, -1)
     for l in range(layers):
-        vpt = p[f"vpt_{l}"].unsqueeze(0).expand(B, -1, -1)
+        if deep_vpt:
+            vpt = p[f"vpt_{l}"].unsqueeze(0).expand(B, -1, -1)
         f = torch.cat([f[:, :1], vpt, f[:, 1:]], dim=1)
         f = block(f, p, f"{e}transformer.resblocks.{l}.")
+        vpt = f[:, 1:1 + num_vpt]
         f = torch.cat([f[:, :1], f[:, 1 + num_vpt:]], dim=1)
     f = layer_norm(f, p[e + "ln_post.weight"], p[e + "ln_post.bias"])
     return f[:, 1:].permute(0, 2, 1).reshape(B, 768, gh, gw)
@@ -220,8 +226,8 @@ def params_from_state(sd: Dict[str, np.ndarray], requires_grad: bool = True) -> 
     return out
 
 
-def forward(p, x, text_features, anchors, layers: int):
-    feats = vit_vpt_forward(p, x, layers)
+def forward(p, x, text_features, anchors, layers: int, deep_vpt: bool = True):
+    feats = vit_vpt_forward(p, x, layers, deep_vpt=deep_vpt)
     return head(p, decoder(p, feats), text_features, anchors) + (feats,)
 
 

@@ -99,12 +99,15 @@ def load_reference():
                                  tokenize=tokenize, eval_utils=eval_utils)
 
 
-def build_ref_model(ref, layers: int, prompt_type: str = "word", anchors=ANCHORS_NWPU, seed: int = 0):
+def build_ref_model(ref, layers: int, prompt_type: str = "word", anchors=ANCHORS_NWPU, seed: int = 0,
+                    deep_vpt: bool = True):
     ref.state["vit_layers"] = layers
     torch.manual_seed(0)
     m = ref.model_mod._clip_ebc("vit_b_16", BINS, anchors, reduction=8, prompt_type=prompt_type,
-                                input_size=224, num_vpt=32, deep_vpt=True, vpt_drop=0.0)
+                                input_size=224, num_vpt=32, deep_vpt=deep_vpt, vpt_drop=0.0)
     sd = syn.full_state(seed, layers=layers)
+    if not deep_vpt:                             # shallow VPT: vpt_0 only (models/clip/model.py:72-75)
+        sd = {k: v for k, v in sd.items() if not (k.startswith("vpt_") and k != "vpt_0")}
     missing, unexpected = m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, strict=False)
     assert not unexpected, unexpected
     assert all(k.endswith("num_batches_tracked") for k in missing) or not missing, missing
@@ -325,9 +328,11 @@ def head_case(ref, seed: int = 5):
                 grad_logit_scale=m.logit_scale.grad.numpy(), text_features=m.text_features.numpy())
 
 
-def e2e_case(ref, layers: int, seed: int = 7, B: int = 2, counts=(37, 5)):
-    """F3/F4: full CLIP-EBC forward + DACE loss + backward on synthetic crops."""
-    m = build_ref_model(ref, layers=layers)
+def e2e_case(ref, layers: int, seed: int = 7, B: int = 2, counts=(37, 5), deep_vpt: bool = True):
+    """F3/F4 (F9: deep_vpt=False, the prompt rows carried from block to block, models/clip/model.py:174-178):
+    full CLIP-EBC forward + DACE loss + backward on synthetic crops."""
+    m = build_ref_model(ref, layers=layers, deep_vpt=deep_vpt)
+    nv = layers if deep_vpt else 1
     img, points, density = syn.synthetic_crops(B, 224, seed=seed, counts=list(counts))
     x = torch.from_numpy(img)
     feats = {}
@@ -340,8 +345,9 @@ def e2e_case(ref, layers: int, seed: int = 7, B: int = 2, counts=(37, 5)):
     loss.backward()
     out = dict(layers=layers, seed=seed, counts=np.asarray(counts), logits=logits.detach().numpy(),
                exp=exp.detach().numpy(), enc_out_sub=feats["ln_post"].numpy()[:, 1::3, ::2],
-               grad_vpt_sub=np.stack([getattr(m, f"vpt_{i}").grad.numpy() for i in range(layers)])[:, :, ::4],
-               grad_vpt_norm=np.asarray([np.linalg.norm(getattr(m, f"vpt_{i}").grad.numpy()) for i in range(layers)]),
+               grad_vpt_sub=np.stack([getattr(m, f"vpt_{i}").grad.numpy() for i in range(nv)])[:, :, ::4],
+               grad_vpt_norm=np.asarray([np.linalg.norm(getattr(m, f"vpt_{i}").grad.numpy()) for i in range(nv)]),
+               deep_vpt=deep_vpt,
                grad_proj_w_sub=m.projection.weight.grad.numpy()[::3, ::3], grad_proj_b=m.projection.bias.grad.numpy(),
                grad_logit_scale=m.logit_scale.grad.numpy(),
                grad_dec_conv1_sub=m.image_decoder[0].conv1.weight.grad.numpy()[::5, ::5],
@@ -544,6 +550,8 @@ def main():
             save("f8_vgg19_ae.npz", **vgg_case(ref))
         if "f1g" in want:
             loss_grids(ref)
+        if "f9" in want:
+            save("f9_shallow_vpt_l12.npz", **e2e_case(ref, layers=12, seed=19, counts=(80, 2), deep_vpt=False))
         return
     prompt_table(ref)
     bpe_merges()
@@ -561,6 +569,7 @@ def main():
     save("f3_e2e_l12.npz", **e2e_case(ref, layers=12))
     save("f7_resnet50.npz", **resnet_case(ref))
     save("f8_vgg19_ae.npz", **vgg_case(ref))
+    save("f9_shallow_vpt_l12.npz", **e2e_case(ref, layers=12, seed=19, counts=(80, 2), deep_vpt=False))
     loss_grids(ref)
 
 

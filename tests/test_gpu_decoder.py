@@ -99,6 +99,37 @@ def test_decoder_eval_uses_running_stats(dtype):
     assert int(blk.bn1.num_batches_tracked) == 0
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_decoder_eval_backward(dtype):
+    """Backward through the decoder with its BatchNorms on the running statistics (model.eval(): frozen-BN
+    fine-tuning): the input gradient is gamma * rstd * g, no batch-mean terms (torch batch_norm_backward with
+    training=False); d gamma / d beta are the column sums.  ADVICE r02."""
+    from ebc_amd.model import _DecoderFn
+    C, B, h, up = 256, 2, 14, 2
+    blk = _block(C)
+    g = torch.Generator().manual_seed(4)
+    feat = torch.randn(B, h, h, C, generator=g)
+    gy = torch.randn(B, h * up, h * up, C, generator=g)
+    params = [p.detach().double().requires_grad_() for p in
+              (blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias)]
+    fr = feat.double().requires_grad_()
+    rm = [blk.bn1.running_mean.double().clone(), blk.bn2.running_mean.double().clone()]
+    rv = [blk.bn1.running_var.double().clone(), blk.bn2.running_var.double().clone()]
+    yr = _ref(fr, *params, up, rm, rv, False)
+    (yr * gy.double()).sum().backward()
+    blk = blk.cuda().eval()
+    fd = feat.cuda().requires_grad_()
+    y = _DecoderFn.apply(fd, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+                         blk.bn2.bias, blk, up, dtype, False)
+    (y.float() * gy.cuda()).sum().backward()
+    assert rel_l2(y.detach().float().cpu().numpy(), yr.detach().numpy()) < TOL[dtype]
+    assert rel_l2(fd.grad.cpu().numpy(), fr.grad.numpy()) < GTOL[dtype]
+    for p, r in zip((blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias),
+                    params):
+        assert rel_l2(p.grad.cpu().numpy(), r.grad.numpy()) < GTOL[dtype], p.shape
+    assert int(blk.bn1.num_batches_tracked) == 0
+
+
 def test_conv3x3_abi_matches_torch():
     """ebc_conv3x3_fwd (implicit GEMM, f16) on a padded NHWC image vs torch conv2d, incl. BN column sums."""
     from ebc_amd import _lib

@@ -129,6 +129,38 @@ def test_bottleneck_eval_uses_running_stats():
     assert int(blk.bn1.num_batches_tracked) == 0
 
 
+def test_bottleneck_eval_backward():
+    """Backward through the Bottleneck decoder on the running statistics (model.eval()): input gradient gamma * rstd
+    * g per BatchNorm, as torch's eval-mode backward."""
+    from ebc_amd.resnet import _BottleneckFn
+    dev = torch.device("cuda")
+    blk = _block(256, 4, dev).eval()
+    with torch.no_grad():
+        for bn in (blk.bn1, blk.bn2, blk.bn3):
+            bn.running_mean.uniform_(-0.1, 0.1)
+            bn.running_var.uniform_(0.5, 2.0)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    feat = torch.randn(2, 7, 7, 256, device=dev, generator=g)
+    params = [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn1.weight, blk.bn1.bias, blk.bn2.weight,
+              blk.bn2.bias, blk.bn3.weight, blk.bn3.bias]
+    fp = feat.clone().requires_grad_(True)
+    y = _BottleneckFn.apply(fp, *params, blk, 2, torch.float32, False)
+    gy = torch.randn(y.shape, device=dev, generator=g)
+    y.backward(gy)
+    mine = [fp.grad] + [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = None
+    ft = feat.permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    x = F.interpolate(ft, scale_factor=2, mode="bilinear")
+    r = F.relu(blk.bn1(blk.conv1(x)))
+    r = F.relu(blk.bn2(blk.conv2(r)))
+    r = F.relu(blk.bn3(blk.conv3(r)) + x)
+    r.backward(gy.permute(0, 3, 1, 2))
+    assert rel_l2(mine[0].permute(0, 3, 1, 2), ft.grad) < 1e-4
+    for p, m in zip(params, mine[1:]):
+        assert rel_l2(m, p.grad) < 1e-4, tuple(p.shape)
+
+
 def test_bench_shape_tile_configs():
     """The config-2 bench products (8 crops of 448: 25088 rows) run the 256x256 tiles."""
     from ebc_amd import _lib

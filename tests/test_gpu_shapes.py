@@ -6,8 +6,8 @@ and the 140-tile eval batch use.  Each test here first asserts WHICH configurati
 (ebc_gemm_tile_config / ebc_conv_tile_config, the same selection the launch makes) and then checks the
 result against torch float64:
   * MLP c_fc + QuickGELU / GELU' and QKV at 16 crops (M = 3664): 256x192 (cfg 3), 192x192 (cfg 4)
-  * the N = 768 products at 16 crops (3-stage 128x96, cfg 13) and at 32 crops (M = 7328: 2-stage
-    128x96, cfg 5), STORE and the f32 residual epilogue
+  * the N = 768 products at 16 crops (128x96 with 4 loader waves: 4-stage ring for K >= 2304, cfg 16, 3-stage
+    for K = 768, cfg 15) and at 32 crops (M = 7328: 2-stage 128x96, cfg 5), STORE and the f32 residual epilogue
   * the 1x1 projection at 16 crops (M = 12544, 128x128, cfg 1) and its dX (128x64, cfg 2)
   * the eval batch (140 tiles, M = 32060): 256x256 (cfg 7) and 256x192 (cfg 3)
   * the decoder BasicBlock at 16 crops (M = 12544: 256x192 implicit GEMM with the BN-statistics,
@@ -71,9 +71,9 @@ def _operands(dt, M, N, K, seed):
 BENCH_PRODUCTS = [
     (3664, 3072, 768, 3, (256, 192)),     # c_fc (+GELU) and GELU' at 16 crops
     (3664, 2304, 768, 4, (192, 192)),     # QKV at 16 crops
-    (3664, 768, 3072, 13, (128, 96)),     # c_proj (+resid) / dX of c_fc at 16 crops
-    (3664, 768, 2304, 13, (128, 96)),     # dX of QKV
-    (3664, 768, 768, 13, (128, 96)),      # out-proj (+resid) / its dX
+    (3664, 768, 3072, 16, (128, 96)),     # c_proj (+resid) / dX of c_fc at 16 crops
+    (3664, 768, 2304, 16, (128, 96)),     # dX of QKV
+    (3664, 768, 768, 15, (128, 96)),      # out-proj (+resid) / its dX
     (7328, 768, 3072, 5, (128, 96)),      # the same at 32 crops (config 4)
     (7328, 768, 768, 5, (128, 96)),
     (7328, 3072, 768, 3, (256, 192)),

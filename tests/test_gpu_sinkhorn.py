@@ -172,3 +172,6 @@ def test_otloss_matches_oracle():
     assert abs(wd - o_wd) <= 1e-4 * abs(o_wd)
     assert abs(float(obj) - o_obj) <= 1e-4 * abs(o_obj) + 1e-4
     assert rel_l2(pdt.grad.cpu().numpy(), o_grad) < 1e-4
+    # a differently normalised marginal is refused (the kernel forms it from pred_density itself)
+    with pytest.raises(ValueError):
+        OTLoss(224, 8, False)(pdt, pdt.detach() / (2 * cnt + 1e-8), [torch.from_numpy(p).to(DEV) for p in pts])

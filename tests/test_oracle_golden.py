@@ -104,14 +104,19 @@ def test_head_oracle_matches_reference():
     assert abs(float(p["logit_scale"].grad) - float(d["grad_logit_scale"])) < 1e-4 * abs(float(d["grad_logit_scale"]))
 
 
-@pytest.mark.parametrize("fixture", ["f4_e2e_l2.npz", "f3_e2e_l12.npz"])
+@pytest.mark.parametrize("fixture", ["f4_e2e_l2.npz", "f3_e2e_l12.npz", "f9_shallow_vpt_l12.npz"])
 def test_e2e_oracle_matches_reference(fixture):
     d = golden(fixture)
     L = int(d["layers"])
+    deep = bool(d["deep_vpt"]) if "deep_vpt" in d else True
+    nv = L if deep else 1
     txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
-    p = ref.params_from_state(syn.full_state(0, layers=L, include_text=False))
+    sd = syn.full_state(0, layers=L, include_text=False)
+    if not deep:                                    # shallow VPT: vpt_0 only
+        sd = {k: v for k, v in sd.items() if not (k.startswith("vpt_") and k != "vpt_0")}
+    p = ref.params_from_state(sd)
     img, pts, dens = syn.synthetic_crops(2, 224, seed=int(d["seed"]), counts=list(d["counts"]))
-    logits, exp, feats = ref.forward(p, torch.from_numpy(img), txt, ANCHORS_NWPU, L)
+    logits, exp, feats = ref.forward(p, torch.from_numpy(img), txt, ANCHORS_NWPU, L, deep_vpt=deep)
     loss, info = ref.dace_loss(logits, exp, torch.from_numpy(dens), pts, BINS)
     loss.backward()
     assert rel_max(logits.detach().numpy(), d["logits"]) < 1e-5
@@ -120,7 +125,7 @@ def test_e2e_oracle_matches_reference(fixture):
     assert rel_max(enc, d["enc_out_sub"]) < 1e-5
     for k in ("loss", "tv_loss", "count_loss", "ce_loss"):
         assert abs(float(info[k]) - float(d["info_" + k])) <= 1e-5 * abs(float(d["info_" + k])), k
-    gv = np.stack([p[f"vpt_{i}"].grad.numpy() for i in range(L)])
+    gv = np.stack([p[f"vpt_{i}"].grad.numpy() for i in range(nv)])
     assert rel_l2(gv[:, :, ::4], d["grad_vpt_sub"]) < 5e-4   # reference fp32 vs fp64: 2e-4
     assert rel_l2(p["projection.weight"].grad.numpy()[::3, ::3], d["grad_proj_w_sub"]) < 1e-4
     assert rel_l2(p["image_decoder.0.conv1.weight"].grad.numpy()[::5, ::5], d["grad_dec_conv1_sub"]) < 5e-3

@@ -9,6 +9,7 @@
 # t:EXPR only the -m gpu tests whose names match EXPR (pytest -k)
 # rbench the clip_resnet50 bench line (configs[1]) -> gpurun_out/TAG_rbench.json
 # rprof  rocprofv3 --kernel-trace --stats of the clip_resnet50 bench, cut to the timed steps
+# pstep  the bench command under rocprofv3: kernel trace + 2 PMC passes, per kernel class (tools/pmc_step.py)
 # Every GPU step has its own time limit and the steps are chained: the first failure ends the session.
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -58,6 +59,26 @@ for what in "$@"; do
       [ -n "$KCALLS" ] && python3 $R/tools/kstats.py "$db" --window --top 0 --calls "$KCALLS" > $O/${TAG}_rcalls.txt
       rm -rf $O/${TAG}_rprof
       head -40 $O/${TAG}_rkstats.txt ;;
+    pstep)
+      # the bench command itself under rocprofv3: a kernel-trace pass and two --pmc passes (each its own run, its own
+      # limit), cut to the timed steps and mapped to bench.py's kernel classes (tools/pmc_step.py)
+      B="$R/bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-trace --classes-out $O/${TAG}_classes.json"
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_ptrace -o run -- \
+        python3 $B > $O/${TAG}_ptrace.log 2>&1) || { tail -30 $O/${TAG}_ptrace.log; exit 1; }
+      db=$(find $O/${TAG}_ptrace -name "*.db" | head -1)
+      python3 $R/tools/kstats.py "$db" --window --per 10 --top 60 > $O/${TAG}_pkstats.txt || { echo "kstats failed"; exit 1; }
+      tail -1 $O/${TAG}_ptrace.log | cut -c1-300
+      i=0
+      for ctrs in "FETCH_SIZE GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES" \
+                  "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctrs -d $O/${TAG}_pmc$i -o run -- \
+          python3 $B > $O/${TAG}_pmc$i.log 2>&1) || { tail -30 $O/${TAG}_pmc$i.log; exit 1; }
+      done
+      python3 $R/tools/pmc_step.py --classes $O/${TAG}_classes.json $O/${TAG}_pmc1 $O/${TAG}_pmc2 \
+        --json $O/${TAG}_pmc_step.json > $O/${TAG}_pmc_step.txt || { echo "pmc_step failed"; exit 1; }
+      rm -rf $O/${TAG}_pmc1 $O/${TAG}_pmc2
+      head -12 $O/${TAG}_pmc_step.txt | cut -c1-400 ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done

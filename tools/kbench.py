@@ -100,8 +100,9 @@ def run(what, args, a):
         dbias, dscale = torch.zeros(CH, device="cuda"), torch.zeros(1, device="cuda")
         p = _lib.ptr
         tf = timeit(lambda: L.ebc_head_fwd(f32, p(Z), p(text), p(ls), p(anchors), p(logits), p(expo), P, HW, NB, CH, st), a.reps)
+        ws = torch.empty(L.ebc_head_bwd_workspace_bytes(P, CH), device="cuda", dtype=torch.uint8)
         tb = timeit(lambda: L.ebc_head_bwd(f32, f16, p(Z), p(text), p(ls), p(anchors), p(dl), p(de), None, p(dZ), p(dbias),
-                                           p(dscale), P, HW, NB, CH, st), a.reps)
+                                           p(dscale), P, HW, NB, CH, p(ws), ws.numel(), st), a.reps)
         print(f"head B={B}: fwd {tf:.2f} us ({P * CH * 4 / tf / 1e3:.0f} GB/s)  bwd {tb:.2f} us ({P * CH * 6 / tb / 1e3:.0f} GB/s)")
     elif what == "conv":
         (B,) = args

@@ -1,0 +1,149 @@
+// GEMM variant lab (experiment harness, not product code): times gemm.hip's kernel templates directly at the
+// ViT-B/16 16-crop shapes (M = 16 x 229), interleaved rounds in one process (cdna_hip_programming.md §5.4 rule
+// 24), outputs of every variant compared bitwise with the first variant of its shape.
+//   build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 -DEBC_GEMM_LAB \
+//          tools/lab/gemm_lab.hip -o tools/lab/bin/gemm_lab
+//   run:   gemm_lab [rounds] [reps]
+#include "../../clip-ebc_amd/csrc/gemm.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+namespace ebc {
+bool probe_on() { return false; }
+int probe_start(int, int, int, int, int, int, int, int, hipStream_t) { return -1; }
+void probe_stop(int, hipStream_t) {}
+}  // namespace ebc
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+__global__ void fill_f16(_Float16* p, size_t n, unsigned seed, float scale)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2654435761u ^ seed;
+        h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+        p[i] = (_Float16)(((h & 0xffff) / 32768.0f - 1.0f) * scale);
+    }
+}
+__global__ void fill_f32(float* p, size_t n, unsigned seed)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2246822519u ^ seed;
+        h ^= h >> 13; h *= 2654435761u; h ^= h >> 16;
+        p[i] = (h & 0xffff) / 32768.0f - 1.0f;
+    }
+}
+
+template <class T> T* dalloc(size_t n) { T* p; CK(hipMalloc(&p, n * sizeof(T))); return p; }
+
+struct Variant { std::string name; std::function<int(const GemmArgs&)> fn; };
+
+using std::string;
+template <class TO, int EPI, int S, int NLW>
+Variant v128x96(const char* nm) {
+    return {nm, [](const GemmArgs& g) { return launch_gemm_k<EF16, TO, EPI, 128, 96, S, 2, 2, 128, 0, false, NLW>(g, 0); }};
+}
+
+int main(int argc, char** argv)
+{
+    const int rounds = argc > 1 ? atoi(argv[1]) : 3, reps = argc > 2 ? atoi(argv[2]) : 30;
+    const int M = 16 * 229;
+    _Float16* A = dalloc<_Float16>((size_t)M * 3072);
+    _Float16* W = dalloc<_Float16>((size_t)3072 * 3072);
+    _Float16* Cfc = dalloc<_Float16>((size_t)M * 3072);
+    _Float16* Afc = dalloc<_Float16>((size_t)M * 3072);
+    float* R = dalloc<float>((size_t)M * 768);
+    float* bias = dalloc<float>(3072);
+    void* C0 = dalloc<float>((size_t)M * 3072);
+    void* C1 = dalloc<float>((size_t)M * 3072);
+    hipLaunchKernelGGL(fill_f16, dim3(1024), dim3(256), 0, 0, A, (size_t)M * 3072, 1u, 1.0f);
+    hipLaunchKernelGGL(fill_f16, dim3(1024), dim3(256), 0, 0, W, (size_t)3072 * 3072, 2u, 0.03f);
+    hipLaunchKernelGGL(fill_f32, dim3(1024), dim3(256), 0, 0, R, (size_t)M * 768, 3u);
+    hipLaunchKernelGGL(fill_f32, dim3(64), dim3(256), 0, 0, bias, (size_t)3072, 4u);
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(fill_f16, dim3(1024), dim3(256), 0, 0, Cfc, (size_t)M * 3072, 5u, 1.0f);
+    CK(hipDeviceSynchronize());
+
+    struct Shape { const char* name; int N, K, epi; bool f32; std::vector<Variant> vars; };
+    std::vector<Shape> shapes;
+    shapes.push_back({"c_proj+res K3072", 768, 3072, EPI_RESID, true,
+                      {v128x96<float, EPI_RESID, 3, 0>("128x96 S3 4w"), v128x96<float, EPI_RESID, 4, 4>("128x96 S4 4w+4L")}});
+    shapes.push_back({"dH2 store K3072", 768, 3072, EPI_STORE, false,
+                      {v128x96<_Float16, EPI_STORE, 3, 0>("128x96 S3 4w"), v128x96<_Float16, EPI_STORE, 4, 4>("128x96 S4 4w+4L")}});
+    shapes.push_back({"out+res K768", 768, 768, EPI_RESID, true,
+                      {v128x96<float, EPI_RESID, 3, 0>("128x96 S3 4w"), v128x96<float, EPI_RESID, 3, 4>("128x96 S3 4w+4L")}});
+
+    // in-step emulation: the c_fc + GELU product (writes 2 x 22.5 MB) runs right before each timed launch; the
+    // K = 3072 products read its output as their A operand, as c_proj does in the step
+    GemmArgs gfc{A, W, Cfc, bias, nullptr, Afc, M, 3072, 768};
+    gfc.kslice = 768;
+    auto cfc = [&]() { return launch_gemm_k<EF16, _Float16, EPI_GELU, 256, 192, 2, 4, 2, 128, 0, false, 0>(gfc, 0); };
+
+    hipEvent_t e0, e1, e2;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
+    for (auto& sh : shapes) {
+        GemmArgs g{sh.K == 3072 ? (void*)Cfc : (void*)A, W, C0, bias, sh.epi == EPI_RESID ? R : nullptr, nullptr, M, sh.N, sh.K};
+        g.kslice = sh.K;
+        const size_t outb = (size_t)M * sh.N * (sh.f32 ? 4 : 2);
+        // correctness: every variant bitwise equal to the first
+        std::vector<char> ref(outb), got(outb);
+        for (size_t v = 0; v < sh.vars.size(); ++v) {
+            g.C = v == 0 ? C0 : C1;
+            CK(hipMemset(g.C, 0, outb));
+            if (sh.vars[v].fn(g)) { printf("%s %s: launch error\n", sh.name, sh.vars[v].name.c_str()); return 1; }
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(v == 0 ? ref.data() : got.data(), g.C, outb, hipMemcpyDeviceToHost));
+            if (v > 0) {
+                size_t bad = 0;
+                for (size_t i = 0; i < outb; ++i) bad += ref[i] != got[i];
+                printf("%-18s %-18s bitwise vs %s: %s (%zu bytes differ)\n", sh.name, sh.vars[v].name.c_str(),
+                       sh.vars[0].name.c_str(), bad ? "DIFFERENT" : "identical", bad);
+            }
+        }
+        g.C = C1;
+        const double tf = 2.0 * M * sh.N * sh.K / 1e12;
+        for (int r = 0; r < rounds; ++r) {
+            for (auto& v : sh.vars) {
+                // alone: back-to-back launches
+                for (int w = 0; w < 3; ++w) v.fn(g);
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < reps; ++i) v.fn(g);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float alone = 0;
+                CK(hipEventElapsedTime(&alone, e0, e1));
+                alone /= reps;
+                // after the c_fc product
+                float inst = 0;
+                for (int i = 0; i < reps; ++i) {
+                    cfc();
+                    CK(hipEventRecord(e0));
+                    v.fn(g);
+                    CK(hipEventRecord(e1));
+                    CK(hipEventSynchronize(e1));
+                    float t;
+                    CK(hipEventElapsedTime(&t, e0, e1));
+                    inst += t;
+                }
+                inst /= reps;
+                printf("%s r%d %-18s %-18s alone %7.2f us (%6.1f TF/s)   after c_fc %7.2f us (%6.1f TF/s)\n", EBC_STORE_NT ? "nt" : "plain", r, sh.name,
+                       v.name.c_str(), alone * 1e3, tf / (alone * 1e-3), inst * 1e3, tf / (inst * 1e-3));
+            }
+        }
+    }
+    for (int r = 0; r < rounds; ++r) {
+        for (int w = 0; w < 3; ++w) cfc();
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < reps; ++i) cfc();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        printf("%s r%d c_fc+gelu 256x192 alone %7.2f us\n", EBC_STORE_NT ? "nt" : "plain", r, t / reps * 1e3);
+    }
+    return 0;
+}
