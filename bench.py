@@ -582,7 +582,9 @@ def main():
                                "frac": round(top["tflops"] / peak, 4), "traffic": committed_traffic(top["kernel"]),
                                "kernel": top["kernel"], "avg_us": top["avg_us"], "flop_per_launch": top["flop_per_launch"],
                                "per_step_us": top["per_step_us"],
-                               "method": "in-step HIP events on the launch stream (ebc_probe), 3 instrumented steps"}
+                               "method": "in-step kernel durations from the runtime's kernel trace (torch.profiler / "
+                                         "roctracer, the rocprofv3 --kernel-trace source) over 3 steps; kernel classes "
+                                         "(shape, epilogue) from 3 ebc_probe steps, matched in launch order"}
             out["kernels"] = kernels[:12]
             out["sinkhorn"] = sink
         if world == 1 and not args.no_cpu_baseline:

@@ -121,10 +121,34 @@ __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* bas
     return load8<E>(base + attn_off<E>(row, col));
 }
 
+// Weight touch (kernels.h TouchList): once its operands are staged (no later global load in the wave to wait behind
+// them), every wave of the launch reads one dword of each of its share of the listed buffers' 128-B lines (64 lines
+// per instruction), so the weights of the GEMMs that follow are on-die when they start.  The loads are inline asm
+// into one register that is kept live and waited for only at the wave's end: nothing stalls on them mid-kernel (an
+// LDS-DMA form made the compiler drain them before the first LDS read that might alias).  Measured on the c_proj
+// product (tools/lab/gemm_lab.hip "mlp-seq"): 37.5 us with its weight in HBM, 28.4 us read onto the die beforehand;
+// a separate touch kernel on a side stream instead cost more in the kernels it ran beside (r03 same-box A/B).
+template <int NW>
+__device__ __forceinline__ void touch_issue(const TouchList& t, unsigned& sink)
+{
+    const int lane = threadIdx.x & 63, nw = NW;
+    const size_t gw = (size_t)blockIdx.x * nw + (threadIdx.x >> 6), GW = (size_t)gridDim.x * nw;
+    for (int b = 0; b < t.n; ++b) {
+        const char* base = reinterpret_cast<const char*>(t.ptr[b]);
+        const size_t lines = t.bytes[b] >> 7;
+        for (size_t c = gw * 64 + lane; c < lines; c += GW * 64) {
+            const char* a = base + (c << 7);
+            asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(a) : "memory");
+        }
+    }
+}
+__device__ __forceinline__ void touch_wait(unsigned sink) { asm volatile("s_waitcnt vmcnt(0)" :: "v"(sink) : "memory"); }
+
 // ------------------------------------------------------------------------------ forward
 template <class E, int NWV, int LFIX>
 __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T* __restrict__ qkv, typename E::T* __restrict__ out,
-                                                       float* __restrict__ lse, int B, int L_, int H, float scale)
+                                                       float* __restrict__ lse, int B, int L_, int H, float scale,
+                                                       TouchList touch)
 {
     const int L = LFIX > 0 ? LFIX : L_;                        // compile-time sequence: tile loops and masks fold
     using T = typename E::T;
@@ -154,6 +178,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     __syncthreads();
 
     if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
+    unsigned tsink = 0;
+    if (touch.n) touch_issue<NWV>(touch, tsink);
     // key tiles past L are skipped; only the ragged last tile is masked; the softmax scale is folded
     // into the exp2 argument: p = 2^(s*c - max*c), c = scale*log2(e)
     const int nkt = (L + 15) >> 4;
@@ -221,6 +247,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
         }
     }
     if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx * scale + logf(sum);   // natural-log units of the scaled scores
+    if (touch.n) touch_wait(tsink);
 }
 
 // ------------------------------------------------------------------------------ backward dQ
@@ -228,7 +255,7 @@ template <class E, int NWV, int LFIX>
 __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                  const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                  float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                 int L_, int H, float scale, int nblk = 0)
+                                                 int L_, int H, float scale, int nblk = 0, const TouchList* touch = nullptr)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -281,6 +308,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* _
     __syncthreads();
 
     if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
+    unsigned tsink = 0;
+    if (touch && touch->n) touch_issue<NWV>(*touch, tsink);
     const int nkt = (L + 15) >> 4;
     const bool ragged = (L & 15) != 0;
     const float c2 = scale * LOG2E, lq2 = lq * LOG2E;          // p = 2^(s*c - lse*log2 e)
@@ -325,6 +354,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* _
             for (int dt = 0; dt < HD / 16; ++dt) row[16 * dt + fr] = E::from(dq_acc[dt][i] * scale);
         }
     }
+    if (touch && touch->n) touch_wait(tsink);
 }
 
 template <class E, int NWV, int LFIX>
@@ -360,7 +390,7 @@ template <class E, int NWV, int LFIX>
 __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                   const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                   const float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                  int L_, int H, float scale, int nblk = 0)
+                                                  int L_, int H, float scale, int nblk = 0, const TouchList* touch = nullptr)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -401,6 +431,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
     __syncthreads();
 
     if (k0 >= L) return;                                       // no live key in this wave (no barrier follows)
+    unsigned tsink = 0;
+    if (touch && touch->n) touch_issue<NWV>(*touch, tsink);
     const int nqt = (L + 15) >> 4;                             // query tiles past L: lse = +inf, p = 0
     const float c2 = scale * LOG2E;
     f32x4 dk[HD / 16], dv[HD / 16];
@@ -448,6 +480,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
             }
         }
     }
+    if (touch && touch->n) touch_wait(tsink);
 }
 
 template <class E, int NWV, int LFIX>
@@ -465,10 +498,12 @@ template <class E, int NWV, int LFIX>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_fused_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                              const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                              typename E::T* __restrict__ dqkv, int ndq, int B, int L_, int H,
-                                                             float scale, int nblk)
+                                                             float scale, int nblk, TouchList touch)
 {
-    if ((int)blockIdx.x < ndq) attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk);
-    else attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x - ndq, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk);
+    if ((int)blockIdx.x < ndq)
+        attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
+    else
+        attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x - ndq, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
 }
 
 int attn_waves(int L) {
@@ -480,24 +515,28 @@ int attn_waves(int L) {
 // the CLIP ViT-B/16 + 32-prompt sequence (1 + 32 + 196 tokens) gets kernels compiled for it
 constexpr int L_VPT32 = 229;
 
-template <class E, int NW, int LFIX> int attn_fwd_nw(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+template <class E, int NW, int LFIX> int attn_fwd_nw(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,
+                                                     const TouchList* touch = nullptr)
 {
     using C = AttnCfg<E>;
+    const TouchList t = touch ? *touch : TouchList{};
     const size_t lds = 2 * C::TILE_BYTES;
     if (!ensure_lds<attn_fwd_kernel<E, NW, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
     const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
     const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_FWD, 0, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_fwd_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
-                       (typename E::T*)out, lse, B, L, H, 0.125f);
+                       (typename E::T*)out, lse, B, L, H, 0.125f, t);
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
-template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,
+                                  const TouchList* touch)
 {
     if (attn_waves(L) == 16)
-        return L == L_VPT32 ? attn_fwd_nw<E, 16, L_VPT32>(qkv, out, lse, B, L, H, st) : attn_fwd_nw<E, 16, 0>(qkv, out, lse, B, L, H, st);
-    return attn_fwd_nw<E, 8, 0>(qkv, out, lse, B, L, H, st);
+        return L == L_VPT32 ? attn_fwd_nw<E, 16, L_VPT32>(qkv, out, lse, B, L, H, st, touch)
+                            : attn_fwd_nw<E, 16, 0>(qkv, out, lse, B, L, H, st, touch);
+    return attn_fwd_nw<E, 8, 0>(qkv, out, lse, B, L, H, st, touch);
 }
 
 template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void* dout, const void* out, const float* lse,
@@ -522,9 +561,11 @@ template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void
     return EBC_OK;
 }
 template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, const void* dout, const void* out, const float* lse,
-                                                           void* dqkv, int B, int L, int H, hipStream_t st, int rows = 0)
+                                                           void* dqkv, int B, int L, int H, hipStream_t st, int rows = 0,
+                                                           const TouchList* touch = nullptr)
 {
     using C = AttnCfg<E>;
+    const TouchList t = touch ? *touch : TouchList{};
     const size_t lds = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
     if (!ensure_lds<attn_bwd_fused_kernel<E, NW, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
     // rows > 0: dQ of queries and dK / dV of keys < rows are wanted (the rest of dqkv is left unwritten)
@@ -534,19 +575,19 @@ template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, cons
     const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 1, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_bwd_fused_kernel<E, NW, LFIX>), dim3(2 * ndq), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, (const typename E::T*)out, lse, (typename E::T*)dqkv, ndq, B, L, H, 0.125f,
-                       nblk);
+                       nblk, t);
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
 
 template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
-                                  void* dqkv, int B, int L, int H, hipStream_t st, int rows)
+                                  void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
 {
-    // 16-bit: dQ and dK/dV roles in one grid; f32 (parity mode): the two kernels one after the other
+    // 16-bit: dQ and dK/dV roles in one grid; f32 (parity mode): the two kernels one after the other (no weight touch)
     if (E::BYTES == 2) {
-        return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows)
-                            : attn_bwd_fused_nw<E, 8, 0>(qkv, dout, out, lse, dqkv, B, L, H, st, rows);
+        return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch)
+                            : attn_bwd_fused_nw<E, 8, 0>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch);
     }
     if (attn_waves(L) == 16)
         return L == L_VPT32 ? attn_bwd_nw<E, 16, L_VPT32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st)
@@ -557,24 +598,25 @@ template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void*
 }  // namespace
 
 namespace ebc {
-int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,
+                  const TouchList* touch)
 {
     if (L <= 0 || L > LP || B <= 0 || H <= 0) return EBC_E_UNSUPPORTED;
     switch (dtype) {
-        case EBC_F32: return attn_fwd_t<EF32>(qkv, out, lse, B, L, H, st);
-        case EBC_F16: return attn_fwd_t<EF16>(qkv, out, lse, B, L, H, st);
-        case EBC_BF16: return attn_fwd_t<EBF16>(qkv, out, lse, B, L, H, st);
+        case EBC_F32: return attn_fwd_t<EF32>(qkv, out, lse, B, L, H, st, nullptr);
+        case EBC_F16: return attn_fwd_t<EF16>(qkv, out, lse, B, L, H, st, touch);
+        case EBC_BF16: return attn_fwd_t<EBF16>(qkv, out, lse, B, L, H, st, touch);
     }
     return EBC_E_ARG;
 }
 int attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
-                  void* dqkv, int B, int L, int H, hipStream_t st, int rows)
+                  void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
 {
     if (L <= 0 || L > LP || B <= 0 || H <= 0 || rows < 0) return EBC_E_UNSUPPORTED;
     switch (dtype) {
-        case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows);
-        case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows);
-        case EBC_BF16: return attn_bwd_t<EBF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows);
+        case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows, nullptr);
+        case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows, touch);
+        case EBC_BF16: return attn_bwd_t<EBF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows, touch);
     }
     return EBC_E_ARG;
 }

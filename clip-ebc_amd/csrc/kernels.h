@@ -4,6 +4,15 @@
 #include <stddef.h>
 
 namespace ebc {
+// Device buffers an attention launch reads onto the die while it computes (the next GEMMs' frozen weights, last read
+// a step ago): every wave of the launch reads a dword of its share of their 128-B lines (attention.hip touch_issue),
+// so the later GEMMs' L2 misses are served by the Infinity Cache instead of HBM.
+struct TouchList {
+    const void* ptr[8];
+    size_t bytes[8];
+    int n;
+    void add(const void* p, size_t b) { if (p && b >= 128 && n < 8) { ptr[n] = p; bytes[n] = b; ++n; } }
+};
 // in-step launch timing (probe.hip): probe_start returns a record index (or -1 when not armed)
 bool probe_on();
 int probe_start(int kind, int epi, int bm, int bn, int mode, int m, int n, int k, hipStream_t st);
@@ -61,12 +70,14 @@ int head_bwd(int dtype_z, int dtype_dz, const void* Z, const float* text, const 
              int P, int HW, int NB, int embed, void* ws, size_t wsb, hipStream_t st);
 int attn_delta(int dtype, const void* dO, const void* O, float* delta, int B, int L, int H, hipStream_t st);
 int cast_f32(int dtype, const float* in, void* out, size_t n, hipStream_t st);
-int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st);
+int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,
+                  const TouchList* touch = nullptr);
 // delta (FA2 D_i = rowsum(dO * O)) is computed by the dQ kernel and written to `delta` [B,H,L]
 // rows > 0: only dQ of the queries and dK / dV of the keys below `rows` are needed (16-bit: the launch covers
 // the first ceil(rows / 128) blocks of each (crop, head); the other dqkv rows are left unwritten)
 int attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
-                  void* dqkv, int B, int L, int H, hipStream_t st, int rows = 0);
+                  void* dqkv, int B, int L, int H, hipStream_t st, int rows = 0,
+                  const TouchList* touch = nullptr);
 // LayerNorm backward of the mapped rows into a dense output: dx_out[r] = dx_in[map r] + LN'(dy[r]) with x, mean,
 // rstd at map r (layer 0's prompt rows: r = (b, j) -> b * gstride + goff + j)
 int layernorm_bwd_rows(int dtype, const void* dy, const float* x, int rpg, int gstride, int goff, const float* mean,

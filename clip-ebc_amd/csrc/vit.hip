@@ -19,6 +19,10 @@
 #include "ebc_common.h"
 #include "kernels.h"
 
+#ifndef EBC_WEIGHT_TOUCH
+#define EBC_WEIGHT_TOUCH 1     // 0: attention launches touch no weights (A/B builds, tools/build_var.sh)
+#endif
+
 namespace {
 
 constexpr int WIDTH = 768, HEADS = 12, MLP = 3072, QKVW = 3 * WIDTH;
@@ -151,6 +155,19 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
                               vpt_bstride, lay.X[0], B, L, G, NV, WIDTH, st));
     // one block on crops [b0, b0 + nb) (rows r0 = b0 * L of every [B][L][*] buffer) on stream sx
     const size_t es = dtype == EBC_F32 ? 4 : 2;
+    // The frozen weights were last read a step ago (HBM).  Block l's attention reads onto the die (Infinity Cache) the
+    // weights of the GEMMs after it -- its out-proj, c_fc and c_proj, and block l+1's QKV -- while it computes
+    // (attention.hip touch_issue): those GEMMs then start with their B operand on-die.  16-bit path only.
+    auto touch_fwd = [&](int l) {
+        ebc::TouchList t{};
+        if (!EBC_WEIGHT_TOUCH) return t;
+        const EbcVitLayer& p = w->layer[l];
+        t.add(p.w_out, (size_t)WIDTH * WIDTH * es);
+        t.add(p.w_fc, (size_t)MLP * WIDTH * es);
+        t.add(p.w_proj, (size_t)WIDTH * MLP * es);
+        if (l + 1 < layers) t.add(w->layer[l + 1].w_qkv, (size_t)QKVW * WIDTH * es);
+        return t;
+    };
     auto block = [&](int l, int b0, int nb, hipStream_t sx) -> int {
         const EbcVitLayer& p = w->layer[l];
         const LayerSave& s = lay.s[training ? l : 0];
@@ -176,7 +193,8 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
         else
             EBC_TRY(ebc::layernorm_fwd(dtype, X, 0, 0, 0, p.ln1_g, p.ln1_b, Hn, nullptr, s.m1 + r0, s.r1 + r0, m, WIDTH, sx));
         EBC_TRY(gemm(EBC_EPI_STORE, 0, Hn, p.w_qkv, QKV, p.b_qkv, nullptr, nullptr, QKVW, WIDTH));
-        EBC_TRY(ebc::attention_fwd(dtype, QKV, O, lse, nb, L, HEADS, sx));
+        const ebc::TouchList tl = touch_fwd(l);
+        EBC_TRY(ebc::attention_fwd(dtype, QKV, O, lse, nb, L, HEADS, sx, &tl));
         EBC_TRY(gemm(EBC_EPI_RESID, 1, O, p.w_out, X1, p.b_out, X, nullptr, WIDTH, WIDTH));
         // x = x + c_proj(QuickGELU(c_fc(ln_2(x))))
         EBC_TRY(ebc::layernorm_fwd(dtype, X1, 0, 0, 0, p.ln2_g, p.ln2_b, Hn, nullptr, s.m2 + r0, s.r2 + r0, m, WIDTH, sx));
@@ -212,12 +230,28 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
     auto gemm = [&](int epi, const void* A, const void* Bm, void* C, void* aux, int m, int n, int k) {
         return ebc::gemm_nt(dtype, epi, 0, A, Bm, C, nullptr, nullptr, aux, m, n, k, st, lay.gws, lay.gws_bytes);
     };
+    // block l's attention backward reads onto the die the transposed weights of the dX products after it: its QKV dX
+    // and block l-1's c_proj / c_fc / out-proj ones (see ebc_vit_forward)
+    const size_t es = dtype == EBC_F32 ? 4 : 2;
+    auto touch_bwd = [&](int l) {
+        ebc::TouchList t{};
+        if (!EBC_WEIGHT_TOUCH) return t;
+        t.add(w->layer[l].wt_qkv, (size_t)WIDTH * QKVW * es);
+        if (l > 0) {
+            const EbcVitLayer& q = w->layer[l - 1];
+            t.add(q.wt_proj, (size_t)MLP * WIDTH * es);
+            t.add(q.wt_fc, (size_t)WIDTH * MLP * es);
+            t.add(q.wt_out, (size_t)WIDTH * WIDTH * es);
+        }
+        return t;
+    };
     // (the CLS / prompt rows of dX, dXt are written as zeros by the same launch: no memsets)
     EBC_TRY(ebc::layernorm_bwd_fill(dtype, dfeat, lay.X[layers], G, L, 1 + NV, lay.mpost, lay.rpost, w->ln_post_g, dX,
                                     lay.dXt, B * G, WIDTH, st));
     for (int l = layers - 1; l >= 0; --l) {
         const EbcVitLayer& p = w->layer[l];
         LayerSave& s = lay.s[l];
+        const ebc::TouchList tl = touch_bwd(l);
         // MLP half: dA = (dX . W_proj) * QuickGELU'(A);  dH2 = dA . W_fc;  dX1 = dX + LN2'(dH2)
         EBC_TRY(gemm(EBC_EPI_GELU_BWD, lay.dXt, p.wt_proj, lay.dA, s.A, M, MLP, WIDTH));
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dA, p.wt_fc, lay.dH, nullptr, M, WIDTH, MLP));
@@ -230,7 +264,7 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
             // rows' input gradient is wanted -- dQ / dK / dV of the first query and key block (rows 1..NV), dH on
             // the B*NV prompt rows (row-mapped A operand), ln_1's backward of those rows straight into the prompt
             // rows (same values as the full backward's rows: every kept element is summed in the same order)
-            EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st, 1 + NV));
+            EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st, 1 + NV, &tl));
             EBC_TRY(ebc::gemm_nt(dtype, EBC_EPI_STORE, 0, lay.dQKV, p.wt_qkv, lay.dH, nullptr, nullptr, nullptr, B * NV,
                                  WIDTH, QKVW, st, lay.gws, lay.gws_bytes, NV, L, 1));
             float* rows = per_batch ? dvpt[0] : lay.vpt_rows;
@@ -238,7 +272,7 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
                                             WIDTH, st));
             break;
         }
-        EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st));
+        EBC_TRY(ebc::attention_bwd(dtype, s.QKV, lay.dO, s.O, s.lse, lay.delta, lay.dQKV, B, L, HEADS, st, 0, &tl));
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dQKV, p.wt_qkv, lay.dH, nullptr, M, WIDTH, QKVW));
         // prompt rows (deep VPT; shallow VPT: layer 0 only): ln_1's backward routes their gradient to the
         // per-crop rows (straight into dvpt_l when it is per crop) and zeroes them in the token stream,

@@ -102,7 +102,8 @@ int main(int argc, char** argv)
         {"256x192 s2 last-arriver", tile(T256x192{}, 2, false)},
         {"256x192 s2 partials+reduce", tile(T256x192{}, 2, true)},
         {"256x192 s4 partials+reduce", tile(T256x192{}, 4, true)},
-        {"256x256 s3 partials+reduce", tile(T256x256{}, 3, true)},
+        {"256x256 s2 partials+reduce", tile(T256x256{}, 2, true)},
+        {"256x192 s7 partials+reduce", tile(T256x192{}, 7, true)},
         {"128x192 s1", tile(T128x192{}, 1, false)},
         {"128x192 s2 partials+reduce", tile(T128x192{}, 2, true)},
     };

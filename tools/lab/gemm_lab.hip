@@ -38,6 +38,17 @@ __global__ void fill_f32(float* p, size_t n, unsigned seed)
     }
 }
 
+// read a buffer once (16 B a lane) so its lines are on-die (Infinity Cache) when the next kernel needs them
+__global__ __launch_bounds__(256) void touch_kernel(const uint4* __restrict__ p, size_t n16, unsigned* sink)
+{
+    unsigned acc = 0;
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+        const uint4 v = p[i];
+        acc ^= v.x ^ v.w;
+    }
+    if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
 template <class T> T* dalloc(size_t n) { T* p; CK(hipMalloc(&p, n * sizeof(T))); return p; }
 
 struct Variant { std::string name; std::function<int(const GemmArgs&)> fn; };
@@ -134,6 +145,75 @@ int main(int argc, char** argv)
                        v.name.c_str(), alone * 1e3, tf / (alone * 1e-3), inst * 1e3, tf / (inst * 1e-3));
             }
         }
+    }
+    // ---- the MLP pair as the step runs it: 12 layers, each with its own weights, c_fc output and residual, so
+    // c_proj's operands are as cold as in the step; per variant of c_proj's tile order (group_m) and ring
+    {
+        const int NL = 12;
+        std::vector<_Float16*> Wfc(NL), Wpr(NL), G(NL), Ax(NL);
+        std::vector<float*> X1(NL), Xn(NL);
+        for (int l = 0; l < NL; ++l) {
+            Wfc[l] = dalloc<_Float16>((size_t)3072 * 768); Wpr[l] = dalloc<_Float16>((size_t)768 * 3072);
+            G[l] = dalloc<_Float16>((size_t)M * 3072); Ax[l] = dalloc<_Float16>((size_t)M * 3072);
+            X1[l] = dalloc<float>((size_t)M * 768); Xn[l] = dalloc<float>((size_t)M * 768);
+            hipLaunchKernelGGL(fill_f16, dim3(1024), dim3(256), 0, 0, Wfc[l], (size_t)3072 * 768, 100u + l, 0.03f);
+            hipLaunchKernelGGL(fill_f16, dim3(1024), dim3(256), 0, 0, Wpr[l], (size_t)3072 * 768, 200u + l, 0.02f);
+            hipLaunchKernelGGL(fill_f32, dim3(1024), dim3(256), 0, 0, X1[l], (size_t)M * 768, 300u + l);
+        }
+        CK(hipDeviceSynchronize());
+        struct PV { const char* name; int gm; std::function<int(const GemmArgs&)> fn; int share = 0; int pf = 0; };
+        hipStream_t side;
+        CK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        hipEvent_t fork;
+        CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        unsigned* sink;
+        CK(hipMalloc(&sink, 64));
+        // share: 1 = every layer uses layer 0's c_proj weight (warm W), 2 = layer 0's residual (warm X1), 4 = both
+        auto S4L = [](const GemmArgs& g) { return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 4, 2, 2, 128, 0, false, 4>(g, 0); };
+        std::vector<PV> pv = {
+            {"S4+4L warm W", 0, S4L, 1},
+            {"S4+4L warm X1", 0, S4L, 2},
+            {"S4+4L warm W+X1", 0, S4L, 3},
+            {"S4+4L touch W (side, 64 WG)", 0, S4L, 0, 64},
+            {"S4+4L touch W (side, 256 WG)", 0, S4L, 0, 256},
+            {"S4+4L rowmajor", 0, [](const GemmArgs& g) { return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 4, 2, 2, 128, 0, false, 4>(g, 0); }},
+            {"S4+4L group_m 3", 3, [](const GemmArgs& g) { return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 4, 2, 2, 128, 0, false, 4>(g, 0); }},
+            {"S4+4L group_m 5", 5, [](const GemmArgs& g) { return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 4, 2, 2, 128, 0, false, 4>(g, 0); }},
+            {"S4+4L group_m 8", 8, [](const GemmArgs& g) { return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 4, 2, 2, 128, 0, false, 4>(g, 0); }},
+            {"S3 4w rowmajor", 0, [](const GemmArgs& g) { return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 3, 2, 2, 128, 0, false, 0>(g, 0); }},
+        };
+        std::vector<hipEvent_t> ev(2 * NL);
+        for (auto& evx : ev) CK(hipEventCreate(&evx));
+        for (int r = 0; r < rounds; ++r)
+            for (auto& v : pv) {
+                float tot = 0, fc = 0;
+                for (int it = 0; it < 3; ++it)
+                    for (int l = 0; l < NL; ++l) {
+                        GemmArgs a{A, Wfc[l], G[l], bias, nullptr, Ax[l], M, 3072, 768};
+                        a.kslice = 768;
+                        GemmArgs b{G[l], Wpr[(v.share & 1) ? 0 : l], Xn[l], bias, X1[(v.share & 2) ? 0 : l], nullptr, M, 768, 3072};
+                        b.kslice = 3072;
+                        b.group_m = v.gm;
+                        if (v.pf) {                     // prefetch c_proj's weight on a side stream beside c_fc
+                            CK(hipEventRecord(fork, 0));
+                            CK(hipStreamWaitEvent(side, fork, 0));
+                            hipLaunchKernelGGL(touch_kernel, dim3(v.pf), dim3(256), 0, side,
+                                               reinterpret_cast<const uint4*>(Wpr[l]), (size_t)768 * 3072 * 2 / 16, sink);
+                        }
+                        CK(hipEventRecord(ev[2 * l]));
+                        launch_gemm_k<EF16, _Float16, EPI_GELU, 256, 192, 2, 4, 2, 128, 0, false, 0>(a, 0);
+                        CK(hipEventRecord(ev[2 * l + 1]));
+                        v.fn(b);
+                        CK(hipEventRecord(e2));
+                        CK(hipEventSynchronize(e2));
+                        float t1 = 0, t2 = 0;
+                        CK(hipEventElapsedTime(&t1, ev[2 * l], ev[2 * l + 1]));
+                        CK(hipEventElapsedTime(&t2, ev[2 * l + 1], e2));
+                        if (it > 0) { fc += t1; tot += t2; }
+                    }
+                printf("%s r%d mlp-seq c_proj %-16s %7.2f us   (c_fc %7.2f us)\n", EBC_STORE_NT ? "nt" : "plain", r, v.name,
+                       tot / (2 * NL) * 1e3, fc / (2 * NL) * 1e3);
+            }
     }
     for (int r = 0; r < rounds; ++r) {
         for (int w = 0; w < 3; ++w) cfc();
