@@ -75,6 +75,8 @@ def parse(argv=None):
     ap.add_argument("--augment", action="store_true",
                     help="SURVEY §8f row f2 instead: the reference's training augmentation on device (RandomResizedCrop + "
                          "flip + RandomApply(jitter, blur, noise) + normalise + dot maps), 16 images x 2 crops per step")
+    ap.add_argument("--noise-rng", default="device", choices=["device", "reference"],
+                    help="--augment: salt-and-pepper uniforms from the device hash or the reference's host rand_like")
     a = ap.parse_args(argv)
     rn = a.model == "clip_resnet50"
     if a.crops_per_gpu is None:
@@ -394,7 +396,7 @@ def run_augment(args, rank, device):
     g = torch.Generator().manual_seed(5 + rank)
     imgs = [torch.rand(3, H, W, generator=g).to(device) for _ in range(NI)]
     labels = [torch.rand(200, 2, generator=g) * torch.tensor([W, H], dtype=torch.float32) for _ in range(NI)]
-    aug = CropAugment()                                     # trainer.py:40-52 defaults
+    aug = CropAugment(noise_rng=args.noise_rng)             # trainer.py:40-52 defaults
     torch.manual_seed(rank)
     for _ in range(args.warmup):
         aug(imgs, labels, NC)
@@ -424,7 +426,7 @@ def run_augment(args, rank, device):
             "value": round(crops / el, 2), "unit": "crops/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic 1536x2048 images in HBM, 200 points each",
-            "config": {"workload": f"{NI} images x {NC} crops -> 224x224 (SURVEY §8f f2)"},
+            "config": {"workload": f"{NI} images x {NC} crops -> 224x224 (SURVEY §8f f2)", "noise_rng": args.noise_rng},
             "device_ms_per_step": round(dev_ms, 4),
             "cpu_baseline": {"value": round(len(sample) / cpu_el, 2), "unit": "crops/s", "cores": torch.get_num_threads(),
                              "kind": "port", "sample": f"{len(sample)} crops of the same plans through oracle/augment_ref.py "

@@ -126,9 +126,10 @@ __device__ __forceinline__ Pix jitter_apply(Pix p, int ops, int from, int to, co
     return p;
 }
 
-__device__ __forceinline__ float finish_px(float v, int c, int e, const EbcCropDesc& d, const EbcAugConst& k) {
+__device__ __forceinline__ float finish_px(float v, int c, int e, const EbcCropDesc& d, const float* __restrict__ noise,
+                                          const EbcAugConst& k) {
     if (d.noise) {
-        const float u = hash_uniform(d.seed, (uint32_t)e);
+        const float u = d.noise_off >= 0 && noise ? noise[d.noise_off + e] : hash_uniform(d.seed, (uint32_t)e);
         if (u < d.saltiness) v = 1.f;
         if (u > 1.f - d.spiciness) v = 0.f;
     }
@@ -173,7 +174,8 @@ __global__ __launch_bounds__(PT) void gray_partial_kernel(const EbcCropDesc* __r
 }
 
 __global__ __launch_bounds__(PT) void pointwise_kernel(const EbcCropDesc* __restrict__ desc, float* __restrict__ out,
-                                                      const float* __restrict__ ws, EbcAugConst k)
+                                                      const float* __restrict__ ws, const float* __restrict__ noise,
+                                                      EbcAugConst k)
 {
     const EbcCropDesc d = desc[blockIdx.y];
     const int y0 = blockIdx.x * RB, nops = n_ops(d.jitter_ops);
@@ -191,9 +193,9 @@ __global__ __launch_bounds__(PT) void pointwise_kernel(const EbcCropDesc* __rest
             const int e = y * d.out_w + x;
             Pix p = jitter_apply({R[e], R[HW + e], R[2 * HW + e]}, d.jitter_ops, 0, nops, d, cmean);
             if (!d.blur) {
-                p.r = finish_px(p.r, 0, e, d, k);
-                p.g = finish_px(p.g, 1, HW + e, d, k);
-                p.b = finish_px(p.b, 2, 2 * HW + e, d, k);
+                p.r = finish_px(p.r, 0, e, d, noise, k);
+                p.g = finish_px(p.g, 1, HW + e, d, noise, k);
+                p.b = finish_px(p.b, 2, 2 * HW + e, d, noise, k);
             }
             R[e] = p.r; R[HW + e] = p.g; R[2 * HW + e] = p.b;
         }
@@ -232,7 +234,8 @@ __global__ __launch_bounds__(PT) void blur_v_kernel(const EbcCropDesc* __restric
 }
 
 __global__ __launch_bounds__(PT) void blur_h_kernel(const EbcCropDesc* __restrict__ desc, float* __restrict__ out,
-                                                   const float* __restrict__ ws, EbcAugConst k)
+                                                   const float* __restrict__ ws, const float* __restrict__ noise,
+                                                   EbcAugConst k)
 {
     __shared__ float kx[EBC_AUG_MAX_BLUR];
     const EbcCropDesc d = desc[blockIdx.y / 3];
@@ -245,7 +248,7 @@ __global__ __launch_bounds__(PT) void blur_h_kernel(const EbcCropDesc* __restric
         for (int x = threadIdx.x; x < W; x += PT) {
             float acc = 0.f;
             for (int i = 0; i < k.blur_k; ++i) acc = fmaf(kx[i], S[y * W + reflect(x + i - hk, W)], acc);
-            O[y * W + x] = finish_px(acc, c, c * H * W + y * W + x, d, k);
+            O[y * W + x] = finish_px(acc, c, c * H * W + y * W + x, d, noise, k);
         }
 }
 
@@ -265,7 +268,7 @@ __global__ void point_map_kernel(const float* __restrict__ pts, const int* __res
 }  // namespace
 
 extern "C" int ebc_augment_crops(const float* src, const EbcCropDesc* desc, int n, int max_crop_h, int max_out_h,
-                                 float* out, float* workspace, EbcAugConst k, ebc_stream_t stream)
+                                 float* out, float* workspace, const float* noise, EbcAugConst k, ebc_stream_t stream)
 {
     if (n < 0 || !desc || !out || !workspace || max_crop_h < 0 || max_out_h < 0) return EBC_E_ARG;
     if (k.blur_k < 1 || k.blur_k > EBC_AUG_MAX_BLUR || (k.blur_k & 1) == 0) return EBC_E_ARG;
@@ -280,11 +283,11 @@ extern "C" int ebc_augment_crops(const float* src, const EbcCropDesc* desc, int 
     const int nb = (max_out_h + RB - 1) / RB;
     hipLaunchKernelGGL(gray_partial_kernel, dim3(nb, n), dim3(PT), 0, st, desc, out, workspace);
     EBC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(pointwise_kernel, dim3(nb, n), dim3(PT), 0, st, desc, out, workspace, k);
+    hipLaunchKernelGGL(pointwise_kernel, dim3(nb, n), dim3(PT), 0, st, desc, out, workspace, noise, k);
     EBC_CHECK_LAUNCH();
     hipLaunchKernelGGL(blur_v_kernel, dim3(nb, 3 * n), dim3(PT), 0, st, desc, out, workspace, k);
     EBC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(blur_h_kernel, dim3(nb, 3 * n), dim3(PT), 0, st, desc, out, workspace, k);
+    hipLaunchKernelGGL(blur_h_kernel, dim3(nb, 3 * n), dim3(PT), 0, st, desc, out, workspace, noise, k);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

@@ -30,6 +30,7 @@ _L = ctypes.c_long
 class EbcCropDesc(ctypes.Structure):
     """include/ebc_hip.h EbcCropDesc (one augmented training crop)."""
     _fields_ = [("src_off", ctypes.c_int64), ("out_off", ctypes.c_int64), ("tmp_off", ctypes.c_int64),
+                ("noise_off", ctypes.c_int64),
                 ("src_h", ctypes.c_int32), ("src_w", ctypes.c_int32), ("top", ctypes.c_int32), ("left", ctypes.c_int32),
                 ("crop_h", ctypes.c_int32), ("crop_w", ctypes.c_int32), ("out_h", ctypes.c_int32), ("out_w", ctypes.c_int32),
                 ("flip", ctypes.c_int32), ("jitter_ops", ctypes.c_int32),
@@ -107,7 +108,7 @@ SIGNATURES = {
     "ebc_avgpool2_bwd": (_I, [_I, _I, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_bn_add_relu_flat": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "ebc_prep_weights_1x1": (_I, [_I, _P, _P, _P, _I, _I, _P]),
-    "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, EbcAugConst, _P]),
+    "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, EbcAugConst, _P]),
     "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "ebc_probe_begin": (_I, [_I]),
     "ebc_probe_end": (_I, [_P, _I]),

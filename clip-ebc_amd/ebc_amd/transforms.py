@@ -19,9 +19,13 @@ Surface (mirrors the reference):
   * `plan_crop(...)` -- one crop's parameters and labels (the host half; used by the tests' oracle).
   * `generate_density_map(points, H, W)` -- datasets/utils.py:11-28 with sigma=None, batched.
 
-Deviations, by design: the salt-and-pepper field is drawn on device from a counter-based hash seeded by
-one host draw (the reference draws `torch.rand_like(image)` on the CPU), so the host RNG stream -- and
-with it the parameters of later crops -- diverges from the reference's after the first noisy crop;
+The salt-and-pepper uniforms come from one of two sources (`noise_rng`):
+  * "device" (default): a counter-based hash on device seeded by ONE host draw -- no 600 KB host draw and
+    upload per noisy crop, but the host RNG stream (and with it every later crop's parameters) diverges
+    from the reference's after the first noisy crop;
+  * "reference": the host draws the field with the reference's own call, `torch.rand_like(image)` on the
+    [3, S, S] crop (datasets/transforms.py:252), at its place in the stream, and uploads it: the whole
+    stream -- every crop's window, flip, jitter factors and noise -- is the reference's draw for draw.
 `hue != 0` is unsupported (the reference's README sets hue = 0: positive values give NaN DMCount losses).
 """
 from __future__ import annotations
@@ -54,6 +58,7 @@ class CropPlan:
     blur: bool = False
     noise: bool = False
     seed: int = 0
+    noise_field: Optional[Tensor] = None     # [3, S, S] uniforms drawn by the host (noise_rng="reference")
 
 
 def _check_jitter(value: float, name: str, center: float = 1.0, clip_first_on_zero: bool = True):
@@ -100,7 +105,11 @@ class CropAugment:
                  brightness: float = 0.1, contrast: float = 0.1, saturation: float = 0.1, hue: float = 0.0,
                  kernel_size: int = 5, saltiness: float = 1e-3, spiciness: float = 1e-3,
                  jitter_prob: float = 0.2, blur_prob: float = 0.2, noise_prob: float = 0.5, flip_prob: float = 0.5,
-                 blur_sigma: Tuple[float, float] = (0.1, 5.0), mean=IMAGENET_MEAN, std=IMAGENET_STD):
+                 blur_sigma: Tuple[float, float] = (0.1, 5.0), mean=IMAGENET_MEAN, std=IMAGENET_STD,
+                 noise_rng: str = "device"):
+        if noise_rng not in ("device", "reference"):
+            raise ValueError(f"noise_rng must be 'device' or 'reference', got {noise_rng!r}")
+        self.noise_rng = noise_rng
         if not 0 < min_scale <= max_scale:
             raise ValueError(f"scale should satisfy 0 < scale[0] <= scale[1], got {(min_scale, max_scale)}.")
         if hue != 0.0:
@@ -124,7 +133,8 @@ class CropAugment:
 
         RandomResizedCrop (datasets/transforms.py:133-171), RandomHorizontalFlip (:174-187), RandomApply
         (:226-239) over ColorJitter (torchvision ColorJitter.get_params: randperm(4), then one uniform per
-        enabled factor), GaussianBlur (no draw) and PepperSaltNoise (one seed draw here)."""
+        enabled factor), GaussianBlur (no draw) and PepperSaltNoise (one seed draw, or with
+        noise_rng="reference" the reference's `torch.rand_like(image)` field, transforms.py:252)."""
         out_h, out_w = self.size
         scale = torch.empty(1).uniform_(self.scale[0], self.scale[1]).item()
         crop_h, crop_w = int(out_h * scale), int(out_w * scale)
@@ -161,7 +171,11 @@ class CropAugment:
             plan.blur = True
         if torch.rand(1) < self.p[2]:
             plan.noise = True
-            plan.seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+            if self.noise_rng == "reference":
+                # rand_like of the float32 [3, out_h, out_w] crop: the same generator call as torch.rand of that shape
+                plan.noise_field = torch.rand(3, out_h, out_w)
+            else:
+                plan.seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
         return plan, label
 
     # ---------------------------------------------------------------- device half
@@ -194,6 +208,7 @@ class CropAugment:
         descs = (_lib.EbcCropDesc * n)()
         tmp = 0
         max_ch = 0
+        fields = []
         for k, p in enumerate(plans):
             src = srcs[pre_index.get(k, p.image)]
             off = src.data_ptr() - base
@@ -213,14 +228,24 @@ class CropAugment:
             d.brightness, d.contrast, d.saturation = f[JIT_BRIGHTNESS], f[JIT_CONTRAST], f[JIT_SATURATION]
             d.blur, d.noise = int(p.blur), int(p.noise)
             d.saltiness, d.spiciness, d.seed = self.saltiness, self.spiciness, p.seed & 0xFFFFFFFF
+            d.noise_off = -1
+            if p.noise and p.noise_field is not None:
+                if tuple(p.noise_field.shape) != (3, out_h, out_w) or p.noise_field.dtype != torch.float32:
+                    raise ValueError(f"noise_field must be float32 [3, {out_h}, {out_w}], got {p.noise_field.shape}")
+                d.noise_off = len(fields) * 3 * out_h * out_w
+                fields.append(p.noise_field)
             d.normalize = int(normalize)
             tmp += 3 * max(p.crop_h, out_h) * out_w
             max_ch = max(max_ch, p.crop_h)
         ws = torch.empty(tmp, device=dev)
         ddesc = _upload(descs, dev)
+        noise = None
+        if fields:
+            noise = torch.stack(fields).pin_memory().to(dev, non_blocking=True)
         src_base = ctypes.c_void_p(base)
         _lib.check(L.ebc_augment_crops(src_base, _lib.ptr(ddesc), n, max_ch, out_h, _lib.ptr(out), _lib.ptr(ws),
-                                       self.const, _lib.stream(dev)), "ebc_augment_crops")
+                                       _lib.ptr(noise), self.const, _lib.stream(dev)),
+                   "ebc_augment_crops")
         return out     # temporaries are released stream-ordered (caching allocator), after the launches
 
     def _resize_whole(self, img: Tensor, h: int, w: int) -> Tensor:
@@ -229,13 +254,13 @@ class CropAugment:
         img = img.contiguous()
         out = torch.empty(1, 3, h, w, device=img.device)
         d = (_lib.EbcCropDesc * 1)()
-        d[0].src_off, d[0].out_off, d[0].tmp_off = 0, 0, 0
+        d[0].src_off, d[0].out_off, d[0].tmp_off, d[0].noise_off = 0, 0, 0, -1
         d[0].src_h, d[0].src_w = img.shape[1], img.shape[2]
         d[0].top, d[0].left, d[0].crop_h, d[0].crop_w, d[0].out_h, d[0].out_w = 0, 0, img.shape[1], img.shape[2], h, w
         ws = torch.empty(3 * max(img.shape[1], h) * w, device=img.device)
         ddesc = _upload(d, img.device)
         _lib.check(L.ebc_augment_crops(_lib.ptr(img), _lib.ptr(ddesc), 1, img.shape[1], h, _lib.ptr(out), _lib.ptr(ws),
-                                       self.const, _lib.stream(img)), "ebc_augment_crops (pre-resize)")
+                                       None, self.const, _lib.stream(img)), "ebc_augment_crops (pre-resize)")
         return out[0]
 
     def __call__(self, images: Sequence[Tensor], labels: Sequence[Tensor], num_crops: int = 1):

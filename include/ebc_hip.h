@@ -216,12 +216,17 @@ int ebc_tile_assemble(const float* preds, float* out, int Cp, int H, int W, int 
  *   jitter_ops            ColorJitter order (transforms.py:190-201 -> torchvision ColorJitter):
  *                         3 bits per slot, 1 brightness, 2 contrast, 3 saturation (hue unsupported)
  *   blur                  GaussianBlur(kernel_size, sigma=(sx, sy)) (transforms.py:217-223), reflect pad
- *   noise                 PepperSaltNoise (transforms.py:242-255), counter-based uniforms from `seed`
+ *   noise                 PepperSaltNoise (transforms.py:242-255) over uniforms u[3][out_h][out_w]:
+ *                         noise_off >= 0: u = noise + noise_off, a field the host drew with the reference's own
+ *                         `torch.rand_like(image)` (transforms.py:252), so the host RNG stream stays the reference's;
+ *                         noise_off < 0: u = counter-based uniforms from `seed` (no host draw, no upload)
  *   normalize             Normalize(ImageNet mean/std) (datasets/crowd.py:64,162)
- * workspace: per crop tmp_off .. + max(3*crop_h*out_w, 3*out_h*out_w) floats (caller-assigned). */
+ * workspace: per crop tmp_off .. + max(3*crop_h*out_w, 3*out_h*out_w) floats (caller-assigned).
+ * noise: the device uniform fields noise_off indexes; NULL = every crop takes the counter-based uniforms. */
 #define EBC_AUG_MAX_BLUR 31
 typedef struct {
     int64_t src_off, out_off, tmp_off;   /* element offsets: source image [3][src_h][src_w], output [3][out_h][out_w], scratch */
+    int64_t noise_off;                   /* element offset of this crop's uniform field in `noise`, or -1 (hash of seed) */
     int32_t src_h, src_w, top, left, crop_h, crop_w, out_h, out_w;
     int32_t flip, jitter_ops;
     float brightness, contrast, saturation;
@@ -237,7 +242,7 @@ typedef struct {
 } EbcAugConst;
 /* max_crop_h / max_out_h: maxima over the descriptors (grid sizing) */
 int ebc_augment_crops(const float* src, const EbcCropDesc* desc, int n, int max_crop_h, int max_out_h, float* out,
-                      float* workspace, EbcAugConst k, ebc_stream_t stream);
+                      float* workspace, const float* noise, EbcAugConst k, ebc_stream_t stream);
 /* generate_density_map(label, H, W, sigma=None) (datasets/utils.py:11-28) for B crops: out [B][1][H][W]
  * = 1 at (clamp(int y), clamp(int x)) of points [sum n, 2] (x, y), offsets [B+1] (device) */
 int ebc_point_map(const float* points, const int* offsets, int B, int H, int W, int max_points, float* out,

@@ -10,8 +10,12 @@ that `ebc_amd.transforms.CropAugment.plan_crop` drew.  Pinning:
     adjust_contrast / adjust_saturation / rgb_to_grayscale / _blend, gaussian_blur with reflect padding
     and the outer-product kernel); torchvision is not importable here, so these two are
     "parity unpinned" against the library itself (the restatement follows its published code);
-  * PepperSaltNoise: the reference's two `torch.where`s (transforms.py:242-255) over the same
-    counter-based uniforms the device draws (`hash_uniform`).
+  * PepperSaltNoise: the reference's two `torch.where`s (transforms.py:242-255) over the plan's host-drawn
+    field (noise_rng="reference") or the same counter-based uniforms the device draws (`hash_uniform`).
+`reference_crop` restates the whole train transform of one crop -- its torch RNG calls in the reference's
+order (RandomResizedCrop :133-171, RandomHorizontalFlip :174-187, RandomApply :226-239 over torchvision
+ColorJitter.get_params / GaussianBlur / PepperSaltNoise's rand_like :252) and the label arithmetic -- so a
+whole multi-crop stream can be compared draw for draw with CropAugment(noise_rng="reference").
 """
 from __future__ import annotations
 
@@ -93,7 +97,10 @@ def apply_plans(images: Sequence[torch.Tensor], plans, size, saltiness=1e-3, spi
         if p.blur:
             img = gaussian_blur(img, kernel_size, sigma[0], sigma[1])
         if p.noise:
-            u = torch.from_numpy(hash_uniform(p.seed, img.numel())).reshape(img.shape)
+            if getattr(p, "noise_field", None) is not None:
+                u = p.noise_field
+            else:
+                u = torch.from_numpy(hash_uniform(p.seed, img.numel())).reshape(img.shape)
             img = torch.where(u < saltiness, 1.0, img)
             img = torch.where(u > 1 - spiciness, 0.0, img)
         if normalize:
@@ -111,3 +118,88 @@ def density_map(label: torch.Tensor, h: int, w: int) -> torch.Tensor:
         lab[:, 1] = lab[:, 1].clamp(min=0, max=h - 1)
         d[0, lab[:, 1], lab[:, 0]] = 1.0
     return d
+
+
+def _resize_pair(img, label, h, w):
+    """datasets/transforms.py:_resize (:28-43)."""
+    ih, iw = img.shape[-2:]
+    if ih == h and iw == w:
+        return img, label
+    img = resize(img, h, w)
+    if len(label) > 0:
+        label[:, 0] = label[:, 0] * w / iw
+        label[:, 1] = label[:, 1] * h / ih
+        label[:, 0] = label[:, 0].clamp(min=0, max=w - 1)
+        label[:, 1] = label[:, 1].clamp(min=0, max=h - 1)
+    return img, label
+
+
+def _crop_pair(img, label, top, left, h, w):
+    """datasets/transforms.py:_crop (:9-25)."""
+    img = img[:, top:top + h, left:left + w]
+    if len(label) > 0:
+        label[:, 0] -= left
+        label[:, 1] -= top
+        m = (label[:, 0] >= 0) & (label[:, 0] < w) & (label[:, 1] >= 0) & (label[:, 1] < h)
+        label = label[m]
+    return img, label
+
+
+def _jitter_range(v):
+    """torchvision ColorJitter._check_input for a scalar: (max(1 - v, 0), 1 + v), None when (1, 1)."""
+    lo, hi = max(1.0 - v, 0.0), 1.0 + v
+    return None if lo == hi == 1.0 else (lo, hi)
+
+
+def reference_crop(image, label, size=224, scale=(1.0, 2.0), brightness=0.1, contrast=0.1, saturation=0.1,
+                   kernel_size=5, saltiness=1e-3, spiciness=1e-3, probs=(0.2, 0.2, 0.5), flip_prob=0.5,
+                   sigma=(0.1, 5.0)):
+    """One crop of the train transform (utils/data_utils.py:15-24) with the reference's RNG calls, unnormalised."""
+    img, label = image.float().clone(), label.float().clone()
+    # RandomResizedCrop (transforms.py:147-171)
+    s = torch.empty(1).uniform_(scale[0], scale[1]).item()
+    ch, cw = int(size * s), int(size * s)
+    ih, iw = img.shape[-2:]
+    if ch <= ih and cw <= iw:
+        top = torch.randint(0, ih - ch + 1, (1,)).item()
+        left = torch.randint(0, iw - cw + 1, (1,)).item()
+    else:
+        ratio = max(ch / ih, cw / iw)
+        rh, rw = int(ih * ratio) + 1, int(iw * ratio) + 1
+        img, label = _resize_pair(img, label, rh, rw)
+        top = torch.randint(0, rh - ch + 1, (1,)).item()
+        left = torch.randint(0, rw - cw + 1, (1,)).item()
+    img, label = _crop_pair(img, label, top, left, ch, cw)
+    img, label = _resize_pair(img, label, size, size)
+    # RandomHorizontalFlip (:179-187)
+    if torch.rand(1) < flip_prob:
+        img = img.flip(-1)
+        if len(label) > 0:
+            label[:, 0] = img.shape[-1] - 1 - label[:, 0]
+            label[:, 0] = label[:, 0].clamp(min=0, max=img.shape[-1] - 1)
+    # RandomApply (:233-239): ColorJitter, GaussianBlur, PepperSaltNoise
+    if torch.rand(1) < probs[0]:
+        rb, rc, rs = _jitter_range(brightness), _jitter_range(contrast), _jitter_range(saturation)
+        fn_idx = torch.randperm(4)          # torchvision ColorJitter.get_params
+        b = None if rb is None else float(torch.empty(1).uniform_(rb[0], rb[1]))
+        c = None if rc is None else float(torch.empty(1).uniform_(rc[0], rc[1]))
+        sa = None if rs is None else float(torch.empty(1).uniform_(rs[0], rs[1]))
+        for fn in fn_idx.tolist():
+            if fn == 0 and b is not None:
+                img = jitter(img, 1, b)
+            elif fn == 1 and c is not None:
+                img = jitter(img, 2, c)
+            elif fn == 2 and sa is not None:
+                img = jitter(img, 3, sa)
+    if torch.rand(1) < probs[1]:
+        img = gaussian_blur(img, kernel_size, sigma[0], sigma[1])
+    if torch.rand(1) < probs[2]:
+        noise = torch.rand_like(img)
+        img = torch.where(noise < saltiness, 1.0, img)
+        img = torch.where(noise > 1 - spiciness, 0.0, img)
+    return img, label
+
+
+def normalize(img):
+    """datasets/crowd.py:64,162 Normalize(ImageNet mean / std)."""
+    return (img - torch.tensor(MEAN)[:, None, None]) / torch.tensor(STD)[:, None, None]

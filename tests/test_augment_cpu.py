@@ -58,3 +58,63 @@ def test_draw_order_is_the_references():
         torch.empty(1).uniform_(0.9, 1.1)
     torch.rand(1); torch.rand(1)
     assert torch.rand(1).item() == after
+
+
+def test_rand_like_is_rand_of_the_shape():
+    """PepperSaltNoise draws torch.rand_like(image) (transforms.py:252); the host half draws torch.rand of the
+    crop's shape: the same generator call, the same values."""
+    torch.manual_seed(5)
+    a = torch.rand_like(torch.empty(3, 224, 224))
+    torch.manual_seed(5)
+    assert torch.equal(a, torch.rand(3, 224, 224))
+
+
+def _stream(aug_kw, shapes, n_per, seed, ref_mode):
+    """(plans, labels, next draw) of CropAugment.plan_crop, or (images, labels, next draw) of the oracle's
+    restated reference transform, over the same seeded multi-crop stream."""
+    from ebc_amd.transforms import CropAugment
+    from oracle import augment_ref as ref
+    g = torch.Generator().manual_seed(17)
+    imgs = [torch.rand(3, h, w, generator=g) for h, w in shapes]
+    labs = [torch.rand(40, 2, generator=g) * torch.tensor([w, h], dtype=torch.float32) for h, w in shapes]
+    torch.manual_seed(seed)
+    outs, labels = [], []
+    if ref_mode:
+        for img, lab in zip(imgs, labs):
+            for _ in range(n_per):
+                o, l = ref.reference_crop(img, lab, 224, (aug_kw["min_scale"], aug_kw["max_scale"]),
+                                          aug_kw["brightness"], aug_kw["contrast"], aug_kw["saturation"], 5,
+                                          aug_kw["saltiness"], aug_kw["spiciness"],
+                                          (aug_kw["jitter_prob"], aug_kw["blur_prob"], aug_kw["noise_prob"]))
+                outs.append(o)
+                labels.append(l)
+    else:
+        aug = CropAugment(224, noise_rng="reference", **aug_kw)
+        for i, (img, lab) in enumerate(zip(imgs, labs)):
+            for _ in range(n_per):
+                p, l = aug.plan_crop(i, img.shape[1], img.shape[2], lab.clone())
+                outs.append(p)
+                labels.append(l)
+    return imgs, outs, labels, torch.rand(1).item()
+
+
+AUG_KW = dict(min_scale=1.0, max_scale=2.0, brightness=0.4, contrast=0.4, saturation=0.4, saltiness=0.02,
+              spiciness=0.02, jitter_prob=0.5, blur_prob=0.3, noise_prob=0.5)
+SHAPES = [(300, 400), (200, 180), (480, 640)]
+
+
+def test_reference_rng_stream_is_the_references():
+    """noise_rng="reference": a multi-crop stream with noisy crops in the middle consumes the reference's draws
+    one for one -- every crop's labels, pixels (oracle pixel path on the drawn plans) and the generator state
+    after the stream equal the restated reference transform's (oracle/augment_ref.reference_crop)."""
+    from oracle import augment_ref as ref
+    imgs, plans, lab_a, nxt_a = _stream(AUG_KW, SHAPES, 3, 23, False)
+    _, ref_imgs, lab_b, nxt_b = _stream(AUG_KW, SHAPES, 3, 23, True)
+    noisy = [k for k, p in enumerate(plans) if p.noise]
+    assert noisy and noisy[0] < len(plans) - 1, "the seed must give a noisy crop before the last one"
+    assert nxt_a == nxt_b
+    for a, b in zip(lab_a, lab_b):
+        assert torch.equal(a, b)
+    got = ref.apply_plans(imgs, plans, (224, 224), saltiness=0.02, spiciness=0.02, normalize=False)
+    for k in range(len(plans)):
+        assert (got[k] - ref_imgs[k]).abs().max().item() < 1e-5, k

@@ -104,3 +104,37 @@ def test_crowd_batch_end_to_end():
     assert torch.isfinite(x).all()
     for p, d in zip(points, dens.cpu()):
         assert torch.equal(d, ref.density_map(p, 224, 224))
+
+
+def test_reference_rng_stream_end_to_end():
+    """CropAugment(noise_rng="reference")(images, labels, num_crops) over a multi-crop stream with noisy crops
+    in the middle equals the restated reference transform run crop after crop from the same seed
+    (oracle/augment_ref.reference_crop: transforms.py:133-262 with rand_like for the noise): labels exact,
+    dot maps exact, normalised pixels within 1e-4 (jitter / blur f32 order), and the generator ends in the same
+    state -- the stream is the reference's draw for draw after every noisy crop."""
+    from ebc_amd.transforms import CropAugment
+    from oracle import augment_ref as ref
+    shapes = [(300, 400), (200, 180), (480, 640)]
+    kw = dict(min_scale=1.0, max_scale=2.0, brightness=0.4, contrast=0.4, saturation=0.4, saltiness=0.02,
+              spiciness=0.02, jitter_prob=0.5, blur_prob=0.3, noise_prob=0.5)
+    g = torch.Generator().manual_seed(17)
+    imgs = [torch.rand(3, h, w, generator=g) for h, w in shapes]
+    labs = [torch.rand(40, 2, generator=g) * torch.tensor([w, h], dtype=torch.float32) for h, w in shapes]
+    torch.manual_seed(23)
+    exp, exp_lab = [], []
+    for img, lab in zip(imgs, labs):
+        for _ in range(3):
+            o, l = ref.reference_crop(img, lab, 224, (1.0, 2.0), 0.4, 0.4, 0.4, 5, 0.02, 0.02, (0.5, 0.3, 0.5))
+            exp.append(ref.normalize(o))
+            exp_lab.append(l)
+    nxt_ref = torch.rand(1).item()
+    torch.manual_seed(23)
+    x, points, dens = CropAugment(224, noise_rng="reference", **kw)([t.cuda() for t in imgs], labs, num_crops=3)
+    nxt = torch.rand(1).item()
+    assert nxt == nxt_ref
+    x = x.cpu()
+    assert x.shape == (9, 3, 224, 224)
+    for k in range(9):
+        assert torch.equal(points[k], exp_lab[k]), k
+        assert torch.equal(dens[k].cpu(), ref.density_map(exp_lab[k], 224, 224)), k
+        assert (x[k] - exp[k]).abs().max().item() < 1e-4, k
