@@ -587,7 +587,7 @@ def main():
                                "method": "in-step kernel durations from the runtime's kernel trace (torch.profiler / "
                                          "roctracer, the rocprofv3 --kernel-trace source) over 3 steps; kernel classes "
                                          "(shape, epilogue) from 3 ebc_probe steps, matched in launch order"}
-            out["kernels"] = kernels[:12]
+            out["kernels"] = kernels[:24]
             out["sinkhorn"] = sink
         if world == 1 and not args.no_cpu_baseline:
             if rn:

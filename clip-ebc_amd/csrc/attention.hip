@@ -131,21 +131,29 @@ __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* bas
 template <int NW>
 __device__ __forceinline__ void touch_issue(const TouchList& t, unsigned& sink)
 {
-    const int lane = threadIdx.x & 63, nw = NW;
-    const size_t gw = (size_t)blockIdx.x * nw + (threadIdx.x >> 6), GW = (size_t)gridDim.x * nw;
+    // the lines of all listed buffers are dealt out as one sequence over every lane of the grid, so no lane loads a
+    // second line before every lane has one (per buffer from lane 0, the first waves took every buffer's first lines
+    // and their ends, i.e. the launch's, grew with the list: r03 per-class A/B, tools/ab_classes.sh)
+    const int nw = NW;
+    const size_t me = ((size_t)blockIdx.x * nw + (threadIdx.x >> 6)) * 64 + (threadIdx.x & 63);
+    const size_t tot = (size_t)gridDim.x * nw * 64;
+    size_t cum = 0;
     for (int b = 0; b < t.n; ++b) {
         const char* base = reinterpret_cast<const char*>(t.ptr[b]);
         const size_t lines = t.bytes[b] >> 7;
-        for (size_t c = gw * 64 + lane; c < lines; c += GW * 64) {
+        for (size_t c = (me + tot - cum % tot) % tot; c < lines; c += tot) {
             const char* a = base + (c << 7);
             asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(a) : "memory");
         }
+        cum += lines;
     }
 }
 __device__ __forceinline__ void touch_wait(unsigned sink) { asm volatile("s_waitcnt vmcnt(0)" :: "v"(sink) : "memory"); }
 
 // ------------------------------------------------------------------------------ forward
-template <class E, int NWV, int LFIX>
+// QT query tiles of 16 per wave: every K row fragment and V column fragment read from LDS feeds QT MFMAs (the LDS
+// reads per query halve at QT = 2; with one tile per wave the forward was bound by re-reading K and V per 16 queries)
+template <class E, int NWV, int LFIX, int QT = 1>
 __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T* __restrict__ qkv, typename E::T* __restrict__ out,
                                                        float* __restrict__ lse, int B, int L_, int H, float scale,
                                                        TouchList touch)
@@ -156,7 +164,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
-    constexpr int QB = 16 * NWV;
+    constexpr int QB = 16 * NWV * QT;
     const int nqb = (L + QB - 1) / QB;
     const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
     const int b = bh / H, h = bh % H;
@@ -168,11 +176,14 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     rows_fetch<E, NWV>(fv, base + 2 * D, D3, L);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
-    const int q0 = qb * QB + w * 16;
-    const int qme = q0 + fr;                                   // this lane's query (column of S^T)
-    typename E::Frag qf[2];
+    const int q0 = qb * QB + w * 16 * QT;                      // this wave's first query; tile t starts at q0 + 16 t
+    typename E::Frag qf[QT][2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qme < L);
+    for (int t = 0; t < QT; ++t) {
+        const int qme = q0 + 16 * t + fr;                      // this lane's query in tile t (column of S^T)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[t][ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qme < L);
+    }
     rows_store<E, NWV>(Ks, fk);
     rows_store<E, NWV>(Vs, fv);
     __syncthreads();
@@ -185,68 +196,91 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     const int nkt = (L + 15) >> 4;
     const bool ragged = (L & 15) != 0;
     const float c2 = scale * LOG2E;
-    f32x4 s[NKT];
+    f32x4 s[QT][NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-        s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < QT; ++t) s[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (kt < nkt) {
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) s[kt] = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], s[kt]);
-        }
-    }
-    // s[kt][i] = S[q = qme][key = 16 kt + 4 fg + i]
-    float mx = -INFINITY;
+            for (int ks = 0; ks < 2; ++ks) {
+                const typename E::Frag kf = lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg);
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-        if (kt < nkt) {
-            if (ragged && kt == nkt - 1) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (16 * kt + 4 * fg + i >= L) s[kt][i] = -INFINITY;
+                for (int t = 0; t < QT; ++t) s[t][kt] = mma(kf, qf[t][ks], s[t][kt]);
             }
-            mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
         }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mc = mx * c2;
-    float sum = 0.f;
+    // s[t][kt][i] = S[q = q0 + 16 t + fr][key = 16 kt + 4 fg + i]
+    float mx[QT], sum[QT];
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-        if (kt < nkt) {
+    for (int t = 0; t < QT; ++t) {
+        mx[t] = -INFINITY;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { s[kt][i] = __builtin_amdgcn_exp2f(fmaf(s[kt][i], c2, -mc)); sum += s[kt][i]; }
+        for (int kt = 0; kt < NKT; ++kt) {
+            if (kt < nkt) {
+                if (ragged && kt == nkt - 1) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (16 * kt + 4 * fg + i >= L) s[t][kt][i] = -INFINITY;
+                }
+                mx[t] = fmaxf(mx[t], fmaxf(fmaxf(s[t][kt][0], s[t][kt][1]), fmaxf(s[t][kt][2], s[t][kt][3])));
+            }
         }
+        mx[t] = fmaxf(mx[t], __shfl_xor(mx[t], 16, 64));
+        mx[t] = fmaxf(mx[t], __shfl_xor(mx[t], 32, 64));
+        const float mc = mx[t] * c2;
+        sum[t] = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+            if (kt < nkt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { s[t][kt][i] = __builtin_amdgcn_exp2f(fmaf(s[t][kt][i], c2, -mc)); sum[t] += s[t][kt][i]; }
+            }
+        }
+        sum[t] += __shfl_xor(sum[t], 16, 64);
+        sum[t] += __shfl_xor(sum[t], 32, 64);
     }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
 
-    f32x4 o[HD / 16];
+    f32x4 o[QT][HD / 16];
 #pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) o[t][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int st = 0; st < NKT / 2; ++st) {
         if (2 * st >= nkt) continue;
-        const float pv[8] = {s[2 * st][0], s[2 * st][1], s[2 * st][2], s[2 * st][3],
-                             s[2 * st + 1][0], s[2 * st + 1][1], s[2 * st + 1][2], s[2 * st + 1][3]};
-        const typename E::Frag pf = pack8<E>(pv);
+        typename E::Frag pf[QT];
 #pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) o[dt] = mma(pf, attn_colfrag<E>(Vs, 32 * st, 16 * dt), o[dt]);
-    }
-    // o[dt][i] = O[q = q0 + 4 fg + i][d = 16 dt + fr]; divide by the row sum held on lane (q - q0)
-    const float inv = 1.0f / sum;
+        for (int t = 0; t < QT; ++t) {
+            const float pv[8] = {s[t][2 * st][0], s[t][2 * st][1], s[t][2 * st][2], s[t][2 * st][3],
+                                 s[t][2 * st + 1][0], s[t][2 * st + 1][1], s[t][2 * st + 1][2], s[t][2 * st + 1][3]};
+            pf[t] = pack8<E>(pv);
+        }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int ql = 4 * fg + i;
-        const float iv = __shfl(inv, ql, 64);
-        const int q = q0 + ql;
-        if (q < L) {
-            T* orow = out + ((size_t)b * L + q) * D + h * HD;
+        for (int dt = 0; dt < HD / 16; ++dt) {
+            const typename E::Frag vf = attn_colfrag<E>(Vs, 32 * st, 16 * dt);
 #pragma unroll
-            for (int dt = 0; dt < HD / 16; ++dt) orow[16 * dt + fr] = E::from(o[dt][i] * iv);
+            for (int t = 0; t < QT; ++t) o[t][dt] = mma(pf[t], vf, o[t][dt]);
         }
     }
-    if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx * scale + logf(sum);   // natural-log units of the scaled scores
+    // o[t][dt][i] = O[q = q0 + 16 t + 4 fg + i][d = 16 dt + fr]; divide by the row sum held on lane (q - q0 - 16 t)
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+        const float inv = 1.0f / sum[t];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ql = 4 * fg + i;
+            const float iv = __shfl(inv, ql, 64);
+            const int q = q0 + 16 * t + ql;
+            if (q < L) {
+                T* orow = out + ((size_t)b * L + q) * D + h * HD;
+#pragma unroll
+                for (int dt = 0; dt < HD / 16; ++dt) orow[16 * dt + fr] = E::from(o[t][dt][i] * iv);
+            }
+        }
+        const int qme = q0 + 16 * t + fr;
+        if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx[t] * scale + logf(sum[t]);   // natural-log units
+    }
     if (touch.n) touch_wait(tsink);
 }
 
@@ -515,16 +549,16 @@ int attn_waves(int L) {
 // the CLIP ViT-B/16 + 32-prompt sequence (1 + 32 + 196 tokens) gets kernels compiled for it
 constexpr int L_VPT32 = 229;
 
-template <class E, int NW, int LFIX> int attn_fwd_nw(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,
-                                                     const TouchList* touch = nullptr)
+template <class E, int NW, int LFIX, int QT = 1> int attn_fwd_nw(const void* qkv, void* out, float* lse, int B, int L, int H,
+                                                                hipStream_t st, const TouchList* touch = nullptr)
 {
     using C = AttnCfg<E>;
     const TouchList t = touch ? *touch : TouchList{};
     const size_t lds = 2 * C::TILE_BYTES;
-    if (!ensure_lds<attn_fwd_kernel<E, NW, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
-    const int grid = B * H * ((L + 16 * NW - 1) / (16 * NW));
+    if (!ensure_lds<attn_fwd_kernel<E, NW, LFIX, QT>>((int)lds, st)) return EBC_E_LAUNCH;
+    const int grid = B * H * ((L + 16 * NW * QT - 1) / (16 * NW * QT));
     const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_FWD, 0, 0, 0, 0, B, L, H, st) : -1;
-    hipLaunchKernelGGL((attn_fwd_kernel<E, NW, LFIX>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
+    hipLaunchKernelGGL((attn_fwd_kernel<E, NW, LFIX, QT>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
                        (typename E::T*)out, lse, B, L, H, 0.125f, t);
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();

@@ -10,6 +10,7 @@
 # rbench the clip_resnet50 bench line (configs[1]) -> gpurun_out/TAG_rbench.json
 # rprof  rocprofv3 --kernel-trace --stats of the clip_resnet50 bench, cut to the timed steps
 # pstep  the bench command under rocprofv3: kernel trace + 2 PMC passes, per kernel class (tools/pmc_step.py)
+# lab:NAME  tools/lab/bin/NAME (LAB_ARGS) -> gpurun_out/TAG_NAME.txt;  plab:NAME  the same under rocprofv3 --kernel-trace --stats
 # Every GPU step has its own time limit and the steps are chained: the first failure ends the session.
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -79,6 +80,19 @@ for what in "$@"; do
         --json $O/${TAG}_pmc_step.json > $O/${TAG}_pmc_step.txt || { echo "pmc_step failed"; exit 1; }
       rm -rf $O/${TAG}_pmc1 $O/${TAG}_pmc2
       head -12 $O/${TAG}_pmc_step.txt | cut -c1-400 ;;
+    lab:*)
+      # a lab binary (tools/lab/bin/NAME, built here), its stdout -> gpurun_out/TAG_NAME.txt; LAB_ARGS passes arguments
+      name=${what#lab:}
+      timeout -k 10 400 $R/tools/lab/bin/$name $LAB_ARGS > $O/${TAG}_$name.txt 2>&1 || { tail -30 $O/${TAG}_$name.txt; exit 1; }
+      tail -8 $O/${TAG}_$name.txt ;;
+    plab:*)
+      # the same under rocprofv3 --kernel-trace --stats: per-kernel-name durations -> gpurun_out/TAG_NAME_stats.csv
+      name=${what#plab:}
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_${name}_p -o run -- \
+        $R/tools/lab/bin/$name $LAB_ARGS > $O/${TAG}_$name.txt 2>&1) || { tail -30 $O/${TAG}_$name.txt; exit 1; }
+      st=$(find $O/${TAG}_${name}_p -name "*kernel_stats.csv" | head -1)
+      cp "$st" $O/${TAG}_${name}_stats.csv && rm -rf $O/${TAG}_${name}_p
+      cut -d, -f1-8 $O/${TAG}_${name}_stats.csv | head -20 ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done

@@ -6,6 +6,7 @@
 //   run:   gemm_lab [rounds] [reps]
 #include "../../clip-ebc_amd/csrc/gemm.hip"
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -59,6 +60,22 @@ Variant v128x96(const char* nm) {
     return {nm, [](const GemmArgs& g) { return launch_gemm_k<EF16, TO, EPI, 128, 96, S, 2, 2, 128, 0, false, NLW>(g, 0); }};
 }
 
+// split-K over `splits` workgroups per tile with the in-kernel last-arriver sum (gemm_nt_kernel SPL path); the
+// counters + partials live in one workspace (counters zero on entry, re-armed by the kernel)
+static void* g_splitws = nullptr;
+constexpr size_t LAB_CNT_BYTES = 16 * 1024;
+template <class TO, int EPI, int BM, int BN, int S, int WGM, int WGN>
+Variant vsplit(const char* nm, int splits) {
+    return {nm, [splits](const GemmArgs& g0) {
+        GemmArgs g = g0;
+        g.splits = splits;
+        g.kslice = g.K / splits;
+        g.cnt = reinterpret_cast<int*>(g_splitws);
+        g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(g_splitws) + LAB_CNT_BYTES);
+        return launch_gemm_k<EF16, TO, EPI, BM, BN, S, WGM, WGN, 128, 0, true, 0>(g, 0);
+    }};
+}
+
 int main(int argc, char** argv)
 {
     const int rounds = argc > 1 ? atoi(argv[1]) : 3, reps = argc > 2 ? atoi(argv[2]) : 30;
@@ -87,6 +104,22 @@ int main(int argc, char** argv)
                       {v128x96<_Float16, EPI_STORE, 3, 0>("128x96 S3 4w"), v128x96<_Float16, EPI_STORE, 4, 4>("128x96 S4 4w+4L")}});
     shapes.push_back({"out+res K768", 768, 768, EPI_RESID, true,
                       {v128x96<float, EPI_RESID, 3, 0>("128x96 S3 4w"), v128x96<float, EPI_RESID, 3, 4>("128x96 S3 4w+4L")}});
+    // r03 split-K A/B: the in-kernel last-arriver sum at the N = 768 shapes
+    CK(hipMalloc(&g_splitws, LAB_CNT_BYTES + ((size_t)64 << 20)));
+    CK(hipMemset(g_splitws, 0, LAB_CNT_BYTES + ((size_t)64 << 20)));
+    shapes.push_back({"split c_proj K3072", 768, 3072, EPI_RESID, true,
+                      {v128x96<float, EPI_RESID, 4, 4>("128x96 S4 4w+4L"),
+                       vsplit<float, EPI_RESID, 128, 192, 3, 2, 2>("128x192 S3 s2", 2),
+                       vsplit<float, EPI_RESID, 128, 96, 2, 2, 2>("128x96 S2 s2", 2),
+                       vsplit<float, EPI_RESID, 256, 192, 2, 4, 2>("256x192 S2 s4", 4),
+                       vsplit<float, EPI_RESID, 256, 192, 2, 4, 2>("256x192 S2 s2", 2)}});
+    shapes.push_back({"split out K768", 768, 768, EPI_RESID, true,
+                      {v128x96<float, EPI_RESID, 3, 4>("128x96 S3 4w+4L"),
+                       v128x96<float, EPI_RESID, 3, 0>("128x96 S3 4w"),
+                       vsplit<float, EPI_RESID, 128, 96, 3, 2, 2>("128x96 S3 s1(SPL)", 1),
+                       vsplit<float, EPI_RESID, 128, 192, 3, 2, 2>("128x192 S3 s2", 2),
+                       vsplit<float, EPI_RESID, 128, 96, 2, 2, 2>("128x96 S2 s2", 2),
+                       vsplit<float, EPI_RESID, 256, 192, 2, 4, 2>("256x192 S2 s4", 4)}});
 
     // in-step emulation: the c_fc + GELU product (writes 2 x 22.5 MB) runs right before each timed launch; the
     // K = 3072 products read its output as their A operand, as c_proj does in the step
@@ -111,8 +144,14 @@ int main(int argc, char** argv)
             if (v > 0) {
                 size_t bad = 0;
                 for (size_t i = 0; i < outb; ++i) bad += ref[i] != got[i];
-                printf("%-18s %-18s bitwise vs %s: %s (%zu bytes differ)\n", sh.name, sh.vars[v].name.c_str(),
-                       sh.vars[0].name.c_str(), bad ? "DIFFERENT" : "identical", bad);
+                double num = 0, den = 0;
+                if (sh.f32) {
+                    const float* a = reinterpret_cast<const float*>(ref.data());
+                    const float* b = reinterpret_cast<const float*>(got.data());
+                    for (size_t i = 0; i < outb / 4; ++i) { num += (double)(a[i] - b[i]) * (a[i] - b[i]); den += (double)a[i] * a[i]; }
+                }
+                printf("%-18s %-18s bitwise vs %s: %s (%zu bytes differ, rel-L2 %.2e)\n", sh.name, sh.vars[v].name.c_str(),
+                       sh.vars[0].name.c_str(), bad ? "DIFFERENT" : "identical", bad, den > 0 ? sqrt(num / den) : 0.0);
             }
         }
         g.C = C1;
