@@ -369,18 +369,23 @@ def probe_steps(step, first, n, device, counts_of, cells=784, trace=True, classe
     return out, sink
 
 
-def committed_traffic(kernel_key):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes (FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE), profiles/r02_pmc_traffic.json; None when no pass covers that kernel."""
-    path = os.path.join(REPO, "profiles", "r02_pmc_traffic.json")
+PMC_FILE = os.path.join("profiles", "r03a_pmc_step.json")
+
+
+def committed_pmc(kernel_key):
+    """PMC figures of one kernel class from the committed rocprofv3 --pmc passes over THIS bench command
+    (tools/gpu_check.sh pstep -> tools/pmc_step.py, PMC_FILE): HBM bytes per launch (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE) and the MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over the busy CU cycles);
+    None when no pass covers that class."""
     try:
-        with open(path) as f:
+        with open(os.path.join(REPO, PMC_FILE)) as f:
             recs = json.load(f)
     except (OSError, ValueError):
         return None
-    for r in recs if isinstance(recs, list) else []:
+    for r in recs.get("classes", []) if isinstance(recs, dict) else []:
         if r.get("kernel") == kernel_key:
-            return r.get("traffic_bytes_per_launch")
+            return {"traffic": round(r["traffic_bytes_per_launch"]), "mfma_busy": round(r["mfma_busy_frac"], 4),
+                    "pmc_avg_us": r.get("avg_duration_us"), "source": PMC_FILE}
     return None
 
 
@@ -580,13 +585,19 @@ def main():
             out["per_rank_crops_s"] = [round(B * args.steps / t, 2) for t in per_rank]
         if kernels:
             top = next(k for k in kernels if "tflops" in k)
+            pmc = committed_pmc(top["kernel"])
             out["roofline"] = {"bound": "mfma", "achieved": top["tflops"], "peak": peak, "unit": "TFLOP/s",
-                               "frac": round(top["tflops"] / peak, 4), "traffic": committed_traffic(top["kernel"]),
+                               "frac": round(top["tflops"] / peak, 4), "traffic": (pmc or {}).get("traffic"),
+                               "mfma_busy": (pmc or {}).get("mfma_busy"), "pmc": pmc,
                                "kernel": top["kernel"], "avg_us": top["avg_us"], "flop_per_launch": top["flop_per_launch"],
                                "per_step_us": top["per_step_us"],
                                "method": "in-step kernel durations from the runtime's kernel trace (torch.profiler / "
                                          "roctracer, the rocprofv3 --kernel-trace source) over 3 steps; kernel classes "
                                          "(shape, epilogue) from 3 ebc_probe steps, matched in launch order"}
+            for k in kernels[:24]:
+                kp = committed_pmc(k["kernel"])
+                if kp:
+                    k["pmc_mfma_busy"], k["pmc_traffic"] = kp["mfma_busy"], kp["traffic"]
             out["kernels"] = kernels[:24]
             out["sinkhorn"] = sink
         if world == 1 and not args.no_cpu_baseline:
