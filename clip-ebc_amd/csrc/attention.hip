@@ -34,6 +34,15 @@ constexpr int NKT = LP / 16;    // 16-row tiles
 // NW waves per workgroup (16 queries / keys each): 16 for the ViT-B/16 sequence (one workgroup per
 // (crop, head), K/V or Q/dO staged once), 8 for short sequences
 constexpr float LOG2E = 1.4426950408889634f;
+// (crop, head) work in XCD order (xcd_remap): each XCD takes a contiguous run of crops, i.e. the token rows the
+// QKV / dO GEMM tiles of that XCD wrote and the next GEMM's tiles on it read; in the backward the dQ and dK/dV
+// workgroups of one (crop, head) are adjacent, so the second reader of K/V (Q/dO) finds them in the same L2
+#ifndef EBC_XCD_ROWS
+#define EBC_XCD_ROWS 1
+#endif
+__device__ __forceinline__ int attn_block() {
+    return EBC_XCD_ROWS ? xcd_remap(blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+}
 
 template <class E> struct AttnCfg {
     using T = typename E::T;
@@ -166,7 +175,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
     constexpr int QB = 16 * NWV * QT;
     const int nqb = (L + QB - 1) / QB;
-    const int bh = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+    const int bid = attn_block();
+    const int bh = bid / nqb, qb = bid % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
     const T* base = qkv + (size_t)b * L * D3 + h * HD;
@@ -397,7 +407,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dq_kernel(const typename E:
                                                           float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
                                                           int L_, int H, float scale)
 {
-    attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, delta, dqkv, B, L_, H, scale);
+    attn_bwd_dq_body<E, NWV, LFIX>(attn_block(), qkv, dout, out, lse, delta, dqkv, B, L_, H, scale);
 }
 
 // ------------------------------------------------------------------------------ backward dK, dV
@@ -522,10 +532,10 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
                                                            const float* __restrict__ lse, const float* __restrict__ delta,
                                                            typename E::T* __restrict__ dqkv, int B, int L_, int H, float scale)
 {
-    attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, nullptr, lse, delta, dqkv, B, L_, H, scale);
+    attn_bwd_dkv_body<E, NWV, LFIX>(attn_block(), qkv, dout, nullptr, lse, delta, dqkv, B, L_, H, scale);
 }
 
-// dQ and dK/dV workgroups in ONE grid (the first ndq blocks take the dQ role): each dK/dV workgroup forms the
+// dQ and dK/dV workgroups in ONE grid (ndq of each role): each dK/dV workgroup forms the
 // row statistic delta itself, so the two roles are independent and run side by side -- two workgroups per CU
 // at 8 waves, the 2 x B x H x ceil(L / 128) workgroups filling the CUs that one role's grid leaves idle
 template <class E, int NWV, int LFIX>
@@ -534,10 +544,13 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_fused_kernel(const typename
                                                              typename E::T* __restrict__ dqkv, int ndq, int B, int L_, int H,
                                                              float scale, int nblk, TouchList touch)
 {
-    if ((int)blockIdx.x < ndq)
-        attn_bwd_dq_body<E, NWV, LFIX>(blockIdx.x, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
+    // logical order (crop, head) -> role -> block: the 2 nblk workgroups of one (crop, head) are adjacent
+    const int id = attn_block(), bh = id / (2 * nblk), rr = id - bh * 2 * nblk;
+    const int role = rr >= nblk, blk = rr - role * nblk;
+    if (!role)
+        attn_bwd_dq_body<E, NWV, LFIX>(bh * nblk + blk, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
     else
-        attn_bwd_dkv_body<E, NWV, LFIX>(blockIdx.x - ndq, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
+        attn_bwd_dkv_body<E, NWV, LFIX>(bh * nblk + blk, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
 }
 
 int attn_waves(int L) {

@@ -73,6 +73,16 @@ __device__ __forceinline__ void ln_row(float4 (&v)[NV], const float4 (&gb)[2 * N
     }
 }
 
+// Row blocks in XCD order (xcd_remap): each XCD takes a contiguous run of rows, the same rows the GEMM tiles that
+// produce and consume them run on that XCD (gemm.hip maps its tiles the same way), so the row operands a kernel
+// reads were last written on its own XCD
+#ifndef EBC_XCD_ROWS
+#define EBC_XCD_ROWS 1
+#endif
+__device__ __forceinline__ int row_block() {
+    return EBC_XCD_ROWS ? xcd_remap(blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+}
+
 // deep-VPT insert fused into ln_1 (model.py:131-140, 161-168): rows 1..NV of every crop are read from
 // the prompt (vpt + b * bstride + (l-1) * D) instead of X, and written into X for the residual path
 struct VptIns {
@@ -88,7 +98,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
                                                      float* rstd_out, int M, VptIns vi)
 {
     constexpr int D = 256 * NV;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int r = row_block() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (r >= M) return;
     const float* xr = x + map(r) * D;
     bool ins = false;
@@ -137,7 +147,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
 {
     constexpr int D = 256 * NV;
     constexpr float inv = 1.0f / (float)D;
-    int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    int r = row_block() * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if constexpr (ZF) {
         // grid over every destination row (M = groups * gstride): rows outside the mapped groups get a zero
@@ -239,7 +249,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const float* __restrict__ pa
                                                     long vpt_bstride, float* X, int B, int L, int G, int NVPT)
 {
     constexpr int D = 256 * NV;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int r = row_block() * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (r >= B * L) return;
     const int b = r / L, s = r % L;
     float* xo = X + (size_t)r * D;
@@ -523,24 +533,33 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const TZ* __restrict__ Z,
 }
 
 // dbias[c] = sum over blocks of part[b][c] (c < CH), dscale = sum of part[b][CH], blocks in order
+// 64 columns per workgroup, 8 waves: wave w sums blocks w, w + 8, ... in eight interleaved chains (all eight loads
+// of a round in flight: one serial chain of nblk dependent L2 round trips per lane took 31 us per step at 392 blocks),
+// then the 8 wave sums are combined in wave order -- a fixed order, so the result is bit-reproducible
 template <int CH>
-__global__ __launch_bounds__(256) void head_bias_finalize_kernel(const float* __restrict__ part, int nblk, float* dbias,
+__global__ __launch_bounds__(512) void head_bias_finalize_kernel(const float* __restrict__ part, int nblk, float* dbias,
                                                                  float* dscale)
 {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c > CH) return;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;             // four interleaved chains, combined in a fixed order
-    int b = 0;
-    for (; b + 4 <= nblk; b += 4) {
-        s0 += part[(size_t)b * (CH + 1) + c];
-        s1 += part[(size_t)(b + 1) * (CH + 1) + c];
-        s2 += part[(size_t)(b + 2) * (CH + 1) + c];
-        s3 += part[(size_t)(b + 3) * (CH + 1) + c];
+    __shared__ float ws[8][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    const bool live = c <= CH;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int b = w;
+    for (; b + 56 < nblk; b += 64) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += live ? part[(size_t)(b + 8 * j) * (CH + 1) + c] : 0.f;
     }
-    for (; b < nblk; ++b) s0 += part[(size_t)b * (CH + 1) + c];
-    const float s = (s0 + s1) + (s2 + s3);
-    if (c < CH) { if (dbias) dbias[c] = s; }
-    else if (dscale) *dscale = s;
+    for (int j = 0; b < nblk; b += 8, ++j) s[j & 7] += live ? part[(size_t)b * (CH + 1) + c] : 0.f;
+    ws[w][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    __syncthreads();
+    if (w == 0 && live) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += ws[k][lane];
+        if (c < CH) { if (dbias) dbias[c] = t; }
+        else if (dscale) *dscale = t;
+    }
 }
 
 // delta[b, h, q] = sum_d dO[b*L+q, h*64+d] * O[b*L+q, h*64+d]   (FA-style backward row statistic)
@@ -822,7 +841,7 @@ static int head_bwd_t(int dtype_z, int dtype_dz, const void* Z, const float* tex
 #undef HB
     EBC_CHECK_LAUNCH();
     if (sums) {
-        hipLaunchKernelGGL(head_bias_finalize_kernel<CH>, dim3(CH / 256 + 1), dim3(256), 0, st, part, nblk, dbias, dscale);
+        hipLaunchKernelGGL(head_bias_finalize_kernel<CH>, dim3(CH / 64 + 1), dim3(512), 0, st, part, nblk, dbias, dscale);
         EBC_CHECK_LAUNCH();
     }
     return EBC_OK;
