@@ -63,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-crops", type=int, default=16, help="crops per CPU-baseline step (BASELINE.md: 16)")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps after 3 warm-up (BASELINE.md)")
     ap.add_argument("--no-probe", action="store_true", help="skip the instrumented in-step kernel timing pass")
+    ap.add_argument("--optim", default="hip", choices=["hip", "torch"],
+                    help="optimizer step: ebc_amd.optim Adam + GradScaler (HIP, 2 launches) or torch's fused Adam + "
+                         "torch.amp.GradScaler (same arithmetic; for A/B)")
     ap.add_argument("--no-trace", action="store_true",
                     help="in-step durations from the HIP events only (no torch.profiler kernel trace; for runs under rocprofv3)")
     ap.add_argument("--classes-out", default=None,
@@ -207,9 +210,14 @@ def setup(args, rank, world, local, device):
         model = wrap_ddp(model, device.index)
     loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=args.size).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
-    opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
     amp_dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.dtype]
-    scaler = torch.amp.GradScaler("cuda", enabled=args.dtype == "fp16")
+    if args.optim == "hip":
+        from ebc_amd import optim as eo            # the reference's Adam + GradScaler step (train.py:53-57)
+        opt = eo.Adam(params, lr=1e-4, weight_decay=1e-4)
+        scaler = eo.GradScaler(enabled=args.dtype == "fp16")
+    else:
+        opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4, fused=True)
+        scaler = torch.amp.GradScaler("cuda", enabled=args.dtype == "fp16")
     B = args.crops_per_gpu
     npool = min(args.pool, args.warmup + args.steps)
     pool = [make_batch(B, rank, s, device, args.size) for s in range(npool)]

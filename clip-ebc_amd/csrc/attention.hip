@@ -198,9 +198,12 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     rows_store<E, NWV>(Vs, fv);
     __syncthreads();
 
-    if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
     unsigned tsink = 0;
-    if (touch.n) touch_issue<NWV>(touch, tsink);
+    if (touch.n) touch_issue<NWV>(touch, tsink);               // every wave takes its share of the touch lines
+    if (q0 >= L) {                                             // no live query in this wave (no barrier follows)
+        if (touch.n) touch_wait(tsink);
+        return;
+    }
     // key tiles past L are skipped; only the ragged last tile is masked; the softmax scale is folded
     // into the exp2 argument: p = 2^(s*c - max*c), c = scale*log2(e)
     const int nkt = (L + 15) >> 4;
@@ -553,6 +556,176 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_fused_kernel(const typename
         attn_bwd_dkv_body<E, NWV, LFIX>(bh * nblk + blk, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
 }
 
+// One 16-wave workgroup per (crop, head) for the whole backward: K, V, Q and dO staged once into LDS (4 x 32 KiB),
+// lse and the row statistic delta (attn_delta_row, the dK/dV body's bits) for every query beside them; then each wave
+// forms dQ of its 16 queries and dK / dV of its 16 keys from LDS alone.  Per (crop, head) the operands are fetched
+// once (5 rows of 128 B per token with O), where the two-role grid fetched K/V per dQ block, Q/dO per dK/dV block
+// and dO + O again per dK/dV block for delta: 2.2x the bytes (PMC r03a: 85 MB per launch) over 1.5 waves of
+// 8-wave workgroups.  The arithmetic is the two-role kernels', operation for operation.
+// rows > 0: only dQ of queries < rows and dK / dV of keys < rows (layer 0's prompt rows).
+template <class E, int LFIX>
+__global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
+                                                           const typename E::T* __restrict__ out, const float* __restrict__ lse,
+                                                           typename E::T* __restrict__ dqkv, int B, int L_, int H, float scale,
+                                                           int rows, TouchList touch)
+{
+    constexpr int NWV = 16;
+    const int L = LFIX > 0 ? LFIX : L_;
+    using T = typename E::T;
+    using C = AttnCfg<E>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Ks = reinterpret_cast<T*>(smem);
+    T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    T* Qs = reinterpret_cast<T*>(smem + 2 * C::TILE_BYTES);
+    T* Ds = reinterpret_cast<T*>(smem + 3 * C::TILE_BYTES);
+    float* ls = reinterpret_cast<float*>(smem + 4 * C::TILE_BYTES);
+    float* dl = ls + LP;
+    const int bh = attn_block(), b = bh / H, h = bh % H;
+    const int D3 = 3 * H * HD, D = H * HD;
+    const T* base = qkv + (size_t)b * L * D3 + h * HD;
+    const T* dob = dout + (size_t)b * L * D + h * HD;
+    RowFetch<E, NWV> fk, fv, fq, fd;
+    rows_fetch<E, NWV>(fk, base + D, D3, L);
+    rows_fetch<E, NWV>(fv, base + 2 * D, D3, L);
+    rows_fetch<E, NWV>(fq, base, D3, L);
+    rows_fetch<E, NWV>(fd, dob, D, L);
+    const int tq = threadIdx.x;
+    float lsv = INFINITY, dlv = 0.f;                            // padding queries: p = 0, delta 0
+    if (tq < L) {
+        lsv = lse[((size_t)b * H + h) * L + tq] * LOG2E;       // lse pre-scaled by log2(e)
+        dlv = attn_delta_row<E>(dob + (size_t)tq * D, out + ((size_t)b * L + tq) * D + h * HD);
+    }
+    rows_store<E, NWV>(Ks, fk);
+    rows_store<E, NWV>(Vs, fv);
+    rows_store<E, NWV>(Qs, fq);
+    rows_store<E, NWV>(Ds, fd);
+    if (tq < LP) { ls[tq] = lsv; dl[tq] = dlv; }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+    const int lim = rows > 0 && rows < L ? rows : L;
+    // every wave takes its share of the weight touch (the lines are dealt over all of the grid's lanes), then a wave
+    // with no live query / key waits for its touch loads and leaves (no barrier follows)
+    unsigned tsink = 0;
+    if (touch.n) touch_issue<NWV>(touch, tsink);
+    if (16 * w >= lim) {
+        if (touch.n) touch_wait(tsink);
+        return;
+    }
+    const int nkt = (L + 15) >> 4;
+    const bool ragged = (L & 15) != 0;
+    const float c2 = scale * LOG2E;
+    {
+        // dQ of queries q0 .. q0 + 15 (the dQ body: S, dP per key tile, dS packed as the A operand of dS K)
+        const int q0 = 16 * w, qme = q0 + fr;
+        typename E::Frag qf[2], df[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            qf[ks] = lds_rowfrag<E>(Qs, qme, 32 * ks + 8 * fg);
+            df[ks] = lds_rowfrag<E>(Ds, qme, 32 * ks + 8 * fg);
+        }
+        const float lq2 = ls[qme], dq = dl[qme];
+        f32x4 dq_acc[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < NKT / 2; ++st) {
+            if (2 * st >= nkt) continue;
+            float ds[8];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int kt = 2 * st + hf;
+                if (kt >= nkt) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) ds[4 * hf + i] = 0.f;
+                    continue;
+                }
+                f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    sv = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], sv);
+                    pv = mma(lds_rowfrag<E>(Vs, 16 * kt + fr, 32 * ks + 8 * fg), df[ks], pv);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq2));
+                    if (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i >= L) p = 0.f;
+                    ds[4 * hf + i] = p * (pv[i] - dq);
+                }
+            }
+            const typename E::Frag dsf = pack8<E>(ds);
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, attn_colfrag<E>(Ks, 32 * st, 16 * dt), dq_acc[dt]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = q0 + 4 * fg + i;
+            if (q < L) {
+                T* row = dqkv + ((size_t)b * L + q) * D3 + h * HD;
+#pragma unroll
+                for (int dt = 0; dt < HD / 16; ++dt) row[16 * dt + fr] = E::from(dq_acc[dt][i] * scale);
+            }
+        }
+    }
+    {
+        // dK, dV of keys k0 .. k0 + 15 (the dK/dV body: S^T, dP^T per query tile, P and dS as A operands)
+        const int k0 = 16 * w, kme = k0 + fr;
+        typename E::Frag kf[2], vf[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            kf[ks] = lds_rowfrag<E>(Ks, kme, 32 * ks + 8 * fg);
+            vf[ks] = lds_rowfrag<E>(Vs, kme, 32 * ks + 8 * fg);
+        }
+        const int nqt = nkt;                                   // query tiles past L: lse = +inf, p = 0
+        f32x4 dk[HD / 16], dv[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll 2
+        for (int st = 0; st < NKT / 2; ++st) {
+            if (2 * st >= nqt) break;
+            float pp[8], ds[8];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int qt = 2 * st + hf;
+                f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    sv = mma(lds_rowfrag<E>(Qs, 16 * qt + fr, 32 * ks + 8 * fg), kf[ks], sv);
+                    pv = mma(lds_rowfrag<E>(Ds, 16 * qt + fr, 32 * ks + 8 * fg), vf[ks], pv);
+                }
+                const float4 l4 = *reinterpret_cast<const float4*>(ls + 16 * qt + 4 * fg);
+                const float4 d4 = *reinterpret_cast<const float4*>(dl + 16 * qt + 4 * fg);
+                const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq[i]));
+                    pp[4 * hf + i] = p;
+                    ds[4 * hf + i] = p * (pv[i] - dq[i]);
+                }
+            }
+            const typename E::Frag pf = pack8<E>(pp), dsf = pack8<E>(ds);
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) {
+                dv[dt] = mma(pf, attn_colfrag<E>(Ds, 32 * st, 16 * dt), dv[dt]);
+                dk[dt] = mma(dsf, attn_colfrag<E>(Qs, 32 * st, 16 * dt), dk[dt]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int key = k0 + 4 * fg + i;
+            if (key < L) {
+                T* row = dqkv + ((size_t)b * L + key) * D3 + h * HD;
+#pragma unroll
+                for (int dt = 0; dt < HD / 16; ++dt) {
+                    row[D + 16 * dt + fr] = E::from(dk[dt][i] * scale);
+                    row[2 * D + 16 * dt + fr] = E::from(dv[dt][i]);
+                }
+            }
+        }
+    }
+    if (touch.n) touch_wait(tsink);
+}
+
 int attn_waves(int L) {
     static const int forced = getenv("EBC_ATTN_NW") ? atoi(getenv("EBC_ATTN_NW")) : 0;
     if (forced == 8 || forced == 16) return forced;
@@ -628,9 +801,34 @@ template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, cons
     return EBC_OK;
 }
 
+template <class E, int LFIX> int attn_bwd_one(const void* qkv, const void* dout, const void* out, const float* lse,
+                                              void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
+{
+    using C = AttnCfg<E>;
+    const TouchList t = touch ? *touch : TouchList{};
+    const size_t lds = 4 * C::TILE_BYTES + 2 * LP * sizeof(float);
+    if (!ensure_lds<attn_bwd_one_kernel<E, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
+    const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 1, 0, 0, 0, B, L, H, st) : -1;
+    hipLaunchKernelGGL((attn_bwd_one_kernel<E, LFIX>), dim3(B * H), dim3(1024), lds, st, (const typename E::T*)qkv,
+                       (const typename E::T*)dout, (const typename E::T*)out, lse, (typename E::T*)dqkv, B, L, H, 0.125f,
+                       rows, t);
+    probe_stop(pi, st);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+// 16-bit backward: one workgroup per (crop, head) (EBC_ATTN_BWD_ONE, default) or the two-role grid
+#ifndef EBC_ATTN_BWD_ONE
+#define EBC_ATTN_BWD_ONE 1
+#endif
+
 template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
                                   void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
 {
+    if constexpr (E::BYTES == 2 && EBC_ATTN_BWD_ONE) {
+        return L == L_VPT32 ? attn_bwd_one<E, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch)
+                            : attn_bwd_one<E, 0>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch);
+    }
     // 16-bit: dQ and dK/dV roles in one grid; f32 (parity mode): the two kernels one after the other (no weight touch)
     if (E::BYTES == 2) {
         return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch)

@@ -54,6 +54,12 @@ class EbcAugConst(ctypes.Structure):
                 ("sigma_x", ctypes.c_float), ("sigma_y", ctypes.c_float)]
 
 
+class EbcAdamTensor(ctypes.Structure):
+    """include/ebc_hip.h EbcAdamTensor (one f32 tensor of the optimizer step)."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_long)]
+
+
 # name -> (restype, argtypes); must mirror include/ebc_hip.h
 SIGNATURES = {
     "ebc_version": (_I, []),
@@ -110,6 +116,7 @@ SIGNATURES = {
     "ebc_prep_weights_1x1": (_I, [_I, _P, _P, _P, _I, _I, _P]),
     "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, EbcAugConst, _P]),
     "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "ebc_adam_step": (_I, [_P, _I, _P, _I, _P, _I, _D, _D, _D, _D, _D, _D, _D, _I, _I, _P]),
     "ebc_probe_begin": (_I, [_I]),
     "ebc_probe_end": (_I, [_P, _I]),
     "ebc_marker": (_I, [_I, _P]),

@@ -353,6 +353,32 @@ int ebc_bn_add_relu_flat(int dtype, const void* z, const float* scale, const flo
 int ebc_prep_weights_1x1(int dtype, const float* w, void* wk, void* wt, int N, int K, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Optimizer step: Adam with the GradScaler folded in.  Replaces the reference's
+ * Adam(params, lr, weight_decay) (utils/train_utils.py:80-85) driven under GradScaler (trainer.py:123) as
+ * grad_scaler.step(optimizer); grad_scaler.update() (train.py:54-57), i.e. torch.optim.Adam (L2 weight decay,
+ * no amsgrad / maximize) + torch.amp.GradScaler's inf check, unscale, skip and scale update.
+ * tensors[n]: HOST array of f32 device tensors (param, grad, exp_avg, exp_avg_sq, numel), any n.
+ * step: DEVICE float[2], the optimizer's step count; scaler: DEVICE float[2][3] = {scale, growth_tracker,
+ *   found_inf} x 2, or NULL (no loss scaling: bf16 / fp32 training).  A call reads entry [parity] of each and
+ *   writes entry [1 - parity] (the next step count; the next scale and tracker and a cleared found_inf), so the
+ *   caller flips each parity after every call.
+ * With a scaler, any non-finite gradient skips the update (params, moments and step count unchanged) and backs
+ *   the scale off; otherwise the gradients are divided by the scale (and, write_unscaled_grad = 1, written back
+ *   unscaled as GradScaler.unscale_ leaves them) and the scale grows by growth_factor every growth_interval
+ *   applied steps.
+ * Two launches (check, update) per 32 tensors; arithmetic as torch's fused Adam (tests/test_gpu_optim.py). */
+typedef struct {
+    float* param;
+    float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    long numel;
+} EbcAdamTensor;
+int ebc_adam_step(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler, int scaler_parity,
+                  double lr, double beta1, double beta2, double eps, double weight_decay, double growth_factor,
+                  double backoff_factor, int growth_interval, int write_unscaled_grad, ebc_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
  * Measurement (bench.py): in-step kernel durations and profile windows.  Not on the reference's
  * surface; the reference has no instrumentation.
  * ebc_probe_begin(capacity): from now on every launch of the instrumented kernels is bracketed by HIP
