@@ -563,6 +563,37 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_fused_kernel(const typename
 // and dO + O again per dK/dV block for delta: 2.2x the bytes (PMC r03a: 85 MB per launch) over 1.5 waves of
 // 8-wave workgroups.  The arithmetic is the two-role kernels', operation for operation.
 // rows > 0: only dQ of queries < rows and dK / dV of keys < rows (layer 0's prompt rows).
+// Lane-constant LDS addressing of the swizzled 16-bit tiles: a row fragment (rows 16 t + fr, columns 32 ks + 8 fg) and a
+// column fragment (rows 32 st + 4 g + q (+16), columns 16 dt + 4 p) land at a per-lane byte offset (ks or dt) plus a
+// compile-time one (t, st), because the chunk swizzle depends on (row >> 1) & 7 only, which those row steps keep: every
+// fragment read is one VGPR address + an immediate (the generic attn_off form cost ~470 address VALU per wave).
+struct AttnLaneOffsets {
+    int row[2];                // ks = 0, 1
+    int col[HD / 16];          // dt = 0 .. 3
+    __device__ __forceinline__ AttnLaneOffsets() {
+        const int l = threadIdx.x & 63, fr = l & 15, fg = l >> 4;
+        const int sr = attn_swz(fr);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) row[ks] = (fr * HD + (((4 * ks + fg) ^ sr) << 3)) * 2;
+        const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3, rr = 4 * g + q, sc = attn_swz(rr);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) col[dt] = (rr * HD + ((((2 * dt + (p >> 1)) ^ sc) << 3) | (4 * (p & 1)))) * 2;
+    }
+};
+template <class E>
+__device__ __forceinline__ typename E::Frag rowfrag_at(const char* tile, int off, int t) {
+    return __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(tile + off + t * 16 * HD * 2));
+}
+template <class E>
+__device__ __forceinline__ typename E::Frag colfrag_at(const char* tile, int off, int st) {
+    const char* a = tile + off + st * 32 * HD * 2;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a + 16 * HD * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(typename E::Frag, v);
+}
+
 template <class E, int LFIX>
 __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                            const typename E::T* __restrict__ out, const float* __restrict__ lse,
@@ -615,47 +646,73 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     const int nkt = (L + 15) >> 4;
     const bool ragged = (L & 15) != 0;
     const float c2 = scale * LOG2E;
+    static_assert(E::BYTES == 2, "swizzled 16-bit tiles");
+    const AttnLaneOffsets lo;
+    // per-lane fragment base pointers of each tile (the row / column steps are immediates on these)
+    const char* Kr[2] = {reinterpret_cast<const char*>(Ks) + lo.row[0], reinterpret_cast<const char*>(Ks) + lo.row[1]};
+    const char* Vr[2] = {reinterpret_cast<const char*>(Vs) + lo.row[0], reinterpret_cast<const char*>(Vs) + lo.row[1]};
+    const char* Qr[2] = {reinterpret_cast<const char*>(Qs) + lo.row[0], reinterpret_cast<const char*>(Qs) + lo.row[1]};
+    const char* Dr[2] = {reinterpret_cast<const char*>(Ds) + lo.row[0], reinterpret_cast<const char*>(Ds) + lo.row[1]};
+    const char* Kc[HD / 16];
+    const char* Qc[HD / 16];
+    const char* Dc[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+        Kc[dt] = reinterpret_cast<const char*>(Ks) + lo.col[dt];
+        Qc[dt] = reinterpret_cast<const char*>(Qs) + lo.col[dt];
+        Dc[dt] = reinterpret_cast<const char*>(Ds) + lo.col[dt];
+    }
     {
         // dQ of queries q0 .. q0 + 15 (the dQ body: S, dP per key tile, dS packed as the A operand of dS K)
         const int q0 = 16 * w, qme = q0 + fr;
         typename E::Frag qf[2], df[2];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            qf[ks] = lds_rowfrag<E>(Qs, qme, 32 * ks + 8 * fg);
-            df[ks] = lds_rowfrag<E>(Ds, qme, 32 * ks + 8 * fg);
+            qf[ks] = rowfrag_at<E>(Qr[ks], 0, w);
+            df[ks] = rowfrag_at<E>(Dr[ks], 0, w);
         }
         const float lq2 = ls[qme], dq = dl[qme];
         f32x4 dq_acc[HD / 16];
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // software-pipelined over key-tile pairs: the S / dP products of pair st + 1 are issued before the softmax
+        // arithmetic of pair st, so each wave has independent MFMAs in flight under its VALU chain
+        f32x4 sv[2][2], pv[2][2];                              // [pair parity][tile of the pair]
+        auto sdp = [&](int kt, f32x4& s_, f32x4& p_) {
+            s_ = f32x4{0.f, 0.f, 0.f, 0.f};
+            p_ = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (kt < nkt) {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    s_ = mma(rowfrag_at<E>(Kr[ks], 0, kt), qf[ks], s_);
+                    p_ = mma(rowfrag_at<E>(Vr[ks], 0, kt), df[ks], p_);
+                }
+            }
+        };
+        sdp(0, sv[0][0], pv[0][0]);
+        sdp(1, sv[0][1], pv[0][1]);
 #pragma unroll
         for (int st = 0; st < NKT / 2; ++st) {
-            if (2 * st >= nkt) continue;
+            if (2 * st >= nkt) break;
+            const int cur = st & 1;
+            if (2 * st + 2 < nkt) {
+                sdp(2 * st + 2, sv[cur ^ 1][0], pv[cur ^ 1][0]);
+                sdp(2 * st + 3, sv[cur ^ 1][1], pv[cur ^ 1][1]);
+            }
             float ds[8];
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 const int kt = 2 * st + hf;
-                if (kt >= nkt) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) ds[4 * hf + i] = 0.f;
-                    continue;
-                }
-                f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) {
-                    sv = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], sv);
-                    pv = mma(lds_rowfrag<E>(Vs, 16 * kt + fr, 32 * ks + 8 * fg), df[ks], pv);
-                }
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq2));
-                    if (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i >= L) p = 0.f;
-                    ds[4 * hf + i] = p * (pv[i] - dq);
+                    float p = __builtin_amdgcn_exp2f(fmaf(sv[cur][hf][i], c2, -lq2));
+                    if (kt >= nkt || (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i >= L)) p = 0.f;
+                    ds[4 * hf + i] = p * (pv[cur][hf][i] - dq);
                 }
             }
             const typename E::Frag dsf = pack8<E>(ds);
 #pragma unroll
-            for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, attn_colfrag<E>(Ks, 32 * st, 16 * dt), dq_acc[dt]);
+            for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, colfrag_at<E>(Kc[dt], 0, st), dq_acc[dt]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -669,45 +726,58 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     }
     {
         // dK, dV of keys k0 .. k0 + 15 (the dK/dV body: S^T, dP^T per query tile, P and dS as A operands)
-        const int k0 = 16 * w, kme = k0 + fr;
+        const int k0 = 16 * w;
         typename E::Frag kf[2], vf[2];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            kf[ks] = lds_rowfrag<E>(Ks, kme, 32 * ks + 8 * fg);
-            vf[ks] = lds_rowfrag<E>(Vs, kme, 32 * ks + 8 * fg);
+            kf[ks] = rowfrag_at<E>(Kr[ks], 0, w);
+            vf[ks] = rowfrag_at<E>(Vr[ks], 0, w);
         }
         const int nqt = nkt;                                   // query tiles past L: lse = +inf, p = 0
         f32x4 dk[HD / 16], dv[HD / 16];
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
-#pragma unroll 2
+        f32x4 sv[2][2], pv[2][2];                              // pipelined as the dQ phase, over query-tile pairs
+        auto sdp = [&](int qt, f32x4& s_, f32x4& p_) {
+            s_ = f32x4{0.f, 0.f, 0.f, 0.f};
+            p_ = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (qt < nqt) {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    s_ = mma(rowfrag_at<E>(Qr[ks], 0, qt), kf[ks], s_);   // S^T[q][key]
+                    p_ = mma(rowfrag_at<E>(Dr[ks], 0, qt), vf[ks], p_);   // dP^T[q][key]
+                }
+            }
+        };
+        sdp(0, sv[0][0], pv[0][0]);
+        sdp(1, sv[0][1], pv[0][1]);
+#pragma unroll
         for (int st = 0; st < NKT / 2; ++st) {
             if (2 * st >= nqt) break;
+            const int cur = st & 1;
+            if (2 * st + 2 < nqt) {
+                sdp(2 * st + 2, sv[cur ^ 1][0], pv[cur ^ 1][0]);
+                sdp(2 * st + 3, sv[cur ^ 1][1], pv[cur ^ 1][1]);
+            }
             float pp[8], ds[8];
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 const int qt = 2 * st + hf;
-                f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) {
-                    sv = mma(lds_rowfrag<E>(Qs, 16 * qt + fr, 32 * ks + 8 * fg), kf[ks], sv);
-                    pv = mma(lds_rowfrag<E>(Ds, 16 * qt + fr, 32 * ks + 8 * fg), vf[ks], pv);
-                }
                 const float4 l4 = *reinterpret_cast<const float4*>(ls + 16 * qt + 4 * fg);
                 const float4 d4 = *reinterpret_cast<const float4*>(dl + 16 * qt + 4 * fg);
                 const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq[i]));
+                    const float p = __builtin_amdgcn_exp2f(fmaf(sv[cur][hf][i], c2, -lq[i]));   // lse = +inf (padding) -> 0
                     pp[4 * hf + i] = p;
-                    ds[4 * hf + i] = p * (pv[i] - dq[i]);
+                    ds[4 * hf + i] = p * (pv[cur][hf][i] - dq[i]);
                 }
             }
             const typename E::Frag pf = pack8<E>(pp), dsf = pack8<E>(ds);
 #pragma unroll
             for (int dt = 0; dt < HD / 16; ++dt) {
-                dv[dt] = mma(pf, attn_colfrag<E>(Ds, 32 * st, 16 * dt), dv[dt]);
-                dk[dt] = mma(dsf, attn_colfrag<E>(Qs, 32 * st, 16 * dt), dk[dt]);
+                dv[dt] = mma(pf, colfrag_at<E>(Dc[dt], 0, st), dv[dt]);
+                dk[dt] = mma(dsf, colfrag_at<E>(Qc[dt], 0, st), dk[dt]);
             }
         }
 #pragma unroll
