@@ -5,7 +5,7 @@
 //   RandomResizedCrop / _crop / _resize   datasets/transforms.py:9-43,133-171
 //       TF.resize(bicubic, antialias=True) = torch F.interpolate(mode="bicubic", antialias=True)
 //   RandomHorizontalFlip                  datasets/transforms.py:174-187
-//   ColorJitter (brightness/contrast/saturation; hue = 0)  datasets/transforms.py:190-201
+//   ColorJitter (brightness/contrast/saturation/hue)      datasets/transforms.py:190-201
 //   GaussianBlur(kernel_size, sigma=(0.1, 5.0))           datasets/transforms.py:217-223
 //   PepperSaltNoise                       datasets/transforms.py:242-255
 //   Normalize(ImageNet mean/std)          datasets/crowd.py:64,162
@@ -110,6 +110,44 @@ __device__ __forceinline__ int reflect(int i, int n) { return i < 0 ? -i : (i >=
 //   blur_v/blur_h: GaussianBlur (vertical taps into scratch, horizontal taps + noise + normalisation)
 struct Pix { float r, g, b; };
 
+// torchvision F.adjust_hue on one float pixel, in its float32 operations (_rgb2hsv, h = (h + f) % 1, _hsv2rgb; the
+// reference's masks select exactly one term, so the masked sums are that term); no contraction into FMAs, so each
+// operation rounds as the reference's separate tensor ops do
+__device__ __forceinline__ Pix adjust_hue(Pix px, float hf) {
+#pragma clang fp contract(off)
+    const float r = px.r, g = px.g, b = px.b;
+    const float maxc = fmaxf(fmaxf(r, g), b), minc = fminf(fminf(r, g), b);
+    const bool eqc = maxc == minc;
+    const float cr = maxc - minc;
+    const float s = cr / (eqc ? 1.0f : maxc);
+    const float crd = eqc ? 1.0f : cr;
+    const float rc = (maxc - r) / crd, gc = (maxc - g) / crd, bc = (maxc - b) / crd;
+    float h;
+    if (maxc == r) h = bc - gc;
+    else if (maxc == g) h = (2.0f + rc) - bc;
+    else h = (4.0f + gc) - rc;
+    h = fmodf(h / 6.0f + 1.0f, 1.0f);
+    // (h + hue) % 1.0: torch.remainder (fmod, then + 1 for a negative remainder)
+    float hh = fmodf(h + hf, 1.0f);
+    if (hh != 0.0f && hh < 0.0f) hh += 1.0f;
+    const float v = maxc;
+    const float fi = floorf(hh * 6.0f);
+    const float f = hh * 6.0f - fi;
+    int i = (int)fi % 6;
+    if (i < 0) i += 6;
+    const float p = fminf(fmaxf(v * (1.0f - s), 0.0f), 1.0f);
+    const float q = fminf(fmaxf(v * (1.0f - s * f), 0.0f), 1.0f);
+    const float t = fminf(fmaxf(v * (1.0f - s * (1.0f - f)), 0.0f), 1.0f);
+    switch (i) {
+        case 0: return {v, t, p};
+        case 1: return {q, v, p};
+        case 2: return {p, v, t};
+        case 3: return {p, q, v};
+        case 4: return {t, p, v};
+        default: return {v, p, q};
+    }
+}
+
 __device__ __forceinline__ Pix jitter_apply(Pix p, int ops, int from, int to, const EbcCropDesc& d, float cmean) {
     for (int slot = from; slot < to; ++slot) {
         const int op = (ops >> (3 * slot)) & 7;
@@ -121,6 +159,8 @@ __device__ __forceinline__ Pix jitter_apply(Pix p, int ops, int from, int to, co
         } else if (op == 3) {
             const float f = d.saturation, gm = (1.f - f) * gray(p.r, p.g, p.b);
             p.r = clamp01(f * p.r + gm); p.g = clamp01(f * p.g + gm); p.b = clamp01(f * p.b + gm);
+        } else if (op == 4) {
+            p = adjust_hue(p, d.hue);
         }
     }
     return p;
@@ -137,10 +177,10 @@ __device__ __forceinline__ float finish_px(float v, int c, int e, const EbcCropD
     return v;
 }
 
-__device__ __forceinline__ int n_ops(int ops) { int n = 0; while (n < 3 && ((ops >> (3 * n)) & 7)) ++n; return n; }
+__device__ __forceinline__ int n_ops(int ops) { int n = 0; while (n < 4 && ((ops >> (3 * n)) & 7)) ++n; return n; }
 __device__ __forceinline__ int contrast_slot(int ops) {
     int c = -1;
-    for (int s = 0; s < 3; ++s) if (((ops >> (3 * s)) & 7) == 2) c = s;
+    for (int s = 0; s < 4; ++s) if (((ops >> (3 * s)) & 7) == 2) c = s;
     return c;
 }
 

@@ -37,7 +37,7 @@ class EbcCropDesc(ctypes.Structure):
                 ("brightness", ctypes.c_float), ("contrast", ctypes.c_float), ("saturation", ctypes.c_float),
                 ("blur", ctypes.c_int32), ("noise", ctypes.c_int32),
                 ("saltiness", ctypes.c_float), ("spiciness", ctypes.c_float),
-                ("seed", ctypes.c_uint32), ("normalize", ctypes.c_int32)]
+                ("seed", ctypes.c_uint32), ("normalize", ctypes.c_int32), ("hue", ctypes.c_float)]
 
 
 class EbcProbeRecord(ctypes.Structure):

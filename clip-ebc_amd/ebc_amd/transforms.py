@@ -26,7 +26,8 @@ The salt-and-pepper uniforms come from one of two sources (`noise_rng`):
   * "reference": the host draws the field with the reference's own call, `torch.rand_like(image)` on the
     [3, S, S] crop (datasets/transforms.py:252), at its place in the stream, and uploads it: the whole
     stream -- every crop's window, flip, jitter factors and noise -- is the reference's draw for draw.
-`hue != 0` is unsupported (the reference's README sets hue = 0: positive values give NaN DMCount losses).
+ColorJitter's hue (torchvision adjust_hue: RGB -> HSV, hue shift, HSV -> RGB) runs per pixel on device; the trainer's
+default is hue = 0 (trainer.py:46), the reference's ColorJitter class default 0.2 (datasets/transforms.py:206).
 """
 from __future__ import annotations
 
@@ -41,7 +42,7 @@ from . import _lib
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)   # datasets/crowd.py:64
 IMAGENET_STD = (0.229, 0.224, 0.225)
-JIT_BRIGHTNESS, JIT_CONTRAST, JIT_SATURATION = 1, 2, 3
+JIT_BRIGHTNESS, JIT_CONTRAST, JIT_SATURATION, JIT_HUE = 1, 2, 3, 4
 
 
 @dataclass
@@ -112,8 +113,8 @@ class CropAugment:
         self.noise_rng = noise_rng
         if not 0 < min_scale <= max_scale:
             raise ValueError(f"scale should satisfy 0 < scale[0] <= scale[1], got {(min_scale, max_scale)}.")
-        if hue != 0.0:
-            raise NotImplementedError("ColorJitter hue != 0 is not supported (the reference runs with hue = 0)")
+        if not 0.0 <= hue <= 0.5:
+            raise ValueError(f"hue values should be between (-0.5, 0.5), got {hue}")     # torchvision _check_input
         if kernel_size % 2 == 0 or not 1 <= kernel_size <= 31:
             raise ValueError("kernel_size must be odd and <= 31")
         self.size = (input_size, input_size)
@@ -121,6 +122,7 @@ class CropAugment:
         self.bright = _check_jitter(brightness, "brightness")
         self.contr = _check_jitter(contrast, "contrast")
         self.satur = _check_jitter(saturation, "saturation")
+        self.hue = None if hue == 0.0 else (-hue, hue)
         self.saltiness, self.spiciness = saltiness, spiciness
         self.p = (jitter_prob, blur_prob, noise_prob)
         self.flip_prob = flip_prob
@@ -160,6 +162,7 @@ class CropAugment:
             b = None if self.bright is None else float(torch.empty(1).uniform_(*self.bright))
             c = None if self.contr is None else float(torch.empty(1).uniform_(*self.contr))
             s = None if self.satur is None else float(torch.empty(1).uniform_(*self.satur))
+            h = None if self.hue is None else float(torch.empty(1).uniform_(*self.hue))
             for fn in fn_idx.tolist():
                 if fn == 0 and b is not None:
                     plan.jitter.append((JIT_BRIGHTNESS, b))
@@ -167,13 +170,21 @@ class CropAugment:
                     plan.jitter.append((JIT_CONTRAST, c))
                 elif fn == 2 and s is not None:
                     plan.jitter.append((JIT_SATURATION, s))
+                elif fn == 3 and h is not None:
+                    plan.jitter.append((JIT_HUE, h))
         if torch.rand(1) < self.p[1]:
             plan.blur = True
         if torch.rand(1) < self.p[2]:
             plan.noise = True
             if self.noise_rng == "reference":
-                # rand_like of the float32 [3, out_h, out_w] crop: the same generator call as torch.rand of that shape
-                plan.noise_field = torch.rand(3, out_h, out_w)
+                # rand_like of the float32 [3, out_h, out_w] crop: the same generator call as torch.rand of that shape,
+                # in the crop's memory order -- torchvision's adjust_hue ends in an einsum that leaves the image
+                # channels-last (strides (1, 3 W, 3)), the later jitter ops keep that layout and GaussianBlur's conv
+                # makes it contiguous again, so after a hue op with no blur the uniforms land in (y, x, c) order
+                if not plan.blur and any(op == JIT_HUE for op, _ in plan.jitter):
+                    plan.noise_field = torch.rand(out_h, out_w, 3).permute(2, 0, 1).contiguous()
+                else:
+                    plan.noise_field = torch.rand(3, out_h, out_w)
             else:
                 plan.seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
         return plan, label
@@ -220,12 +231,13 @@ class CropAugment:
             if p.top + p.crop_h > d.src_h or p.left + p.crop_w > d.src_w or p.top < 0 or p.left < 0:
                 raise ValueError(f"crop window outside its image: {p}")
             d.flip = int(p.flip)
-            ops, f = 0, {JIT_BRIGHTNESS: 1.0, JIT_CONTRAST: 1.0, JIT_SATURATION: 1.0}
+            ops, f = 0, {JIT_BRIGHTNESS: 1.0, JIT_CONTRAST: 1.0, JIT_SATURATION: 1.0, JIT_HUE: 0.0}
             for slot, (op, v) in enumerate(p.jitter):
                 ops |= op << (3 * slot)
                 f[op] = v
             d.jitter_ops = ops
             d.brightness, d.contrast, d.saturation = f[JIT_BRIGHTNESS], f[JIT_CONTRAST], f[JIT_SATURATION]
+            d.hue = f[JIT_HUE]
             d.blur, d.noise = int(p.blur), int(p.noise)
             d.saltiness, d.spiciness, d.seed = self.saltiness, self.spiciness, p.seed & 0xFFFFFFFF
             d.noise_off = -1

@@ -214,7 +214,8 @@ int ebc_tile_assemble(const float* preds, float* out, int Cp, int H, int W, int 
  *                         torch F.interpolate(bicubic, antialias=True) taps; src == NULL skips it
  *   flip                  RandomHorizontalFlip (transforms.py:174-187), on the resize store
  *   jitter_ops            ColorJitter order (transforms.py:190-201 -> torchvision ColorJitter):
- *                         3 bits per slot, 1 brightness, 2 contrast, 3 saturation (hue unsupported)
+ *                         3 bits per slot (up to 4 slots), 1 brightness, 2 contrast, 3 saturation, 4 hue
+ *                         (torchvision adjust_hue: _rgb2hsv, h = (h + hue) % 1, _hsv2rgb, per pixel)
  *   blur                  GaussianBlur(kernel_size, sigma=(sx, sy)) (transforms.py:217-223), reflect pad
  *   noise                 PepperSaltNoise (transforms.py:242-255) over uniforms u[3][out_h][out_w]:
  *                         noise_off >= 0: u = noise + noise_off, a field the host drew with the reference's own
@@ -234,6 +235,7 @@ typedef struct {
     float saltiness, spiciness;
     uint32_t seed;
     int32_t normalize;
+    float hue;                           /* ColorJitter hue factor in [-0.5, 0.5] (op 4) */
 } EbcCropDesc;
 typedef struct {
     float mean[3], std[3];

@@ -7,7 +7,8 @@ that `ebc_amd.transforms.CropAugment.plan_crop` drew.  Pinning:
     `_crop` is a slice (datasets/transforms.py:9-43,133-171) -- pinned by torch itself;
   * flip, normalise: exact (transforms.py:174-187, datasets/crowd.py:64,162);
   * ColorJitter / GaussianBlur: torchvision's functional algorithms restated (adjust_brightness /
-    adjust_contrast / adjust_saturation / rgb_to_grayscale / _blend, gaussian_blur with reflect padding
+    adjust_contrast / adjust_saturation / adjust_hue with _rgb2hsv / _hsv2rgb / rgb_to_grayscale / _blend,
+    gaussian_blur with reflect padding
     and the outer-product kernel); torchvision is not importable here, so these two are
     "parity unpinned" against the library itself (the restatement follows its published code);
   * PepperSaltNoise: the reference's two `torch.where`s (transforms.py:242-255) over the plan's host-drawn
@@ -58,8 +59,60 @@ def _blend(a, b, ratio):
     return (ratio * a + (1.0 - ratio) * b).clamp(0, 1.0)
 
 
+def _rgb2hsv(img):
+    """torchvision.transforms._functional_tensor._rgb2hsv."""
+    r, g, b = img.unbind(dim=-3)
+    maxc = torch.max(img, dim=-3).values
+    minc = torch.min(img, dim=-3).values
+    eqc = maxc == minc
+    cr = maxc - minc
+    ones = torch.ones_like(maxc)
+    s = cr / torch.where(eqc, ones, maxc)
+    cr_divisor = torch.where(eqc, ones, cr)
+    rc = (maxc - r) / cr_divisor
+    gc = (maxc - g) / cr_divisor
+    bc = (maxc - b) / cr_divisor
+    hr = (maxc == r) * (bc - gc)
+    hg = ((maxc == g) & (maxc != r)) * (2.0 + rc - bc)
+    hb = ((maxc != g) & (maxc != r)) * (4.0 + gc - rc)
+    h = hr + hg + hb
+    h = torch.fmod((h / 6.0 + 1.0), 1.0)
+    return torch.stack((h, s, maxc), dim=-3)
+
+
+def _hsv2rgb(img):
+    """torchvision.transforms._functional_tensor._hsv2rgb."""
+    h, s, v = img.unbind(dim=-3)
+    i = torch.floor(h * 6.0)
+    f = (h * 6.0) - i
+    i = i.to(dtype=torch.int32)
+    p = torch.clamp((v * (1.0 - s)), 0.0, 1.0)
+    q = torch.clamp((v * (1.0 - s * f)), 0.0, 1.0)
+    t = torch.clamp((v * (1.0 - s * (1.0 - f))), 0.0, 1.0)
+    i = i % 6
+    mask = i.unsqueeze(dim=-3) == torch.arange(6, device=i.device).view(-1, 1, 1)
+    a1 = torch.stack((v, q, p, p, t, v), dim=-3)
+    a2 = torch.stack((t, v, v, q, p, p), dim=-3)
+    a3 = torch.stack((p, p, t, v, v, q), dim=-3)
+    a4 = torch.stack((a1, a2, a3), dim=-4)
+    return torch.einsum("...ijk, ...xijk -> ...xjk", mask.to(dtype=img.dtype), a4)
+
+
+def adjust_hue(img, hue_factor: float):
+    """torchvision F.adjust_hue on a float [3, H, W] image."""
+    if not (-0.5 <= hue_factor <= 0.5):
+        raise ValueError(f"hue_factor ({hue_factor}) is not in [-0.5, 0.5].")
+    hsv = _rgb2hsv(img)
+    h, s, v = hsv.unbind(dim=-3)
+    h = (h + hue_factor) % 1.0
+    return _hsv2rgb(torch.stack((h, s, v), dim=-3))
+
+
 def jitter(img, op, f):
-    """torchvision adjust_brightness (1) / adjust_contrast (2) / adjust_saturation (3) on float images."""
+    """torchvision adjust_brightness (1) / adjust_contrast (2) / adjust_saturation (3) / adjust_hue (4) on float
+    images."""
+    if op == 4:
+        return adjust_hue(img, f)
     if op == 1:
         return _blend(img, torch.zeros_like(img), f)
     if op == 2:
@@ -153,7 +206,7 @@ def _jitter_range(v):
 
 def reference_crop(image, label, size=224, scale=(1.0, 2.0), brightness=0.1, contrast=0.1, saturation=0.1,
                    kernel_size=5, saltiness=1e-3, spiciness=1e-3, probs=(0.2, 0.2, 0.5), flip_prob=0.5,
-                   sigma=(0.1, 5.0)):
+                   sigma=(0.1, 5.0), hue=0.0):
     """One crop of the train transform (utils/data_utils.py:15-24) with the reference's RNG calls, unnormalised."""
     img, label = image.float().clone(), label.float().clone()
     # RandomResizedCrop (transforms.py:147-171)
@@ -184,6 +237,7 @@ def reference_crop(image, label, size=224, scale=(1.0, 2.0), brightness=0.1, con
         b = None if rb is None else float(torch.empty(1).uniform_(rb[0], rb[1]))
         c = None if rc is None else float(torch.empty(1).uniform_(rc[0], rc[1]))
         sa = None if rs is None else float(torch.empty(1).uniform_(rs[0], rs[1]))
+        hf = None if hue == 0.0 else float(torch.empty(1).uniform_(-hue, hue))
         for fn in fn_idx.tolist():
             if fn == 0 and b is not None:
                 img = jitter(img, 1, b)
@@ -191,6 +245,8 @@ def reference_crop(image, label, size=224, scale=(1.0, 2.0), brightness=0.1, con
                 img = jitter(img, 2, c)
             elif fn == 2 and sa is not None:
                 img = jitter(img, 3, sa)
+            elif fn == 3 and hf is not None:
+                img = jitter(img, 4, hf)
     if torch.rand(1) < probs[1]:
         img = gaussian_blur(img, kernel_size, sigma[0], sigma[1])
     if torch.rand(1) < probs[2]:

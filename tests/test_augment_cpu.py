@@ -85,7 +85,8 @@ def _stream(aug_kw, shapes, n_per, seed, ref_mode):
                 o, l = ref.reference_crop(img, lab, 224, (aug_kw["min_scale"], aug_kw["max_scale"]),
                                           aug_kw["brightness"], aug_kw["contrast"], aug_kw["saturation"], 5,
                                           aug_kw["saltiness"], aug_kw["spiciness"],
-                                          (aug_kw["jitter_prob"], aug_kw["blur_prob"], aug_kw["noise_prob"]))
+                                          (aug_kw["jitter_prob"], aug_kw["blur_prob"], aug_kw["noise_prob"]),
+                                          hue=aug_kw.get("hue", 0.0))
                 outs.append(o)
                 labels.append(l)
     else:
@@ -118,3 +119,46 @@ def test_reference_rng_stream_is_the_references():
     got = ref.apply_plans(imgs, plans, (224, 224), saltiness=0.02, spiciness=0.02, normalize=False)
     for k in range(len(plans)):
         assert (got[k] - ref_imgs[k]).abs().max().item() < 1e-5, k
+
+
+def test_reference_rng_stream_with_hue():
+    """ColorJitter with hue != 0 (the reference ColorJitter's class default is 0.2, datasets/transforms.py:206):
+    get_params draws the hue factor after the saturation factor and applies it at fn_idx 3; the stream and the
+    pixels (oracle pixel path on the drawn plans) equal the restated reference transform's."""
+    from oracle import augment_ref as ref
+    kw = dict(AUG_KW, hue=0.2, jitter_prob=0.9)
+    imgs, plans, lab_a, nxt_a = _stream(kw, SHAPES, 3, 31, False)
+    _, ref_imgs, lab_b, nxt_b = _stream(kw, SHAPES, 3, 31, True)
+    assert any(op == 4 for p in plans for op, _ in p.jitter)
+    assert nxt_a == nxt_b
+    got = ref.apply_plans(imgs, plans, (224, 224), saltiness=0.02, spiciness=0.02, normalize=False)
+    for k in range(len(plans)):
+        assert (got[k] - ref_imgs[k]).abs().max().item() < 1e-5, k
+
+
+def test_hue_leaves_the_noise_field_channels_last():
+    """The reference's rand_like follows its image's layout: channels-last after adjust_hue (einsum), contiguous
+    again after GaussianBlur -- the layout CropAugment(noise_rng="reference") draws its field in."""
+    from oracle import augment_ref as ref
+    x = torch.rand(3, 24, 20)
+    y = ref.jitter(ref.adjust_hue(x, 0.1), 1, 1.05)
+    assert y.stride() == (1, 60, 3)
+    assert ref.gaussian_blur(y, 5, 1.0, 1.0).is_contiguous()
+    torch.manual_seed(2)
+    a = torch.rand_like(y)
+    torch.manual_seed(2)
+    assert torch.equal(a, torch.rand(24, 20, 3).permute(2, 0, 1))
+
+
+def test_adjust_hue_restatement_properties():
+    """torchvision adjust_hue restated (oracle): hue 0 keeps the image, a third of a turn maps the primaries
+    red -> green -> blue, and +f then -f returns the image (to f32 rounding)."""
+    from oracle import augment_ref as ref
+    g = torch.Generator().manual_seed(3)
+    img = torch.rand(3, 17, 19, generator=g)
+    assert (ref.adjust_hue(img, 0.0) - img).abs().max().item() < 1e-6
+    prim = torch.eye(3).reshape(3, 3, 1)                   # pixel k = primary k
+    out = ref.adjust_hue(prim, 1.0 / 3.0)
+    assert torch.allclose(out, torch.roll(torch.eye(3), 1, dims=0).reshape(3, 3, 1), atol=1e-6)   # [channel, pixel]
+    back = ref.adjust_hue(ref.adjust_hue(img, 0.23), -0.23)
+    assert (back - img).abs().max().item() < 1e-5

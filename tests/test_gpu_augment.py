@@ -59,19 +59,21 @@ def test_small_image_pre_resize_branch():
         assert len(l) == 0 or (float(l.min()) >= 0 and float(l.max()) <= 223)
 
 
-@pytest.mark.parametrize("probs", [(1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0), (1.0, 1.0, 1.0), (0.2, 0.2, 0.5)])
-def test_full_pipeline_matches_oracle(probs):
+@pytest.mark.parametrize("probs,hue", [((1.0, 0.0, 0.0), 0.0), ((0.0, 1.0, 0.0), 0.0), ((0.0, 0.0, 1.0), 0.0),
+                                       ((1.0, 1.0, 1.0), 0.0), ((0.2, 0.2, 0.5), 0.0), ((1.0, 0.0, 0.0), 0.3),
+                                       ((1.0, 1.0, 1.0), 0.1)])
+def test_full_pipeline_matches_oracle(probs, hue):
     from ebc_amd.transforms import CropAugment
     from oracle import augment_ref as ref
     shapes = [(480, 640), (300, 300), (768, 1024)]
-    aug = CropAugment(224, 1.0, 2.0, brightness=0.4, contrast=0.4, saturation=0.4, saltiness=0.02, spiciness=0.02,
-                      jitter_prob=probs[0], blur_prob=probs[1], noise_prob=probs[2])
+    aug = CropAugment(224, 1.0, 2.0, brightness=0.4, contrast=0.4, saturation=0.4, hue=hue, saltiness=0.02,
+                      spiciness=0.02, jitter_prob=probs[0], blur_prob=probs[1], noise_prob=probs[2])
     imgs = _images(shapes, 3)
     plans, _ = _plans(aug, shapes, 4, seed=11)
     out = aug.apply([x.cuda() for x in imgs], plans).cpu()
     exp = ref.apply_plans(imgs, plans, (224, 224), saltiness=0.02, spiciness=0.02)
     if probs[0] == 1.0:
-        assert all(len(p.jitter) == 3 for p in plans)
+        assert all(len(p.jitter) == (4 if hue else 3) for p in plans)
     if probs[2] == 1.0:                                    # the noise really fires (both salt and pepper)
         raw = aug.apply([x.cuda() for x in imgs], plans, normalize=False).cpu()
         assert (raw == 1.0).any() and (raw == 0.0).any()
@@ -106,7 +108,8 @@ def test_crowd_batch_end_to_end():
         assert torch.equal(d, ref.density_map(p, 224, 224))
 
 
-def test_reference_rng_stream_end_to_end():
+@pytest.mark.parametrize("hue", [0.0, 0.2])
+def test_reference_rng_stream_end_to_end(hue):
     """CropAugment(noise_rng="reference")(images, labels, num_crops) over a multi-crop stream with noisy crops
     in the middle equals the restated reference transform run crop after crop from the same seed
     (oracle/augment_ref.reference_crop: transforms.py:133-262 with rand_like for the noise): labels exact,
@@ -116,7 +119,7 @@ def test_reference_rng_stream_end_to_end():
     from oracle import augment_ref as ref
     shapes = [(300, 400), (200, 180), (480, 640)]
     kw = dict(min_scale=1.0, max_scale=2.0, brightness=0.4, contrast=0.4, saturation=0.4, saltiness=0.02,
-              spiciness=0.02, jitter_prob=0.5, blur_prob=0.3, noise_prob=0.5)
+              spiciness=0.02, jitter_prob=0.5, blur_prob=0.3, noise_prob=0.5, hue=hue)
     g = torch.Generator().manual_seed(17)
     imgs = [torch.rand(3, h, w, generator=g) for h, w in shapes]
     labs = [torch.rand(40, 2, generator=g) * torch.tensor([w, h], dtype=torch.float32) for h, w in shapes]
@@ -124,7 +127,7 @@ def test_reference_rng_stream_end_to_end():
     exp, exp_lab = [], []
     for img, lab in zip(imgs, labs):
         for _ in range(3):
-            o, l = ref.reference_crop(img, lab, 224, (1.0, 2.0), 0.4, 0.4, 0.4, 5, 0.02, 0.02, (0.5, 0.3, 0.5))
+            o, l = ref.reference_crop(img, lab, 224, (1.0, 2.0), 0.4, 0.4, 0.4, 5, 0.02, 0.02, (0.5, 0.3, 0.5), hue=hue)
             exp.append(ref.normalize(o))
             exp_lab.append(l)
     nxt_ref = torch.rand(1).item()
