@@ -125,6 +125,15 @@ __device__ __forceinline__ typename E::Frag gload8(const typename E::T* p, bool 
     return z;
 }
 
+// 4 consecutive output elements (8 B for 16-bit): the P.V / dS.K products are issued with the column fragment as the
+// A operand, so each lane ends with 4 consecutive head-dim columns of ONE row (its query / key fr) and stores them in
+// one instruction (16 two-byte stores per lane before)
+template <class E>
+__device__ __forceinline__ void store4(typename E::T* p, float a, float b, float c, float d) {
+    typedef typename E::T t4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<t4*>(p) = t4{E::from(a), E::from(b), E::from(c), E::from(d)};
+}
+
 template <class E>
 __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* base, int row, int col) {
     return load8<E>(base + attn_off<E>(row, col));
@@ -273,23 +282,19 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
         for (int dt = 0; dt < HD / 16; ++dt) {
             const typename E::Frag vf = attn_colfrag<E>(Vs, 32 * st, 16 * dt);
 #pragma unroll
-            for (int t = 0; t < QT; ++t) o[t][dt] = mma(pf[t], vf, o[t][dt]);
+            for (int t = 0; t < QT; ++t) o[t][dt] = mma(vf, pf[t], o[t][dt]);      // O^T tile
         }
     }
-    // o[t][dt][i] = O[q = q0 + 16 t + 4 fg + i][d = 16 dt + fr]; divide by the row sum held on lane (q - q0 - 16 t)
+    // o[t][dt][i] = O[q = q0 + 16 t + fr][d = 16 dt + 4 fg + i]; this lane holds query fr's row sum itself
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
         const float inv = 1.0f / sum[t];
+        const int q = q0 + 16 * t + fr;
+        if (q < L) {
+            T* orow = out + ((size_t)b * L + q) * D + h * HD + 4 * fg;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ql = 4 * fg + i;
-            const float iv = __shfl(inv, ql, 64);
-            const int q = q0 + 16 * t + ql;
-            if (q < L) {
-                T* orow = out + ((size_t)b * L + q) * D + h * HD;
-#pragma unroll
-                for (int dt = 0; dt < HD / 16; ++dt) orow[16 * dt + fr] = E::from(o[t][dt][i] * iv);
-            }
+            for (int dt = 0; dt < HD / 16; ++dt)
+                store4<E>(orow + 16 * dt, o[t][dt][0] * inv, o[t][dt][1] * inv, o[t][dt][2] * inv, o[t][dt][3] * inv);
         }
         const int qme = q0 + 16 * t + fr;
         if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx[t] * scale + logf(sum[t]);   // natural-log units
@@ -712,16 +717,15 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
             }
             const typename E::Frag dsf = pack8<E>(ds);
 #pragma unroll
-            for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, colfrag_at<E>(Kc[dt], 0, st), dq_acc[dt]);
+            for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(colfrag_at<E>(Kc[dt], 0, st), dsf, dq_acc[dt]);   // dQ^T
         }
+        // dq_acc[dt][i] = dQ[q0 + fr][16 dt + 4 fg + i]
+        if (qme < L) {
+            T* row = dqkv + ((size_t)b * L + qme) * D3 + h * HD + 4 * fg;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = q0 + 4 * fg + i;
-            if (q < L) {
-                T* row = dqkv + ((size_t)b * L + q) * D3 + h * HD;
-#pragma unroll
-                for (int dt = 0; dt < HD / 16; ++dt) row[16 * dt + fr] = E::from(dq_acc[dt][i] * scale);
-            }
+            for (int dt = 0; dt < HD / 16; ++dt)
+                store4<E>(row + 16 * dt, dq_acc[dt][0] * scale, dq_acc[dt][1] * scale, dq_acc[dt][2] * scale,
+                          dq_acc[dt][3] * scale);
         }
     }
     {
@@ -776,20 +780,18 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
             const typename E::Frag pf = pack8<E>(pp), dsf = pack8<E>(ds);
 #pragma unroll
             for (int dt = 0; dt < HD / 16; ++dt) {
-                dv[dt] = mma(pf, colfrag_at<E>(Dc[dt], 0, st), dv[dt]);
-                dk[dt] = mma(dsf, colfrag_at<E>(Qc[dt], 0, st), dk[dt]);
+                dv[dt] = mma(colfrag_at<E>(Dc[dt], 0, st), pf, dv[dt]);     // dV^T
+                dk[dt] = mma(colfrag_at<E>(Qc[dt], 0, st), dsf, dk[dt]);    // dK^T
             }
         }
+        // dk / dv[dt][i] = dK / dV[k0 + fr][16 dt + 4 fg + i]
+        const int key = k0 + fr;
+        if (key < L) {
+            T* row = dqkv + ((size_t)b * L + key) * D3 + h * HD + 4 * fg;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int key = k0 + 4 * fg + i;
-            if (key < L) {
-                T* row = dqkv + ((size_t)b * L + key) * D3 + h * HD;
-#pragma unroll
-                for (int dt = 0; dt < HD / 16; ++dt) {
-                    row[D + 16 * dt + fr] = E::from(dk[dt][i] * scale);
-                    row[2 * D + 16 * dt + fr] = E::from(dv[dt][i]);
-                }
+            for (int dt = 0; dt < HD / 16; ++dt) {
+                store4<E>(row + D + 16 * dt, dk[dt][0] * scale, dk[dt][1] * scale, dk[dt][2] * scale, dk[dt][3] * scale);
+                store4<E>(row + 2 * D + 16 * dt, dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
             }
         }
     }

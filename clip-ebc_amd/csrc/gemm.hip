@@ -40,11 +40,6 @@ using namespace ebc;
 #ifndef EBC_GELU_PREFETCH
 #define EBC_GELU_PREFETCH 1
 #endif
-// wave priority experiments (cdna_hip_programming.md T5): 1 = s_setprio(1) around every k-step's MFMA cluster,
-// 2 = static s_setprio(1) for the younger half of an 8-wave workgroup
-#ifndef EBC_GEMM_PRIO
-#define EBC_GEMM_PRIO 0
-#endif
 
 namespace {
 
@@ -460,9 +455,6 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             if constexpr (TN & 1) rp4[a] = *reinterpret_cast<const rp4_t*>(g.resid + ro + (TN / 2) * 32 + fq * 4);
         }
     }
-    if constexpr (EBC_GEMM_PRIO == 2 && NW >= 8) {
-        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * NW / 2) __builtin_amdgcn_s_setprio(1);
-    }
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
         if (s < nk) stage(s, s);
@@ -497,9 +489,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             __builtin_amdgcn_sched_barrier(0);
             return;
         }
-        if constexpr (EBC_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
         mma_all(ac, bc);
-        if constexpr (EBC_GEMM_PRIO == 1) __builtin_amdgcn_s_setprio(0);
         // keep the next step's fragment reads ahead of (interleaved with) this step's MFMAs and
         // stop the scheduler from sinking them next to their first use
         // (all of them within the first half of the MFMAs, two per MFMA)
