@@ -247,7 +247,7 @@ def _attn_flops(B, L, H, d=64):
 
 # kernel-name families of the probe kinds (the launch order of a family's kernels = the order of its probe records)
 _FAMILY = {"gemm": ("gemm_nt_kernel",), "dace_loss": ("dace_loss_kernel",),
-           "attn_fwd": ("attn_fwd_kernel",), "attn_bwd_dq": ("attn_bwd_dq_kernel", "attn_bwd_fused_kernel"),
+           "attn_fwd": ("attn_fwd_kernel",), "attn_bwd_dq": ("attn_bwd_dq_kernel", "attn_bwd_fused_kernel", "attn_bwd_one_kernel"),
            "attn_bwd_dkv": ("attn_bwd_dkv_kernel",), "ln_fwd": ("ln_fwd_kernel",), "ln_bwd": ("ln_bwd_kernel",)}
 
 
@@ -331,7 +331,16 @@ def probe_steps(step, first, n, device, counts_of, cells=784, trace=True, classe
             key, flops = f"dace_loss_kernel B={r.m} g={r.k}", 0.0
             dace.append(traced[ri] * 1e-3 if traced[ri] is not None else r.ms)
         elif kind.startswith("attn"):
-            key, flops = f"{kind} B={r.m} L={r.n} heads={r.k}", _attn_flops(r.m, r.n, r.k)
+            # algorithmic products (FA2 counting): forward 2 (QK^T, PV), the whole backward 5 (S, dP, dV, dK, dQ) = 2.5x;
+            # the 16-bit backward is ONE launch (probe epi 1, recorded as attn_bwd_dq), the f32 one a dQ (S, dP, dQ)
+            # and a dK/dV launch (dV, dK)
+            mult = 1.0
+            if kind == "attn_bwd_dq":
+                mult = 2.5 if r.epi == 1 else 1.5
+            elif kind == "attn_bwd_dkv":
+                mult = 1.0
+            name = "attn_bwd" if (kind == "attn_bwd_dq" and r.epi == 1) else kind
+            key, flops = f"{name} B={r.m} L={r.n} heads={r.k}", mult * _attn_flops(r.m, r.n, r.k)
         else:
             key, flops = f"{kind} rows={r.m}", 0.0
         keys.append(key)
