@@ -26,6 +26,19 @@ import torch
 from . import _lib
 
 
+def _dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense: the elements fill numel consecutive slots from data_ptr() in some dim order."""
+    if t.is_contiguous():
+        return True
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
 class Adam(torch.optim.Optimizer):
     """torch.optim.Adam(params, lr, betas, eps, weight_decay) with its step on HIP."""
 
@@ -37,18 +50,23 @@ class Adam(torch.optim.Optimizer):
         self._parity: Dict[int, int] = {}
 
     def _group_tensors(self, gi: int, group) -> List[_lib.EbcAdamTensor]:
+        """The launch's flat view: the update is elementwise, so each tensor is taken in memory order -- param,
+        gradient and moments must share one dense layout (a channels-last conv weight from MIOpen included): a
+        gradient in another layout is replaced by a copy in the parameter's (p.grad keeps its values)."""
         out = []
         for p in group["params"]:
             if p.grad is None:
                 continue
             if p.dtype != torch.float32 or p.grad.dtype != torch.float32 or not p.is_cuda:
                 raise RuntimeError("ebc_amd.optim.Adam: f32 HIP parameters and gradients only")
-            if p.grad.is_sparse or not p.grad.is_contiguous() or not p.is_contiguous():
-                raise RuntimeError("ebc_amd.optim.Adam: dense contiguous parameters and gradients only")
+            if p.grad.is_sparse or not _dense(p):
+                raise RuntimeError("ebc_amd.optim.Adam: dense (non-overlapping) parameters and gradients only")
+            if p.grad.stride() != p.stride() or not _dense(p.grad):
+                p.grad = torch.empty_like(p).copy_(p.grad)                  # the parameter's layout
             st = self.state[p]
             if not st:
-                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             out.append(_lib.EbcAdamTensor(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
                                           st["exp_avg_sq"].data_ptr(), p.numel()))
         return out

@@ -111,3 +111,25 @@ def test_adam_state_dict_roundtrip():
     opt2 = eo.Adam(_params(SHAPES[:3], 0, dev), lr=1e-3, weight_decay=1e-4)
     opt2.load_state_dict(sd)
     assert float(opt2.state_dict()["state"][0]["step"]) == 1.0
+
+
+def test_adam_channels_last_params_and_strided_grads():
+    """clip_resnet50's MIOpen stem leaves channels-last conv weights / gradients: the step runs in memory order on a
+    parameter's own dense layout and takes a gradient in another layout through a copy in the parameter's."""
+    from ebc_amd import optim as eo
+    dev = torch.device("cuda:0")
+    res = {}
+    for kind in ("ebc", "torch"):
+        g = torch.Generator().manual_seed(5)
+        p1 = torch.nn.Parameter(torch.randn(8, 3, 5, 5, generator=g).to(dev).to(memory_format=torch.channels_last))
+        p2 = torch.nn.Parameter(torch.randn(6, 4, generator=g).to(dev))
+        opt = eo.Adam([p1, p2], lr=1e-3, weight_decay=1e-4) if kind == "ebc" else \
+            torch.optim.Adam([p1, p2], lr=1e-3, weight_decay=1e-4, foreach=True)   # fused refuses mixed layouts
+        for i in range(3):
+            gg = torch.Generator().manual_seed(100 + i)
+            p1.grad = torch.randn(8, 3, 5, 5, generator=gg).to(dev)                  # contiguous: p1 is channels-last
+            p2.grad = torch.randn(4, 6, generator=gg).to(dev).t()                     # a transposed view
+            opt.step()
+        res[kind] = (p1.detach().clone(), p2.detach().clone())
+    for a, b in zip(res["ebc"], res["torch"]):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9)
