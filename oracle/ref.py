@@ -191,14 +191,26 @@ def batch_norm_train(x, w, b):
     return F.batch_norm(x, None, None, w, b, training=True, momentum=0.1, eps=1e-5)
 
 
-def decoder(p, x):
-    """BasicBlock (models/utils.py:290-303) after bilinear x2 (models/clip/model.py:195-196)."""
+def batch_norm_eval(x, w, b, rm, rv):
+    """BatchNorm2d in eval mode: the running statistics."""
+    return F.batch_norm(x, rm, rv, w, b, training=False, momentum=0.1, eps=1e-5)
+
+
+def decoder(p, x, train: bool = True):
+    """BasicBlock (models/utils.py:290-303) after bilinear x2 (models/clip/model.py:195-196); train=False: the
+    BatchNorms use their running statistics (model.eval(), eval.py / utils/eval_utils.py)."""
     x = F.interpolate(x, scale_factor=2.0, mode="bilinear")
     d = "image_decoder.0."
+
+    def bn(o, name):
+        if train:
+            return batch_norm_train(o, p[d + name + ".weight"], p[d + name + ".bias"])
+        return batch_norm_eval(o, p[d + name + ".weight"], p[d + name + ".bias"], p[d + name + ".running_mean"],
+                               p[d + name + ".running_var"])
     o = F.conv2d(x, p[d + "conv1.weight"], padding=1)
-    o = F.relu(batch_norm_train(o, p[d + "bn1.weight"], p[d + "bn1.bias"]))
+    o = F.relu(bn(o, "bn1"))
     o = F.conv2d(o, p[d + "conv2.weight"], padding=1)
-    o = batch_norm_train(o, p[d + "bn2.weight"], p[d + "bn2.bias"])
+    o = bn(o, "bn2")
     return F.relu(o + x)
 
 
@@ -226,9 +238,9 @@ def params_from_state(sd: Dict[str, np.ndarray], requires_grad: bool = True) -> 
     return out
 
 
-def forward(p, x, text_features, anchors, layers: int, deep_vpt: bool = True):
+def forward(p, x, text_features, anchors, layers: int, deep_vpt: bool = True, train: bool = True):
     feats = vit_vpt_forward(p, x, layers, deep_vpt=deep_vpt)
-    return head(p, decoder(p, feats), text_features, anchors) + (feats,)
+    return head(p, decoder(p, feats, train), text_features, anchors) + (feats,)
 
 
 # ----------------------------------------------------------------------------- clip_resnet50 (config 2)

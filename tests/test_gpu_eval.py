@@ -94,3 +94,34 @@ def test_sliding_window_qnrf_140_tiles():
         out16 = sliding_window_predict(m, img, 224, 224)
     rel = float((out16 - out32).norm() / out32.norm())
     assert rel < 2e-2, rel
+
+
+def test_sliding_window_140_tiles_vs_oracle():
+    """The config-5 eval (140 tiles of a 2048x3072 image, one forward, fp32) against an independent computation: the
+    oracle restatement (oracle/ref.py: ViT-B/16 + deep VPT, eval-mode BasicBlock decoder, head) run per tile in
+    fp32 torch on the same device with the model's own state_dict, assembled by the reference's overlap average
+    (F5 pins that assembly).  Bar: the fp32 step's (rel-L2 1e-3 of the density map, max-abs 1e-3 of its scale)."""
+    from ebc_amd.eval_utils import sliding_window_predict, tile_grid
+    from ebc_amd.model import get_model
+    from oracle import ref
+    txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
+    m = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", text_features=txt,
+                  weights_seed=0).cuda().eval()
+    H, W = 2048, 3072
+    g = np.random.Generator(np.random.PCG64(11))
+    mean = np.array([0.485, 0.456, 0.406], np.float32).reshape(1, 3, 1, 1)
+    std = np.array([0.229, 0.224, 0.225], np.float32).reshape(1, 3, 1, 1)
+    img = torch.from_numpy(((g.random((1, 3, H, W), dtype=np.float32) - mean) / std).astype(np.float32)).cuda()
+    rows, cols = tile_grid(H, W, (224, 224), (224, 224))
+    out = sliding_window_predict(m, img, 224, 224)[0].cpu()
+    p = {k: v.detach().clone().cuda().float() if v.is_floating_point() else v.detach().clone().cuda()
+         for k, v in m.state_dict().items()}
+    tiles = [img[:, :, min(i * 224, H - 224):min(i * 224, H - 224) + 224, min(j * 224, W - 224):min(j * 224, W - 224) + 224]
+             for i in range(rows) for j in range(cols)]
+    with torch.no_grad():
+        preds = torch.cat([ref.forward(p, torch.cat(tiles[k:k + 20]), txt.cuda(), ANCHORS_NWPU, 12, train=False)[1].cpu()
+                           for k in range(0, len(tiles), 20)])
+    want = _assemble(preds, H, W)
+    rel = float((out - want).norm() / want.norm())
+    assert rel < 1e-3, rel
+    assert float((out - want).abs().max()) < 1e-3 * float(want.abs().max())
