@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -165,9 +165,14 @@ def block(x, p, pre, heads=12):
 
 
 def vit_vpt_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, layers: int, num_vpt: int = 32,
-                    deep_vpt: bool = True) -> torch.Tensor:
-    """CLIP_EBC._forward_vpt (models/clip/model.py:142-189), vpt_drop=0: deep VPT (vpt_l inserted before block l) or
-    shallow (vpt_0 before block 0, then each block's output prompt rows carried into the next, model.py:174-178)."""
+                    deep_vpt: bool = True, vpt_masks: Optional[List[torch.Tensor]] = None) -> torch.Tensor:
+    """CLIP_EBC._forward_vpt (models/clip/model.py:142-189): deep VPT (vpt_l inserted before block l) or
+    shallow (vpt_0 before block 0, then each block's output prompt rows carried into the next, model.py:174-178).
+
+    vpt_masks (vpt_drop > 0, training): _prepare_vpt (model.py:131-140) expands vpt_l to [B, num_vpt, 768] and
+    passes it through its own nn.Dropout `vpt_drop_l` (model.py:76,137); vpt_masks[l] is that dropout's per-element
+    multiplier (0 or 1/(1-p), [B, num_vpt, 768]) -- applied to the expanded prompt of every layer that prepares one
+    (all layers deep; layer 0 only shallow)."""
     B, _, H, W = x.shape
     gh, gw = H // 16, W // 16
     e = "image_encoder."
@@ -175,10 +180,13 @@ def vit_vpt_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, layers: int, nu
     cls = p[e + "class_embedding"].view(1, 1, -1).expand(B, 1, 768)
     f = torch.cat([cls, f], dim=1) + p[e + "positional_embedding"]
     f = layer_norm(f, p[e + "ln_pre.weight"], p[e + "ln_pre.bias"])
-    vpt = p["vpt_0"].unsqueeze(0).expand(B, -1, -1)
+    def prepare(l):
+        v = p[f"vpt_{l}"].unsqueeze(0).expand(B, -1, -1)
+        return v * vpt_masks[l] if vpt_masks is not None else v
+    vpt = prepare(0)
     for l in range(layers):
-        if deep_vpt:
-            vpt = p[f"vpt_{l}"].unsqueeze(0).expand(B, -1, -1)
+        if deep_vpt and l > 0:
+            vpt = prepare(l)
         f = torch.cat([f[:, :1], vpt, f[:, 1:]], dim=1)
         f = block(f, p, f"{e}transformer.resblocks.{l}.")
         vpt = f[:, 1:1 + num_vpt]
@@ -238,8 +246,8 @@ def params_from_state(sd: Dict[str, np.ndarray], requires_grad: bool = True) -> 
     return out
 
 
-def forward(p, x, text_features, anchors, layers: int, deep_vpt: bool = True, train: bool = True):
-    feats = vit_vpt_forward(p, x, layers, deep_vpt=deep_vpt)
+def forward(p, x, text_features, anchors, layers: int, deep_vpt: bool = True, train: bool = True, vpt_masks=None):
+    feats = vit_vpt_forward(p, x, layers, deep_vpt=deep_vpt, vpt_masks=vpt_masks)
     return head(p, decoder(p, feats, train), text_features, anchors) + (feats,)
 
 
