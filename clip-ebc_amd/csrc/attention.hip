@@ -798,6 +798,370 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     if (touch.n) touch_wait(tsink);
 }
 
+// ------------------------------------------------------------------------------ sequences longer than LP
+// The reference interpolates the positional embedding to any grid (models/clip/_clip/image_encoder.py:183-198); the
+// trainer's default input_size 448 makes 1 + 32 + 28*28 = 817 tokens.  Past LP rows a (crop, head)'s K / V (forward,
+// dQ) or Q / dO (dK / dV) no longer fit LDS, so these kernels stream them through it in chunks of LP rows: 8-wave
+// workgroups of 128 queries (keys), the next chunk's global loads issued right after the current chunk is staged, so
+// they fly under its MFMAs.  The forward keeps a running row maximum m and sum l per query (online softmax: O and l
+// rescaled by 2^((m_old - m_new) c) when a chunk raises m); the backward kernels are the two-role pair (dQ publishes
+// delta = rowsum(dO * O), dK / dV reads it), accumulating over the chunks in registers.  Per chunk the arithmetic is
+// the LP-resident kernels'.
+constexpr int LNW = 8;                  // waves per workgroup
+constexpr int L_MAX = 16384;            // 1 + prompts + (H/16)(W/16) up to 2048x2048 inputs
+
+template <class E>
+__global__ __launch_bounds__(64 * LNW) void attn_fwd_long_kernel(const typename E::T* __restrict__ qkv,
+                                                                typename E::T* __restrict__ out, float* __restrict__ lse,
+                                                                int B, int L, int H, float scale)
+{
+    using T = typename E::T;
+    using C = AttnCfg<E>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Ks = reinterpret_cast<T*>(smem);
+    T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    constexpr int QB = 16 * LNW;
+    const int nqb = (L + QB - 1) / QB;
+    const int bid = attn_block();
+    const int bh = bid / nqb, qb = bid % nqb;
+    const int b = bh / H, h = bh % H;
+    const int D3 = 3 * H * HD, D = H * HD;
+    const T* base = qkv + (size_t)b * L * D3 + h * HD;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+    const int q0 = qb * QB + w * 16, qme = q0 + fr;           // waves past L still stage chunks (barriers)
+    RowFetch<E, LNW> fk, fv;
+    rows_fetch<E, LNW>(fk, base + D, D3, min(L, LP));
+    rows_fetch<E, LNW>(fv, base + 2 * D, D3, min(L, LP));
+    typename E::Frag qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qme < L);
+    const float c2 = scale * LOG2E;
+    float m = -INFINITY, sum = 0.f;
+    f32x4 o[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nch = (L + LP - 1) / LP;
+    for (int ch = 0; ch < nch; ++ch) {
+        const int c0 = ch * LP, Lc = min(LP, L - c0);
+        if (ch) __syncthreads();                               // every wave is done with the previous chunk
+        rows_store<E, LNW>(Ks, fk);
+        rows_store<E, LNW>(Vs, fv);
+        __syncthreads();
+        if (ch + 1 < nch) {
+            const int n1 = min(LP, L - c0 - LP);
+            rows_fetch<E, LNW>(fk, base + (size_t)(c0 + LP) * D3 + D, D3, n1);
+            rows_fetch<E, LNW>(fv, base + (size_t)(c0 + LP) * D3 + 2 * D, D3, n1);
+        }
+        // s[kt][i] = S[q = q0 + fr][key = c0 + 16 kt + 4 fg + i]; keys past the chunk's end masked
+        const int nkt = (Lc + 15) >> 4;
+        // (all products first, then the mask and the maximum: the LP kernel's order -- reading each tile's maximum
+        // right behind its MFMA pair measured wrong maxima on gfx950 for some query lanes)
+        f32x4 s[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+            s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (kt < nkt) {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) s[kt] = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], s[kt]);
+            }
+        }
+        float mc = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+            if (kt < nkt) {
+                if (kt == nkt - 1) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (16 * kt + 4 * fg + i >= Lc) s[kt][i] = -INFINITY;
+                }
+                mc = fmaxf(mc, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+            }
+        }
+        mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+        mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+        const float mn = fmaxf(m, mc);
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * c2);   // first chunk: 2^-inf = 0
+        const float mcn = mn * c2;
+        float cs = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+            if (kt < nkt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { s[kt][i] = __builtin_amdgcn_exp2f(fmaf(s[kt][i], c2, -mcn)); cs += s[kt][i]; }
+            }
+        }
+        cs += __shfl_xor(cs, 16, 64);
+        cs += __shfl_xor(cs, 32, 64);
+        sum = sum * alpha + cs;
+        m = mn;
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[dt][i] *= alpha;
+#pragma unroll
+        for (int st = 0; st < NKT / 2; ++st) {
+            if (2 * st >= nkt) continue;
+            const float pv[8] = {s[2 * st][0], s[2 * st][1], s[2 * st][2], s[2 * st][3],
+                                 s[2 * st + 1][0], s[2 * st + 1][1], s[2 * st + 1][2], s[2 * st + 1][3]};
+            const typename E::Frag pf = pack8<E>(pv);
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) o[dt] = mma(attn_colfrag<E>(Vs, 32 * st, 16 * dt), pf, o[dt]);
+        }
+    }
+    // o[dt][i] = O[q = q0 + fr][d = 16 dt + 4 fg + i]
+    if (qme < L) {
+        const float inv = 1.0f / sum;
+        T* orow = out + ((size_t)b * L + qme) * D + h * HD + 4 * fg;
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+            store4<E>(orow + 16 * dt, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+        if (fg == 0 && lse) lse[((size_t)b * H + h) * L + qme] = m * scale + logf(sum);   // natural-log units
+    }
+}
+
+template <class E>
+__global__ __launch_bounds__(64 * LNW) void attn_bwd_dq_long_kernel(const typename E::T* __restrict__ qkv,
+                                                                   const typename E::T* __restrict__ dout,
+                                                                   const typename E::T* __restrict__ out,
+                                                                   const float* __restrict__ lse, float* __restrict__ delta,
+                                                                   typename E::T* __restrict__ dqkv, int B, int L, int H,
+                                                                   float scale)
+{
+    using T = typename E::T;
+    using C = AttnCfg<E>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Ks = reinterpret_cast<T*>(smem);
+    T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    constexpr int QB = 16 * LNW;
+    const int nqb = (L + QB - 1) / QB;
+    const int bid = attn_block();
+    const int bh = bid / nqb, qb = bid % nqb;
+    const int b = bh / H, h = bh % H;
+    const int D3 = 3 * H * HD, D = H * HD;
+    const T* base = qkv + (size_t)b * L * D3 + h * HD;
+    RowFetch<E, LNW> fk, fv;
+    rows_fetch<E, LNW>(fk, base + D, D3, min(L, LP));
+    rows_fetch<E, LNW>(fv, base + 2 * D, D3, min(L, LP));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+    const int q0 = qb * QB + w * 16, qme = q0 + fr;
+    const bool qv = qme < L;
+    typename E::Frag qf[2], df[2], of[2];
+    const T* drow = dout + ((size_t)b * L + qme) * D + h * HD;
+    const T* orow = out + ((size_t)b * L + qme) * D + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        qf[ks] = gload8<E>(base + (size_t)qme * D3 + 32 * ks + 8 * fg, qv);
+        df[ks] = gload8<E>(drow + 32 * ks + 8 * fg, qv);
+        of[ks] = gload8<E>(orow + 32 * ks + 8 * fg, qv);
+    }
+    const float lq = qv ? lse[((size_t)b * H + h) * L + qme] : INFINITY;
+    float dq;                                                  // delta = rowsum(dO * O), published for dK / dV
+    {
+        float dd = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dd = fmaf((float)df[ks][j], (float)of[ks][j], dd);
+        }
+        dd += __shfl_xor(dd, 16, 64);
+        dd += __shfl_xor(dd, 32, 64);
+        dq = qv ? dd : 0.f;
+        if (fg == 0 && qv) delta[((size_t)b * H + h) * L + qme] = dd;
+    }
+    const float c2 = scale * LOG2E, lq2 = lq * LOG2E;
+    f32x4 dq_acc[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nch = (L + LP - 1) / LP;
+    for (int ch = 0; ch < nch; ++ch) {
+        const int c0 = ch * LP, Lc = min(LP, L - c0);
+        if (ch) __syncthreads();
+        rows_store<E, LNW>(Ks, fk);
+        rows_store<E, LNW>(Vs, fv);
+        __syncthreads();
+        if (ch + 1 < nch) {
+            const int n1 = min(LP, L - c0 - LP);
+            rows_fetch<E, LNW>(fk, base + (size_t)(c0 + LP) * D3 + D, D3, n1);
+            rows_fetch<E, LNW>(fv, base + (size_t)(c0 + LP) * D3 + 2 * D, D3, n1);
+        }
+        const int nkt = (Lc + 15) >> 4;
+#pragma unroll
+        for (int st = 0; st < NKT / 2; ++st) {
+            if (2 * st >= nkt) continue;
+            float ds[8];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int kt = 2 * st + hf;
+                if (kt >= nkt) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) ds[4 * hf + i] = 0.f;
+                    continue;
+                }
+                f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    sv = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], sv);
+                    pv = mma(lds_rowfrag<E>(Vs, 16 * kt + fr, 32 * ks + 8 * fg), df[ks], pv);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq2));
+                    if (kt == nkt - 1 && 16 * kt + 4 * fg + i >= Lc) p = 0.f;
+                    ds[4 * hf + i] = p * (pv[i] - dq);
+                }
+            }
+            const typename E::Frag dsf = pack8<E>(ds);
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(dsf, attn_colfrag<E>(Ks, 32 * st, 16 * dt), dq_acc[dt]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = q0 + 4 * fg + i;
+        if (q < L) {
+            T* row = dqkv + ((size_t)b * L + q) * D3 + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) row[16 * dt + fr] = E::from(dq_acc[dt][i] * scale);
+        }
+    }
+}
+
+template <class E>
+__global__ __launch_bounds__(64 * LNW) void attn_bwd_dkv_long_kernel(const typename E::T* __restrict__ qkv,
+                                                                    const typename E::T* __restrict__ dout,
+                                                                    const float* __restrict__ lse,
+                                                                    const float* __restrict__ delta,
+                                                                    typename E::T* __restrict__ dqkv, int B, int L, int H,
+                                                                    float scale)
+{
+    using T = typename E::T;
+    using C = AttnCfg<E>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Qs = reinterpret_cast<T*>(smem);
+    T* Ds = reinterpret_cast<T*>(smem + C::TILE_BYTES);
+    float* ls = reinterpret_cast<float*>(smem + 2 * C::TILE_BYTES);
+    float* dl = ls + LP;
+    constexpr int QB = 16 * LNW;
+    const int nkb = (L + QB - 1) / QB;
+    const int bid = attn_block();
+    const int bh = bid / nkb, kb = bid % nkb;
+    const int b = bh / H, h = bh % H;
+    const int D3 = 3 * H * HD, D = H * HD;
+    const T* base = qkv + (size_t)b * L * D3 + h * HD;
+    const T* dob = dout + (size_t)b * L * D + h * HD;
+    const float* lrow = lse + ((size_t)b * H + h) * L;
+    const float* drw = delta + ((size_t)b * H + h) * L;
+    RowFetch<E, LNW> fq, fd;
+    rows_fetch<E, LNW>(fq, base, D3, min(L, LP));
+    rows_fetch<E, LNW>(fd, dob, D, min(L, LP));
+    const int t = threadIdx.x;
+    // this thread's lse (pre-scaled by log2 e) and delta of chunk row t; padding rows: p = 0
+    float lsv = INFINITY, dlv = 0.f;
+    if (t < LP && t < L) { lsv = lrow[t] * LOG2E; dlv = drw[t]; }
+    const int lane = t & 63, w = t >> 6, fr = lane & 15, fg = lane >> 4;
+    const int k0 = kb * QB + w * 16, kme = k0 + fr;
+    const bool kv = kme < L;
+    typename E::Frag kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        kf[ks] = gload8<E>(base + (size_t)kme * D3 + D + 32 * ks + 8 * fg, kv);
+        vf[ks] = gload8<E>(base + (size_t)kme * D3 + 2 * D + 32 * ks + 8 * fg, kv);
+    }
+    const float c2 = scale * LOG2E;
+    f32x4 dk[HD / 16], dv[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    const int nch = (L + LP - 1) / LP;
+    for (int ch = 0; ch < nch; ++ch) {
+        const int c0 = ch * LP, Lc = min(LP, L - c0);
+        if (ch) __syncthreads();
+        rows_store<E, LNW>(Qs, fq);
+        rows_store<E, LNW>(Ds, fd);
+        if (t < LP) { ls[t] = lsv; dl[t] = dlv; }
+        __syncthreads();
+        if (ch + 1 < nch) {
+            const int c1 = c0 + LP, n1 = min(LP, L - c1);
+            rows_fetch<E, LNW>(fq, base + (size_t)c1 * D3, D3, n1);
+            rows_fetch<E, LNW>(fd, dob + (size_t)c1 * D, D, n1);
+            lsv = INFINITY; dlv = 0.f;
+            if (t < n1) { lsv = lrow[c1 + t] * LOG2E; dlv = drw[c1 + t]; }
+        }
+        const int nqt = (Lc + 15) >> 4;                        // query rows past the chunk's end: lse = +inf, p = 0
+#pragma unroll 2
+        for (int st = 0; st < NKT / 2; ++st) {
+            if (2 * st >= nqt) break;
+            float pp[8], ds[8];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int qt = 2 * st + hf;
+                f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, pv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    sv = mma(lds_rowfrag<E>(Qs, 16 * qt + fr, 32 * ks + 8 * fg), kf[ks], sv);   // S^T[q][key]
+                    pv = mma(lds_rowfrag<E>(Ds, 16 * qt + fr, 32 * ks + 8 * fg), vf[ks], pv);   // dP^T[q][key]
+                }
+                const float4 l4 = *reinterpret_cast<const float4*>(ls + 16 * qt + 4 * fg);
+                const float4 d4 = *reinterpret_cast<const float4*>(dl + 16 * qt + 4 * fg);
+                const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float p = __builtin_amdgcn_exp2f(fmaf(sv[i], c2, -lq[i]));
+                    pp[4 * hf + i] = p;
+                    ds[4 * hf + i] = p * (pv[i] - dq[i]);
+                }
+            }
+            const typename E::Frag pf = pack8<E>(pp), dsf = pack8<E>(ds);
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) {
+                dv[dt] = mma(pf, attn_colfrag<E>(Ds, 32 * st, 16 * dt), dv[dt]);
+                dk[dt] = mma(dsf, attn_colfrag<E>(Qs, 32 * st, 16 * dt), dk[dt]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int key = k0 + 4 * fg + i;
+        if (key < L) {
+            T* row = dqkv + ((size_t)b * L + key) * D3 + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < HD / 16; ++dt) {
+                row[D + 16 * dt + fr] = E::from(dk[dt][i] * scale);
+                row[2 * D + 16 * dt + fr] = E::from(dv[dt][i]);
+            }
+        }
+    }
+}
+
+template <class E> int attn_fwd_long(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st)
+{
+    using C = AttnCfg<E>;
+    const size_t lds = 2 * C::TILE_BYTES;
+    if (!ensure_lds<attn_fwd_long_kernel<E>>((int)lds, st)) return EBC_E_LAUNCH;
+    const int grid = B * H * ((L + 16 * LNW - 1) / (16 * LNW));
+    hipLaunchKernelGGL((attn_fwd_long_kernel<E>), dim3(grid), dim3(64 * LNW), lds, st, (const typename E::T*)qkv,
+                       (typename E::T*)out, lse, B, L, H, 0.125f);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
+template <class E> int attn_bwd_long(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
+                                     void* dqkv, int B, int L, int H, hipStream_t st)
+{
+    using C = AttnCfg<E>;
+    const size_t lds_dq = 2 * C::TILE_BYTES, lds_kv = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
+    if (!ensure_lds<attn_bwd_dq_long_kernel<E>>((int)lds_dq, st) || !ensure_lds<attn_bwd_dkv_long_kernel<E>>((int)lds_kv, st))
+        return EBC_E_LAUNCH;
+    const int grid = B * H * ((L + 16 * LNW - 1) / (16 * LNW));
+    hipLaunchKernelGGL((attn_bwd_dq_long_kernel<E>), dim3(grid), dim3(64 * LNW), lds_dq, st, (const typename E::T*)qkv,
+                       (const typename E::T*)dout, (const typename E::T*)out, lse, delta, (typename E::T*)dqkv, B, L, H,
+                       0.125f);
+    EBC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attn_bwd_dkv_long_kernel<E>), dim3(grid), dim3(64 * LNW), lds_kv, st, (const typename E::T*)qkv,
+                       (const typename E::T*)dout, lse, (const float*)delta, (typename E::T*)dqkv, B, L, H, 0.125f);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
 int attn_waves(int L) {
     static const int forced = getenv("EBC_ATTN_NW") ? atoi(getenv("EBC_ATTN_NW")) : 0;
     if (forced == 8 || forced == 16) return forced;
@@ -918,7 +1282,15 @@ namespace ebc {
 int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,
                   const TouchList* touch)
 {
-    if (L <= 0 || L > LP || B <= 0 || H <= 0) return EBC_E_UNSUPPORTED;
+    if (L <= 0 || L > L_MAX || B <= 0 || H <= 0) return EBC_E_UNSUPPORTED;
+    if (L > LP) {                                  // K / V streamed through LDS in chunks (no weight touch)
+        switch (dtype) {
+            case EBC_F32: return attn_fwd_long<EF32>(qkv, out, lse, B, L, H, st);
+            case EBC_F16: return attn_fwd_long<EF16>(qkv, out, lse, B, L, H, st);
+            case EBC_BF16: return attn_fwd_long<EBF16>(qkv, out, lse, B, L, H, st);
+        }
+        return EBC_E_ARG;
+    }
     switch (dtype) {
         case EBC_F32: return attn_fwd_t<EF32>(qkv, out, lse, B, L, H, st, nullptr);
         case EBC_F16: return attn_fwd_t<EF16>(qkv, out, lse, B, L, H, st, touch);
@@ -929,7 +1301,16 @@ int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int 
 int attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
                   void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
 {
-    if (L <= 0 || L > LP || B <= 0 || H <= 0 || rows < 0) return EBC_E_UNSUPPORTED;
+    if (L <= 0 || L > L_MAX || B <= 0 || H <= 0 || rows < 0) return EBC_E_UNSUPPORTED;
+    if (L > LP) {                                  // the two-role chunked pair; rows > 0 computes every row (a superset)
+        if (!delta || !lse) return EBC_E_ARG;
+        switch (dtype) {
+            case EBC_F32: return attn_bwd_long<EF32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+            case EBC_F16: return attn_bwd_long<EF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+            case EBC_BF16: return attn_bwd_long<EBF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st);
+        }
+        return EBC_E_ARG;
+    }
     switch (dtype) {
         case EBC_F32: return attn_bwd_t<EF32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows, nullptr);
         case EBC_F16: return attn_bwd_t<EF16>(qkv, dout, out, lse, delta, dqkv, B, L, H, st, rows, touch);

@@ -138,7 +138,7 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
     if (!check_weights(w) || !image || !ws || !feat || B <= 0 || H % 16 || W % 16) return EBC_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     const int NV = w->num_vpt, G = (H / 16) * (W / 16), L = 1 + NV + G, layers = w->layers;
-    if (L > 256) return EBC_E_UNSUPPORTED;
+    if (L > 16384) return EBC_E_UNSUPPORTED;                 // attention.hip L_MAX
     Layout lay = carve(ws, B, L, G, layers, dtype, training);
     if (lay.bytes > ws_bytes) return EBC_E_ARG;
     if (NV > 0 && (!vpt || !vpt[0])) return EBC_E_ARG;

@@ -712,18 +712,16 @@ def _clip_ebc(backbone: str, bins, anchor_points, reduction=None, freeze_text_en
                     vpt_drop=vpt_drop, decoder_cfg=decoder_cfg, **kw)
 
 
-MAX_TOKENS = 256      # attention.hip LP: a (crop, head)'s whole K / V (or Q / dO) stays in LDS
+MAX_TOKENS = 16384    # attention.hip L_MAX (sequences past 256 tokens stream K / V through LDS in chunks)
 
 
 def _check_tokens(h: int, w: int, num_vpt: int) -> None:
-    """The ViT sequence (CLS + prompts + (h/16)(w/16) patches) must fit the attention kernels' LDS-resident tiles."""
+    """The ViT sequence (CLS + prompts + (h/16)(w/16) patches) must fit the attention kernels' bound."""
     tokens = 1 + num_vpt + (h // PATCH) * (w // PATCH)
     if tokens > MAX_TOKENS:
         raise NotImplementedError(
             f"clip_vit_b_16 on {h}x{w} inputs with {num_vpt} prompts is a sequence of {tokens} tokens; the HIP attention "
-            f"kernels hold a whole (crop, head) sequence in LDS, up to {MAX_TOKENS} tokens (224x224 with 32 prompts: "
-            f"229).  The reference interpolates the positional embedding to any grid (image_encoder.py:183-198); use "
-            f"input_size <= 224 (sliding-window eval: window 224)")
+            f"kernels take up to {MAX_TOKENS} tokens")
 
 
 def get_model(backbone: str, input_size: int, reduction: int, bins: Optional[List[Tuple[float, float]]] = None,
