@@ -52,6 +52,12 @@ def main():
 
         def theirs():
             torch.nn.functional.linear(A, B)
+        if os.environ.get("GB_CHECK") and epi == 0:      # the forced tile's main loop against torch (fp32 sum)
+            ours()
+            ref = A.float() @ B.float().t() + bias
+            err = ((C.float() - ref).norm() / ref.norm()).item()
+            print(f"  check {name}: rel-L2 {err:.2e}")
+            assert err < 2e-3, err
         t1, t2 = timeit(ours), timeit(theirs)
         f = 2.0 * M * N * K
         tot_e += t1; tot_t += t2
