@@ -176,7 +176,10 @@ int ebc_layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int
                       const float* gamma, const float* dx_in, float* dx_out, void* dx_out_t, int M, int D,
                       ebc_stream_t stream);
 /* Multi-head attention on the packed qkv [B*L, 3*H*64] (nn.MultiheadAttention, need_weights=False,
- * blocks.py:35-37): out [B*L, H*64], lse [B,H,L]; backward writes dqkv [B*L, 3*H*64]. */
+ * blocks.py:35-37): out [B*L, H*64], lse [B,H,L]; backward writes dqkv [B*L, 3*H*64].
+ * L <= 256: K/V (and Q/dO) resident in LDS, one workgroup per (crop, head); 256 < L <= 16384 (the position
+ * embedding interpolated for larger inputs, image_encoder.py:183-198): K/V streamed through LDS in 256-row chunks
+ * with an online softmax; longer sequences return EBC_E_UNSUPPORTED. */
 int ebc_attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, ebc_stream_t stream);
 int ebc_attention_bwd(int dtype, const void* qkv, const void* dout, const void* out, const float* lse,
                       float* delta_ws, void* dqkv, int B, int L, int H, ebc_stream_t stream);
