@@ -386,7 +386,7 @@ def probe_steps(step, first, n, device, counts_of, cells=784, trace=True, classe
     return out, sink
 
 
-PMC_FILE = os.path.join("profiles", "r03n_pmc_step.json")
+PMC_FILE = os.path.join("profiles", "r03s_pmc_step.json")
 
 
 def committed_pmc(kernel_key):
