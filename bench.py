@@ -14,9 +14,11 @@ Rank 0 prints ONE JSON line:
   value        crops/s over all ranks, K timed steps between barriers + device syncs, max over ranks
   median_ms    median per-step time (HIP events on the step stream; BASELINE.md "Timing")
   roofline     the step's dominant kernel by in-step time (every instrumented launch of a few extra steps
-               bracketed by HIP events on its own stream, ebc_probe_*): algorithmic FLOP per launch /
-               its average duration vs the dense fp16 MFMA peak; `kernels` lists the top classes, and
-               `sinkhorn` the loss kernel's algorithmic bytes / duration vs HBM peak
+               bracketed by HIP events on its own stream, ebc_probe_*): algorithmic FLOP per launch (2*M*N*K,
+               K of a conv weight gradient = the B*H*W interior pixels, not its padded K loop) / its average
+               duration vs the dense fp16 MFMA peak; `kernels` lists the top classes
+  sinkhorn     the fused DACE/DMCount/Sinkhorn launch: duration, iterations, us per iteration and its measured
+               HBM bytes (committed rocprofv3 PMC pass) -- a latency-bound kernel, not an HBM-bound one
   cpu_baseline the oracle's fp32 CPU step (oracle/ref.py) on the host cores, rank 0 at N = 1 only
 The timed region is bracketed by `ebc_marker` kernels, so a rocprofv3 trace of this command can be cut
 to exactly the timed steps (tools/kstats.py --window).
@@ -111,13 +113,45 @@ def make_batch(B, rank, step, device, size=224):
             torch.from_numpy(dens).to(device), [len(p) for p in pts])
 
 
+def host_cores():
+    """(cores this process may run on, the affinity-mask size, the cgroup CPU quota in cores or None): the GPU box
+    shows the whole machine in the affinity mask (256 CPUs) but gives a job its per-GPU share through the cgroup's
+    cpu.max quota; more threads than the quota only time-slice the same share."""
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    share = None
+    if quota is None and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        share = int(os.environ["OMP_NUM_THREADS"])     # the pool's declared per-GPU CPU share (16 on the GPU box)
+    cap = quota if quota is not None else share
+    usable = affinity if cap is None else max(1, min(affinity, int(cap)))
+    return usable, affinity, quota if quota is not None else share
+
+
 def cpu_baseline(args, crops, steps):
     """The oracle (oracle/ref.py: torch-fp32 CPU restatement of the reference step, pinned by the golden
-    fixtures) on the host cores: B = 16, 3 warm-up + 5 timed steps (BASELINE.md "CPU baseline")."""
+    fixtures) on the host cores: B = 16, 3 warm-up + 5 timed steps (BASELINE.md "CPU baseline"), on as many torch
+    threads as the process may use (the affinity mask, capped by the cgroup CPU quota when there is one)."""
     from oracle import ref
     from ebc_amd import synthetic as syn
+    usable, affinity, quota = host_cores()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(usable)
     nthreads = torch.get_num_threads()
-    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     sd = syn.full_state(0, layers=12, include_text=False)
     p = ref.params_from_state(sd)
     train = [v for k, v in p.items() if v.requires_grad]
@@ -138,10 +172,14 @@ def cpu_baseline(args, crops, steps):
     for s in range(steps):
         step(3 + s)
     dt = time.perf_counter() - t0
+    torch.set_num_threads(prev_threads)
+    qtxt = (f"a per-job CPU share of {quota:g} cores (cgroup cpu.max, else OMP_NUM_THREADS)" if quota is not None
+            else "no CPU quota")
     return {"value": round(crops * steps / dt, 4), "unit": "crops/s", "cores": nthreads, "kind": "port",
+            "cores_available": {"affinity": affinity, "cpu_share": quota},
             "sample": f"{steps} timed steps (after 3 warm-up) x {crops} crops of the oracle oracle/ref.py "
                       f"(fwd + DACE/DMCount + bwd + Adam, fp32, 12 layers) on {nthreads} torch threads "
-                      f"({affinity} CPUs in the affinity mask); {dt:.1f}s"}
+                      f"({affinity} CPUs in the affinity mask, {qtxt}); {dt:.1f}s"}
 
 
 def resnet_flop_per_crop(size=448, reduction=8):
@@ -236,6 +274,7 @@ def setup(args, rank, world, local, device):
         if world > 1:
             dist.all_reduce(loss_fn.last_terms)
     step.pool = pool
+    step.loss_fn = loss_fn
     return step
 
 
@@ -276,9 +315,9 @@ def trace_steps(step, first, n):
     return [(nm, d) for _, nm, d in evs] or None
 
 
-def probe_steps(step, first, n, device, counts_of, cells=784, trace=True, classes_out=None):
+def probe_steps(step, first, n, device, trace=True, classes_out=None):
     """Per-step kernel classes (shape + epilogue of every instrumented launch, ebc_probe_*) sorted by time, and
-    the Sinkhorn roofline entry.  The classes come from n steps whose launches are bracketed by HIP events; their
+    the loss launch's average duration (us).  The classes come from n steps whose launches are bracketed by HIP events; their
     durations from n further steps traced without anything between the launches (trace_steps), matched to the
     classes by launch order per kernel family; the event durations (which include the gaps the events add) are
     kept as `event_avg_us` and are the fallback when the trace does not match."""
@@ -367,23 +406,8 @@ def probe_steps(step, first, n, device, counts_of, cells=784, trace=True, classe
             rec["flop_per_launch"] = c["flop_per_launch"]
         out.append(rec)
     out.sort(key=lambda r: -r["per_step_us"])
-    sink = None
-    if dace:
-        # 4 n M (2 I + I/10) + 3*4*M + 8 n bytes per crop, M = 784 cells (28x28; 3136 at 448),
-        # I = 100 iterations executed
-        byts = []
-        s0 = first + n if all(t is not None for t in traced) else first     # the steps the durations come from
-        for i in range(n):
-            cnt = counts_of(s0 + i)
-            byts.append(sum(4 * c * cells * (2 * 100 + 10) + 3 * 4 * cells + 8 * c for c in cnt if c > 0))
-        avg_b, avg_s = sum(byts) / len(byts), sum(dace) / len(dace) * 1e-3
-        sink = {"bound": "hbm", "achieved": round(avg_b / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(avg_b / avg_s / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": int(avg_b),
-                "avg_us": round(avg_s * 1e6, 1),
-                "kernel": f"dace_loss_kernel<{int(cells ** 0.5)}> (fused DACE + DMCount + Sinkhorn, 100 its)",
-                "note": "reference-algorithm bytes (materialised K); the kernel keeps K factored in LDS, so this "
-                        "is an equivalent rate, not HBM traffic"}
-    return out, sink
+    dace_us = sum(dace) / len(dace) * 1e3 if dace else None
+    return out, dace_us
 
 
 PMC_FILE = os.path.join("profiles", "r03s_pmc_step.json")
@@ -392,7 +416,8 @@ PMC_FILE = os.path.join("profiles", "r03s_pmc_step.json")
 def committed_pmc(kernel_key):
     """PMC figures of one kernel class from the committed rocprofv3 --pmc passes over THIS bench command
     (tools/gpu_check.sh pstep -> tools/pmc_step.py, PMC_FILE): HBM bytes per launch (FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE) and the MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over the busy CU cycles);
+    correction + WRITE_SIZE), the MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over the launch's duration x 1024
+    SIMDs at the 2.4 GHz maximum clock: a lower bound) and, when the pass has them, VALU / MFMA instructions;
     None when no pass covers that class."""
     try:
         with open(os.path.join(REPO, PMC_FILE)) as f:
@@ -401,9 +426,39 @@ def committed_pmc(kernel_key):
         return None
     for r in recs.get("classes", []) if isinstance(recs, dict) else []:
         if r.get("kernel") == kernel_key:
-            return {"traffic": round(r["traffic_bytes_per_launch"]), "mfma_busy": round(r["mfma_busy_frac"], 4),
-                    "pmc_avg_us": r.get("avg_duration_us"), "source": PMC_FILE}
+            out = {"traffic": round(r["traffic_bytes_per_launch"]) if "traffic_bytes_per_launch" in r else None,
+                   "mfma_busy": round(r["mfma_busy_frac"], 4) if "mfma_busy_frac" in r else None,
+                   "pmc_avg_us": r.get("avg_duration_us"), "source": PMC_FILE}
+            for k in ("sq_clock_ghz", "valu_per_mfma"):
+                if k in r:
+                    out[k] = round(r[k], 3)
+            return out
     return None
+
+
+def sinkhorn_entry(dace_us, iters, cells):
+    """The loss launch as what bounds it: one 1024-thread workgroup per crop (B of the 256 CUs), 100 dependent
+    Sinkhorn iterations of two LDS-resident products, a division pass and two barriers each -- latency, not bytes.
+    HBM bytes per launch from the committed PMC pass over the bench command (same key as the kernels list)."""
+    g = int(round(cells ** 0.5))
+    pmc = None
+    try:
+        with open(os.path.join(REPO, PMC_FILE)) as f:
+            for r in json.load(f).get("classes", []):
+                if r.get("kernel", "").startswith("dace_loss_kernel") and f"g={g}" in r.get("kernel", ""):
+                    pmc = r
+    except (OSError, ValueError):
+        pass
+    out = {"bound": "latency", "kernel": f"dace_loss_kernel<{g}> (fused DACE + DMCount + Sinkhorn)",
+           "avg_us": round(dace_us, 1), "iterations": iters,
+           "us_per_iteration": round(dace_us / iters, 3) if iters else None}
+    if pmc and "traffic_bytes_per_launch" in pmc:
+        b = pmc["traffic_bytes_per_launch"]
+        out.update({"hbm_bytes_per_launch": round(b), "hbm_gbs": round(b / (pmc["avg_duration_us"] * 1e-6) / 1e9, 1),
+                    "hbm_peak_gbs": HBM_PEAK_GBS,
+                    "hbm_frac": round(b / (pmc["avg_duration_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+                    "pmc_source": PMC_FILE})
+    return out
 
 
 # ----------------------------------------------------------------------------- other workloads
@@ -570,9 +625,11 @@ def main():
     kernels, sink = None, None
     if not args.no_probe:
         first = args.warmup + args.steps
-        kernels, sink = probe_steps(step, first, 3, device, lambda i: step.pool[i % len(step.pool)][3],
-                                    cells=(args.size // 8) ** 2, trace=not args.no_trace,
-                                    classes_out=args.classes_out if rank == 0 else None)
+        kernels, dace_us = probe_steps(step, first, 3, device, trace=not args.no_trace,
+                                       classes_out=args.classes_out if rank == 0 else None)
+        st_l = getattr(step.loss_fn, "last_stats", None)
+        iters = int(st_l[:, 5].max()) if st_l is not None else None      # Sinkhorn iterations run (max over crops)
+        sink = sinkhorn_entry(dace_us, iters, (args.size // 8) ** 2) if dace_us else None
     if rank == 0:
         peak = MFMA_PEAK_TF[args.dtype]
         rn = args.model == "clip_resnet50"

@@ -37,12 +37,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 // (crop, head) work in XCD order (xcd_remap): each XCD takes a contiguous run of crops, i.e. the token rows the
 // QKV / dO GEMM tiles of that XCD wrote and the next GEMM's tiles on it read; in the backward the dQ and dK/dV
 // workgroups of one (crop, head) are adjacent, so the second reader of K/V (Q/dO) finds them in the same L2
-#ifndef EBC_XCD_ROWS
-#define EBC_XCD_ROWS 1
-#endif
-__device__ __forceinline__ int attn_block() {
-    return EBC_XCD_ROWS ? xcd_remap(blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-}
+__device__ __forceinline__ int attn_block() { return xcd_remap(blockIdx.x, (int)gridDim.x); }
 
 template <class E> struct AttnCfg {
     using T = typename E::T;
@@ -141,32 +136,48 @@ __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* bas
 
 // Weight touch (kernels.h TouchList): once its operands are staged (no later global load in the wave to wait behind
 // them), every wave of the launch reads one dword of each of its share of the listed buffers' 128-B lines (64 lines
-// per instruction), so the weights of the GEMMs that follow are on-die when they start.  The loads are inline asm
-// into one register that is kept live and waited for only at the wave's end: nothing stalls on them mid-kernel (an
-// LDS-DMA form made the compiler drain them before the first LDS read that might alias).  Measured on the c_proj
+// per instruction), so the weights of the GEMMs that follow are on-die when they start.  Measured on the c_proj
 // product (tools/lab/gemm_lab.hip "mlp-seq"): 37.5 us with its weight in HBM, 28.4 us read onto the die beforehand;
 // a separate touch kernel on a side stream instead cost more in the kernels it ran beside (r03 same-box A/B).
+// The lines of all listed buffers are dealt out as one sequence over every lane of the grid, so no lane loads a
+// second line before every lane has one (the bench's sets are 8-14 MB: at most one line per lane).  The loads are
+// ordinary loads the compiler counts: a lane's first two lines land in registers that only touch_wait (an empty asm
+// at the wave's end that names them) consumes, so the compiler's own s_waitcnt insertion waits for them there and
+// nothing stalls mid-kernel; further lines (a set larger than twice the grid's lanes) load in a loop that waits for
+// each.  (r03's form -- inline-asm loads into a "+v" register -- let the register allocator reuse that register
+// while a load was still in flight: the compiler takes an asm output as written at the statement.)
+struct TouchSink { unsigned a = 0, b = 0; };
 template <int NW>
-__device__ __forceinline__ void touch_issue(const TouchList& t, unsigned& sink)
+__device__ __forceinline__ void touch_issue(const TouchList& t, TouchSink& s)
 {
-    // the lines of all listed buffers are dealt out as one sequence over every lane of the grid, so no lane loads a
-    // second line before every lane has one (per buffer from lane 0, the first waves took every buffer's first lines
-    // and their ends, i.e. the launch's, grew with the list: r03 per-class A/B, tools/ab_classes.sh)
-    const int nw = NW;
-    const size_t me = ((size_t)blockIdx.x * nw + (threadIdx.x >> 6)) * 64 + (threadIdx.x & 63);
-    const size_t tot = (size_t)gridDim.x * nw * 64;
+    const size_t me = ((size_t)blockIdx.x * NW + (threadIdx.x >> 6)) * 64 + (threadIdx.x & 63);
+    const size_t tot = (size_t)gridDim.x * NW * 64;
+    // the buffer walk is wave-uniform (the list's pointers stay scalar kernel-argument loads)
+    const unsigned* p0 = nullptr;
+    const unsigned* p1 = nullptr;
     size_t cum = 0;
     for (int b = 0; b < t.n; ++b) {
+        const size_t n = t.bytes[b] >> 7;
         const char* base = reinterpret_cast<const char*>(t.ptr[b]);
-        const size_t lines = t.bytes[b] >> 7;
-        for (size_t c = (me + tot - cum % tot) % tot; c < lines; c += tot) {
-            const char* a = base + (c << 7);
-            asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(a) : "memory");
-        }
-        cum += lines;
+        if (me >= cum && me < cum + n) p0 = reinterpret_cast<const unsigned*>(base + ((me - cum) << 7));
+        if (me + tot >= cum && me + tot < cum + n) p1 = reinterpret_cast<const unsigned*>(base + ((me + tot - cum) << 7));
+        cum += n;
     }
+    if (p0) s.a = *p0;
+    if (p1) s.b = *p1;
+    if (me + 2 * tot < cum) {                    // more lines than twice the grid's lanes: the rest, waited one by one
+        size_t c = 0;
+        for (int b = 0; b < t.n; ++b) {
+            const size_t n = t.bytes[b] >> 7;
+            const char* base = reinterpret_cast<const char*>(t.ptr[b]);
+            for (size_t gi = me + 2 * tot; gi < c + n; gi += tot)
+                if (gi >= c) s.b ^= *reinterpret_cast<const unsigned*>(base + ((gi - c) << 7));
+            c += n;
+        }
+    }
+    asm volatile("" ::: "memory");               // the loads stay here (no memory access moves across)
 }
-__device__ __forceinline__ void touch_wait(unsigned sink) { asm volatile("s_waitcnt vmcnt(0)" :: "v"(sink) : "memory"); }
+__device__ __forceinline__ void touch_wait(const TouchSink& s) { asm volatile("" :: "v"(s.a), "v"(s.b)); }
 
 // ------------------------------------------------------------------------------ forward
 // QT query tiles of 16 per wave: every K row fragment and V column fragment read from LDS feeds QT MFMAs (the LDS
@@ -207,7 +218,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     rows_store<E, NWV>(Vs, fv);
     __syncthreads();
 
-    unsigned tsink = 0;
+    TouchSink tsink;
     if (touch.n) touch_issue<NWV>(touch, tsink);               // every wave takes its share of the touch lines
     if (q0 >= L) {                                             // no live query in this wave (no barrier follows)
         if (touch.n) touch_wait(tsink);
@@ -307,7 +318,7 @@ template <class E, int NWV, int LFIX>
 __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                  const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                  float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                 int L_, int H, float scale, int nblk = 0, const TouchList* touch = nullptr)
+                                                 int L_, int H, float scale)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -316,8 +327,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* _
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
     constexpr int QB = 16 * NWV;
-    // nblk > 0: only the first nblk query blocks of every (crop, head) are launched
-    const int nqb = nblk > 0 ? nblk : (L + QB - 1) / QB;
+    const int nqb = (L + QB - 1) / QB;
     const int bh = bid / nqb, qb = bid % nqb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
@@ -360,8 +370,6 @@ __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* _
     __syncthreads();
 
     if (q0 >= L) return;                                       // no live query in this wave (no barrier follows)
-    unsigned tsink = 0;
-    if (touch && touch->n) touch_issue<NWV>(*touch, tsink);
     const int nkt = (L + 15) >> 4;
     const bool ragged = (L & 15) != 0;
     const float c2 = scale * LOG2E, lq2 = lq * LOG2E;          // p = 2^(s*c - lse*log2 e)
@@ -406,7 +414,6 @@ __device__ __forceinline__ void attn_bwd_dq_body(int bid, const typename E::T* _
             for (int dt = 0; dt < HD / 16; ++dt) row[16 * dt + fr] = E::from(dq_acc[dt][i] * scale);
         }
     }
-    if (touch && touch->n) touch_wait(tsink);
 }
 
 template <class E, int NWV, int LFIX>
@@ -442,7 +449,7 @@ template <class E, int NWV, int LFIX>
 __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                   const typename E::T* __restrict__ out, const float* __restrict__ lse,
                                                   const float* __restrict__ delta, typename E::T* __restrict__ dqkv, int B,
-                                                  int L_, int H, float scale, int nblk = 0, const TouchList* touch = nullptr)
+                                                  int L_, int H, float scale)
 {
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
@@ -453,7 +460,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
     float* ls = reinterpret_cast<float*>(smem + 2 * C::TILE_BYTES);
     float* dl = ls + LP;
     constexpr int QB = 16 * NWV;
-    const int nkb = nblk > 0 ? nblk : (L + QB - 1) / QB;     // nblk > 0: only the first nblk key blocks
+    const int nkb = (L + QB - 1) / QB;
     const int bh = bid / nkb, kb = bid % nkb;
     const int b = bh / H, h = bh % H;
     const int D3 = 3 * H * HD, D = H * HD;
@@ -483,8 +490,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
     __syncthreads();
 
     if (k0 >= L) return;                                       // no live key in this wave (no barrier follows)
-    unsigned tsink = 0;
-    if (touch && touch->n) touch_issue<NWV>(*touch, tsink);
     const int nqt = (L + 15) >> 4;                             // query tiles past L: lse = +inf, p = 0
     const float c2 = scale * LOG2E;
     f32x4 dk[HD / 16], dv[HD / 16];
@@ -532,7 +537,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* 
             }
         }
     }
-    if (touch && touch->n) touch_wait(tsink);
 }
 
 template <class E, int NWV, int LFIX>
@@ -541,24 +545,6 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_dkv_kernel(const typename E
                                                            typename E::T* __restrict__ dqkv, int B, int L_, int H, float scale)
 {
     attn_bwd_dkv_body<E, NWV, LFIX>(attn_block(), qkv, dout, nullptr, lse, delta, dqkv, B, L_, H, scale);
-}
-
-// dQ and dK/dV workgroups in ONE grid (ndq of each role): each dK/dV workgroup forms the
-// row statistic delta itself, so the two roles are independent and run side by side -- two workgroups per CU
-// at 8 waves, the 2 x B x H x ceil(L / 128) workgroups filling the CUs that one role's grid leaves idle
-template <class E, int NWV, int LFIX>
-__global__ __launch_bounds__(64 * NWV) void attn_bwd_fused_kernel(const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
-                                                             const typename E::T* __restrict__ out, const float* __restrict__ lse,
-                                                             typename E::T* __restrict__ dqkv, int ndq, int B, int L_, int H,
-                                                             float scale, int nblk, TouchList touch)
-{
-    // logical order (crop, head) -> role -> block: the 2 nblk workgroups of one (crop, head) are adjacent
-    const int id = attn_block(), bh = id / (2 * nblk), rr = id - bh * 2 * nblk;
-    const int role = rr >= nblk, blk = rr - role * nblk;
-    if (!role)
-        attn_bwd_dq_body<E, NWV, LFIX>(bh * nblk + blk, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
-    else
-        attn_bwd_dkv_body<E, NWV, LFIX>(bh * nblk + blk, qkv, dout, out, lse, nullptr, dqkv, B, L_, H, scale, nblk, &touch);
 }
 
 // One 16-wave workgroup per (crop, head) for the whole backward: K, V, Q and dO staged once into LDS (4 x 32 KiB),
@@ -642,7 +628,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     const int lim = rows > 0 && rows < L ? rows : L;
     // every wave takes its share of the weight touch (the lines are dealt over all of the grid's lanes), then a wave
     // with no live query / key waits for its touch loads and leaves (no barrier follows)
-    unsigned tsink = 0;
+    TouchSink tsink;
     if (touch.n) touch_issue<NWV>(touch, tsink);
     if (16 * w >= lim) {
         if (touch.n) touch_wait(tsink);
@@ -1162,11 +1148,7 @@ template <class E> int attn_bwd_long(const void* qkv, const void* dout, const vo
     return EBC_OK;
 }
 
-int attn_waves(int L) {
-    static const int forced = getenv("EBC_ATTN_NW") ? atoi(getenv("EBC_ATTN_NW")) : 0;
-    if (forced == 8 || forced == 16) return forced;
-    return L > 128 ? 16 : 8;
-}
+int attn_waves(int L) { return L > 128 ? 16 : 8; }
 
 // the CLIP ViT-B/16 + 32-prompt sequence (1 + 32 + 196 tokens) gets kernels compiled for it
 constexpr int L_VPT32 = 229;
@@ -1216,27 +1198,6 @@ template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
-template <class E, int NW, int LFIX> int attn_bwd_fused_nw(const void* qkv, const void* dout, const void* out, const float* lse,
-                                                           void* dqkv, int B, int L, int H, hipStream_t st, int rows = 0,
-                                                           const TouchList* touch = nullptr)
-{
-    using C = AttnCfg<E>;
-    const TouchList t = touch ? *touch : TouchList{};
-    const size_t lds = 2 * C::TILE_BYTES + 2 * LP * sizeof(float);
-    if (!ensure_lds<attn_bwd_fused_kernel<E, NW, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
-    // rows > 0: dQ of queries and dK / dV of keys < rows are wanted (the rest of dqkv is left unwritten)
-    const int nblk = rows > 0 ? std::min((rows + 16 * NW - 1) / (16 * NW), (L + 16 * NW - 1) / (16 * NW))
-                              : (L + 16 * NW - 1) / (16 * NW);
-    const int ndq = B * H * nblk;
-    const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 1, 0, 0, 0, B, L, H, st) : -1;
-    hipLaunchKernelGGL((attn_bwd_fused_kernel<E, NW, LFIX>), dim3(2 * ndq), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
-                       (const typename E::T*)dout, (const typename E::T*)out, lse, (typename E::T*)dqkv, ndq, B, L, H, 0.125f,
-                       nblk, t);
-    probe_stop(pi, st);
-    EBC_CHECK_LAUNCH();
-    return EBC_OK;
-}
-
 template <class E, int LFIX> int attn_bwd_one(const void* qkv, const void* dout, const void* out, const float* lse,
                                               void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
 {
@@ -1253,22 +1214,15 @@ template <class E, int LFIX> int attn_bwd_one(const void* qkv, const void* dout,
     return EBC_OK;
 }
 
-// 16-bit backward: one workgroup per (crop, head) (EBC_ATTN_BWD_ONE, default) or the two-role grid
-#ifndef EBC_ATTN_BWD_ONE
-#define EBC_ATTN_BWD_ONE 1
-#endif
+// 16-bit backward: one workgroup per (crop, head) (r03: the two-role grid of 8-wave dQ and dK/dV workgroups fetched
+// 2.2x the bytes and ran 388 vs 367 us per step); f32 (parity mode): the dQ and dK/dV kernels one after the other
 
 template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void* out, const float* lse, float* delta,
                                   void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
 {
-    if constexpr (E::BYTES == 2 && EBC_ATTN_BWD_ONE) {
+    if constexpr (E::BYTES == 2) {
         return L == L_VPT32 ? attn_bwd_one<E, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch)
                             : attn_bwd_one<E, 0>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch);
-    }
-    // 16-bit: dQ and dK/dV roles in one grid; f32 (parity mode): the two kernels one after the other (no weight touch)
-    if (E::BYTES == 2) {
-        return L == L_VPT32 ? attn_bwd_fused_nw<E, 8, L_VPT32>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch)
-                            : attn_bwd_fused_nw<E, 8, 0>(qkv, dout, out, lse, dqkv, B, L, H, st, rows, touch);
     }
     if (attn_waves(L) == 16)
         return L == L_VPT32 ? attn_bwd_nw<E, 16, L_VPT32>(qkv, dout, out, lse, delta, dqkv, B, L, H, st)

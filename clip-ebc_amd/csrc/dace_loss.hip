@@ -21,8 +21,6 @@
 //    (bregman_pytorch.py:117-126), stop when err <= stopThr or it > maxIter, NaN/Inf rollback
 //    to the previous (u, v) and break (:111-115), the 1e-16 epsilons, denormals kept (the build
 //    never flushes f32 denormals).  The err pass's K^T u is reused by the next iteration.
-#include <cstdio>
-#include <cstdlib>
 #include <type_traits>
 
 #include "ebc_common.h"
@@ -32,16 +30,12 @@ using namespace ebc;
 
 namespace {
 
-#ifndef EBC_DACE_NT
-#define EBC_DACE_NT 1024
-#endif
-constexpr int NT = EBC_DACE_NT;          // threads per workgroup (16 waves, 4 per SIMD)
+// threads per workgroup (16 waves, 4 per SIMD): r02 measured the 100-iteration floor at 512 and 1024 threads the same,
+// 256 threads 1.5x slower; 1024 keeps one pass over the cells / blocks per phase at G = 28
+constexpr int NT = 1024;
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
-#ifndef EBC_SORTED_W16_MIN_POINTS
-#define EBC_SORTED_W16_MIN_POINTS 257
-#endif
-constexpr int SORTED_W16_MIN_POINTS = EBC_SORTED_W16_MIN_POINTS;   // crops from this many points: 16 lanes per block
+constexpr int SORTED_W16_MIN_POINTS = 257;   // crops from this many points: 16 lanes per block (r02 probe)
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
 
 // G = the LDS grid (a multiple of 4 >= the crop's density grid g = size / reduction); cells with a row or
@@ -93,7 +87,6 @@ struct Params {
     int lds_cap_s;         // max points kept in LDS with full factor rows (bucketed path)
     int lds_cap_c;         // max points kept in LDS with compact factor rows (bucketed path)
     int total_points;      // sum of n over the crops (probe records only)
-    unsigned long long* prof;   // diagnostics (EBC_DACE_PROF=1): per crop 16 counters, else null
 };
 
 // ---------------------------------------------------------------------------------------
@@ -138,13 +131,8 @@ template <int G, typename FP, typename IP>
 __device__ void sinkhorn_crop(int n, int g, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                               const float* __restrict__ pts, FP Ey, FP Ex, FP u0, FP u1, IP win,
                               const float* b, float* v0, float* v1, float* part, float* misc,
-                              int* iters_out, int* rolled_out, float* err_last_out, unsigned long long* pr)
+                              int* iters_out, int* rolled_out, float* err_last_out)
 {
-    // diagnostics: pr[0..3] += shader cycles in K^T u / v / K v / err phases (thread 0's view)
-    unsigned long long tk = 0;
-    auto tick = [&](int k) {
-        if (pr && threadIdx.x == 0) { const unsigned long long c = clock64(); if (k >= 0) pr[k] += c - tk; tk = c; }
-    };
     constexpr int GG = G * G;
     const int t = threadIdx.x;
     const float a = 1.0f / (float)n;                         // target_prob = ones/n
@@ -220,12 +208,9 @@ __device__ void sinkhorn_crop(int n, int g, int size, int red, int norm, float r
     // K v: 8 lanes per point, lane q takes window rows q, q+8, ...; the 8 row sums meet by shuffles
     constexpr int WC = 10;
     const int q = t & 7;
-
-    tick(-1);
     while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
         if (!have_ktu) ktu_pass(u);
         have_ktu = 0;
-        tick(0);
         int* fl = flag + (it & 1);
         // v = b / (K^T u + eps)
         int bad = 0;
@@ -237,7 +222,6 @@ __device__ void sinkhorn_crop(int n, int g, int size, int red, int norm, float r
         if (bad) *fl = 1;
         __syncthreads();
         if (t == 0) flag[(it + 1) & 1] = 0;                   // nobody reads it until after the next barrier
-        tick(1);
         // u = a / (K v + eps); two points per 8-lane group per round so their LDS latencies overlap
         for (int i0 = 0; i0 < n; i0 += NT / 4) {
             float kv[2];
@@ -278,7 +262,6 @@ __device__ void sinkhorn_crop(int n, int g, int size, int red, int norm, float r
             }
         }
         __syncthreads();
-        tick(2);
         if (*fl) { rolled = 1; break; }                       // keep (u, v): rollback, :111-115
         { FP tu = u; u = un; un = tu; float* tv = v; v = vn; vn = tv; }
         if (it % eval_freq == 0) {                            // :117-126
@@ -291,7 +274,6 @@ __device__ void sinkhorn_crop(int n, int g, int size, int red, int norm, float r
             }
             err = block_sum(e, misc);
             err_last = err;
-            tick(3);
         }
         ++it;
     }
@@ -329,16 +311,11 @@ template <int G, int CW, int LPB>
 __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float reg, int max_iter, float stop_thr, int eval_freq,
                                 const float* __restrict__ pts, float* Ey, float* Ex, float* u0, float* u1, int* win,
                                 int* key, float* spts, int* bk, const float* b, float* v0, float* v1, float* part,
-                                float* misc, int* iters_out, int* rolled_out, float* err_last_out,
-                                unsigned long long* pr)
+                                float* misc, int* iters_out, int* rolled_out, float* err_last_out)
 {
     using C = Cfg<G>;
     constexpr int GG = G * G, NB1 = C::NB1, NBK = C::NBK, HALO = C::HALO;
     const int t = threadIdx.x;
-    unsigned long long tk = 0;
-    auto tick = [&](int k) {
-        if (pr && t == 0) { const unsigned long long c = clock64(); if (k >= 0) pr[k] += c - tk; tk = c; }
-    };
     int* cnt = bk;                 // [NBK] bucket sizes
     int* start = bk + NBK;         // [NBK + 1] bucket starts in the sorted order
     int* tmpwin = reinterpret_cast<int*>(u1);
@@ -541,7 +518,6 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
     constexpr int LPT = LPB == 16 ? 2 : 4;
     const int q = t & (LPT - 1);
     int to_eval = eval_freq;
-    tick(-1);
     while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
         int* fl = flag + (it & 1);
         // phase A: v = b / (K^T u + eps) (K^T u reused from the err pass)
@@ -553,7 +529,6 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
             float k0, k1;
             if (have_ktu) { k0 = part[j]; k1 = CPL == 2 ? part[j + 1] : 0.f; }
             else ktu_block(blk, R, u, k0, k1);
-            tick(1);                                          // diagnostics: "v" = K^T u gather time
             const float v0n = b[j] / (k0 + M_EPS);
             vn[j] = v0n;
             bad |= (int)!isfinite(v0n);
@@ -567,7 +542,6 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
         if (bad) *fl = 1;
         __syncthreads();
         if (t == 0) flag[(it + 1) & 1] = 0;
-        tick(0);
         // phase B: u = a / (K v + eps)
         for (int i0 = 0; i0 < n; i0 += NT / LPT) {
             const int i = i0 + t / LPT;
@@ -607,7 +581,6 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
             }
         }
         __syncthreads();
-        tick(2);
         if (*fl) { rolled = 1; break; }                       // keep (u, v): rollback, :111-115
         { float* tu = u; u = un; un = tu; float* tv = v; v = vn; vn = tv; }
         if (--to_eval == 0) {                                 // it % eval_freq == 0 (:117-126); K^T u kept
@@ -631,7 +604,6 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
             err = block_sum(e, misc);
             err_last = err;
             have_ktu = 1;
-            tick(3);
         }
         ++it;
     }
@@ -695,7 +667,6 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     float* facc = part + GG;                                  // LDS factors, compact rows (bucketed path)
 
     const int p0 = P.offsets[b], n = P.offsets[b + 1] - p0;
-    if (P.prof && t == 0) { for (int k = 0; k < 16; ++k) P.prof[b * 16 + k] = 0; P.prof[b * 16 + 6] = clock64(); P.prof[b * 16 + 5] = n; }
 
     // 1. pred density, target block sums (losses/utils.py:4-9)
     for (int j = t; j < GG; j += NT) { pd[j] = live(j) ? P.pred_density[(size_t)b * gg + gidx(j)] : 0.f; td[j] = 0.f; }
@@ -774,7 +745,6 @@ __device__ void crop_body(const Params& P, int b, float* lds)
             // Inlined copies so each sees one address space for the factors: LDS-resident crops get
             // ds_* accesses (a select between LDS and global would make them flat_*).
             auto post = [&](auto cw, auto Ey, auto Ex, auto u0, auto win, const float* cpts) {
-                if (P.prof && t == 0) P.prof[b * 16 + 8] = clock64();
                 const int WY = __float_as_int(misc[1]);
                 __syncthreads();
                 // beta = reg * log(v + eps); gradient (dm_loss.py:65-74)
@@ -802,8 +772,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                 float* Ey = base; float* Ex = Ey + (size_t)n * G; float* u0 = Ex + (size_t)n * G; float* u1 = u0 + n;
                 int* win = reinterpret_cast<int*>(u1 + n);
                 sinkhorn_crop<G>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr, P.eval_freq, pts, Ey, Ex, u0,
-                                 u1, win, bb, v0, v1, part, misc, &iters, &rolled, &err_last,
-                                 P.prof ? P.prof + b * 16 : nullptr);
+                                 u1, win, bb, v0, v1, part, misc, &iters, &rolled, &err_last);
                 post(std::integral_constant<int, G>{}, Ey, Ex, u0, win, pts);
             };
             // bucketed path in LDS: full factor rows while they fit (fewest VALU per candidate), else
@@ -820,11 +789,10 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                 const bool ok = (W16 && n >= SORTED_W16_MIN_POINTS)
                     ? sinkhorn_sorted<G, CW, W16 ? 16 : 8>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr,
                                                            P.eval_freq, pts, Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1,
-                                                           part, misc, &iters, &rolled, &err_last,
-                                                           P.prof ? P.prof + b * 16 : nullptr)
+                                                           part, misc, &iters, &rolled, &err_last)
                     : sinkhorn_sorted<G, CW, 8>(n, P.g, P.size, P.red, P.norm_cood, P.reg, P.max_iter, P.stop_thr,
                                                 P.eval_freq, pts, Ey, Ex, u0, u1, win, key, spts, bkt, bb, v0, v1, part, misc,
-                                                &iters, &rolled, &err_last, P.prof ? P.prof + b * 16 : nullptr);
+                                                &iters, &rolled, &err_last);
                 if (!ok) return false;
                 post(cw, Ey, Ex, u0, win, spts);
                 return true;
@@ -852,7 +820,6 @@ __device__ void crop_body(const Params& P, int b, float* lds)
             P.grad_density[(size_t)b * gg + gidx(j)] = P.w_count * (P.w_ot * v1[j] + wtv * gtv + gcount);
         }
     }
-    if (P.prof && t == 0) { P.prof[b * 16 + 7] = clock64(); P.prof[b * 16 + 4] = iters; }
     if (t == 0) {
         float* st = P.crop_stats + (size_t)b * 8;
         st[0] = ce; st[1] = tv_b; st[2] = cnt_b; st[3] = ot_b; st[4] = wd_b;
@@ -906,24 +873,10 @@ template <int G> int launch(const Params& P0, hipStream_t st)
     P.lds_cap_s = (int)((LDS_MAX - C::FIXED_BYTES_C) / (sizeof(float) * C::PER_POINT));
     P.lds_cap_c = (int)((LDS_MAX - C::FIXED_BYTES_C) / (sizeof(float) * C::PER_POINT_C));
     if (!ensure_lds<dace_loss_kernel<G>>(LDS_MAX, st)) return EBC_E_LAUNCH;
-    static unsigned long long* dprof = nullptr;
-    static const bool want_prof = getenv("EBC_DACE_PROF") != nullptr;
-    if (want_prof && !dprof && P.B <= 1024) (void)hipMalloc(&dprof, 1024 * 16 * sizeof(unsigned long long));
-    if (want_prof) P.prof = dprof;
     const int pi = probe_on() ? probe_start(EBC_PROBE_DACE, P.count_mode, 0, 0, 0, P.B, P.total_points, G, st) : -1;
     hipLaunchKernelGGL(dace_loss_kernel<G>, dim3(P.B), dim3(NT), LDS_MAX, st, P);
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
-    if (P.prof) {   // diagnostics only: synchronous read-back and a line per crop on stderr
-        unsigned long long h[1024 * 16];
-        (void)hipStreamSynchronize(st);
-        (void)hipMemcpy(h, P.prof, (size_t)P.B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-        for (int b = 0; b < P.B; ++b) {
-            const unsigned long long* q = h + b * 16;
-            fprintf(stderr, "dace_prof crop %d n %llu iters %llu total %llu ktu %llu v %llu kv %llu err %llu sinkhorn_end %llu\n", b,
-                    q[5], q[4], q[7] - q[6], q[0], q[1], q[2], q[3], q[8] ? q[8] - q[6] : 0ull);
-        }
-    }
     return EBC_OK;
 }
 

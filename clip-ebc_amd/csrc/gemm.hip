@@ -23,24 +23,6 @@
 
 using namespace ebc;
 
-// cache-policy bits of the operand LDS-DMA loads (experiment builds: tools/build_gemm_exp.sh)
-#ifndef EBC_GLDS_AUX
-#define EBC_GLDS_AUX 0
-#endif
-// MODE 0 epilogue of the 8-wave tiles: operand loads in this many row phases, scheduling fence per row group
-#ifndef EBC_EPI_PHASES
-#define EBC_EPI_PHASES 2
-#endif
-#ifndef EBC_EPI_SCHED
-#define EBC_EPI_SCHED 1
-#endif
-#ifndef EBC_RESID_PREFETCH
-#define EBC_RESID_PREFETCH 1
-#endif
-#ifndef EBC_GELU_PREFETCH
-#define EBC_GELU_PREFETCH 1
-#endif
-
 namespace {
 
 enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4, EPI_ADD_RELU_GRAD = 5 };
@@ -74,6 +56,9 @@ struct GemmArgs {
     int tile0 = 0, ntile = 0;
     // MODE 0 row-mapped A operand: A row of output row r = (r / a_rpg) * a_gstride + a_goff + r % a_rpg (a_rpg 0: r)
     int a_rpg = 0, a_gstride = 0, a_goff = 0;
+    // algorithmic K the probe records (0: K).  MODE 2's K loop runs over padded image rows; its algorithmic K is
+    // the interior pixel count B*H*W (bench.py counts 2*M*N*kalg FLOP)
+    int kalg = 0;
 };
 
 // Slab rows are ROWB bytes (one BK-deep K slice): 128 (BK = 64 for 16-bit, 32 for f32) or 64
@@ -116,14 +101,8 @@ template <int I, int N, class F> __device__ __forceinline__ void static_for(F&& 
     }
 }
 
-// output stores (EBC_STORE_NT: non-temporal, experiment builds)
-#ifndef EBC_STORE_NT
-#define EBC_STORE_NT 0
-#endif
-template <class V> __device__ __forceinline__ void st_out(V* p, const V& v) {
-    if constexpr (EBC_STORE_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+// output stores (default cache policy: r02 measured nt operand loads 25-35 % slower, nt stores no faster)
+template <class V> __device__ __forceinline__ void st_out(V* p, const V& v) { *p = v; }
 template <class TO> __device__ __forceinline__ void store4(TO* p, const float* v);
 template <> __device__ __forceinline__ void store4<float>(float* p, const float* v) {
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -316,13 +295,13 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         for (int i = 0; i < NLDF; ++i) {
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src[i] + (isa[i] ? oa : ob)),
-                EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, EBC_GLDS_AUX);
+                EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < NT4; ++j) {
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src[NLDF + j] + (isa[NLDF + j] ? oa : ob)),
-                EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, EBC_GLDS_AUX);
+                EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, 0);
         }
     };
     // the compute waves stage the ring themselves unless loader waves do
@@ -425,14 +404,13 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
     // 4-wave RESID tiles (one wave per SIMD: registers to spare): the f32 residual operand of the epilogue is
     // loaded before the ring fills, so its latency hides under the first tiles' instead of being paid after the
     // K loop (vmcnt retires loads in order: issued any later, a counted ring wait would block on it mid-loop)
-    constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && NW + NLW <= 8 && EBC_RESID_PREFETCH;
+    constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && NW + NLW <= 8;
     typedef float rp8_t __attribute__((ext_vector_type(8)));
     typedef float rp4_t __attribute__((ext_vector_type(4)));
     rp8_t rp8[PREF ? TM : 1][TN / 2 > 0 ? TN / 2 : 1];
     rp4_t rp4[PREF && (TN & 1) ? TM : 1];
     // 8-wave GELU' tiles (256 registers a wave): the first half of the rows' pre-activation operand the same way
-    constexpr bool PREF_G = MODE == 0 && EPI == EPI_GELU_BWD && NW >= 8 && TM % 2 == 0 && (TN & 1) == 0 &&
-                            EBC_GELU_PREFETCH;
+    constexpr bool PREF_G = MODE == 0 && EPI == EPI_GELU_BWD && NW >= 8 && TM % 2 == 0 && (TN & 1) == 0;
     typedef T gp8_t __attribute__((ext_vector_type(8)));
     gp8_t gp8[PREF_G ? TM / 2 : 1][TN / 2 > 0 ? TN / 2 : 1];
     if constexpr (PREF_G) {
@@ -627,9 +605,10 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         const int mb = m0 + wm * WM + fr;
         const int nb = n0 + wn * WN;
         // 8-wave tiles run two waves per SIMD (256 registers each): their operands are loaded for half of the
-        // row groups at a time (the whole wave tile at once spilled: GELU' 256x192, 27 registers)
+        // row groups at a time (the whole wave tile at once spilled: GELU' 256x192, 27 registers), with a scheduling
+    // fence per row group
         constexpr int PREG = PRE ? TM * (NP * (int)sizeof(pa8) + ODD * (int)sizeof(pa4)) / 4 : 0;
-        constexpr int PH = (NW >= 8 && PREG > 24 && TM % 2 == 0) ? EBC_EPI_PHASES : 1;
+        constexpr int PH = (NW >= 8 && PREG > 24 && TM % 2 == 0) ? 2 : 1;
         constexpr int TMP = TM / PH;
         float bv[NP > 0 ? NP : 1][8], bo[4];
 #pragma unroll
@@ -701,7 +680,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     if constexpr (PRE) finish(v, 4, bo, p4[a], ro + NP * 32 + fg * 4);
                     else finish(v, 4, bo, 0, ro + NP * 32 + fg * 4);
                 }
-                if constexpr (EBC_EPI_SCHED && NW >= 8) __builtin_amdgcn_sched_barrier(0);
+                if constexpr (NW >= 8) __builtin_amdgcn_sched_barrier(0);
             }
         });
     } else {
@@ -824,7 +803,7 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
     const int tiles = g.ntile ? g.ntile : ((g.M + BM - 1) / BM) * (g.N / BN) - g.tile0;
     if (tiles <= 0 || g.tile0 + tiles > ((g.M + BM - 1) / BM) * (g.N / BN)) return EBC_E_ARG;
     const int nwg = tiles * g.splits;
-    const int pi = probe_on() ? probe_start(EBC_PROBE_GEMM, EPI, BM, BN, MODE, g.M, g.N, g.K, st) : -1;
+    const int pi = probe_on() ? probe_start(EBC_PROBE_GEMM, EPI, BM, BN, MODE, g.M, g.N, g.kalg ? g.kalg : g.K, st) : -1;
     hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL, NLW>), dim3(nwg),
                        dim3(64 * (WGM * WGN + NLW)), LDS, st, g);
     probe_stop(pi, st);
@@ -832,8 +811,8 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
     return EBC_OK;
 }
 
-// Split-K launches exist for the weight gradients (MODE 2, and MODE 0 f32 stores), the conv GEMMs' tail tiles
-// (MODE 1) and forced MODE 0 store splits; every other product runs the split-free instance.
+// Split-K launches exist for the weight gradients (MODE 2, and MODE 0 f32 stores) and the conv GEMMs' tail tiles
+// (MODE 1); every other product runs the split-free instance.
 template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0, int NLW = 0>
 int launch_gemm(const GemmArgs& g, hipStream_t st)
 {
@@ -850,33 +829,21 @@ int launch_gemm(const GemmArgs& g, hipStream_t st)
 #ifndef EBC_GEMM_LAB
 namespace {
 
-// Tile configurations (EBC_GEMM_CFG=<n> forces one; EBC_GEMM_SPLITS=<s> forces the split count):
-//   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   6: 256x128/8w
-//   7: 256x256/8w   (2-stage rings of 128-B K rows)
-//   8: 128x64 S3   9: 128x128 S3   10: 256x128/8w S3   11: 192x128/8w S3   12: 128x64 S4   13: 128x96 S3
-//   14: 128x192 S3   (r02: 8-wave 128x96 S3 / S4 measured within noise of the 4-wave tile: not built)
+// Tile configurations the heuristics below pick (the other shapes r01-r03 swept -- 256x128, 192x128, 128x192, 3- and
+// 4-stage rings, 64-B K-row rings -- measured slower at every shape of this path; tools/lab/gemm_lab.hip times any):
+//   1: 128x128/4w   2: 128x64/4w   3: 256x192/8w   4: 192x192/8w   5: 128x96/4w   7: 256x256/8w
+//   (2-stage rings of 128-B K rows)   13: 128x96 S3 (conv weight gradients)
 //   15: 128x96 S3 + 4 loader waves   16: 128x96 S4 + 4 loader waves   (r03, tools/lab/gemm_lab.hip)
-//   20: 256x256/8w  21: 256x128/8w  22: 128x256/8w  24: 128x128/4w   (4-stage rings
-//       of 64-B K rows, 16-bit only; r01: a 256x192 4-stage ring measured 10-15 % slower than
-//       cfg 3's 2-stage 128-B ring on the decoder convs and the MLP, so no such config is built)
 // The L2 -> LDS fill rate per CU (~70 GB/s, MI355X_MICROARCH.md "gather into LDS") bounds a tile at
 // BM*BN/(BM+BN) flop per byte, so the default takes the 256-wide tiles and splits K where the
 // output has too few tiles to fill the 256 CUs.
 struct TileCfg { int id, bm, bn; };
-constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {6, 256, 128},
-                            {7, 256, 256}, {8, 128, 64}, {9, 128, 128}, {10, 256, 128}, {11, 192, 128}, {12, 128, 64},
-                            {13, 128, 96}, {14, 128, 192}, {15, 128, 96}, {16, 128, 96}, {20, 256, 256}, {21, 256, 128},
-                            {22, 128, 256}, {24, 128, 128}};
+constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {7, 256, 256},
+                            {13, 128, 96}, {15, 128, 96}, {16, 128, 96}};
 const TileCfg* find_cfg(int id) {
     for (const TileCfg& c : CFGS) if (c.id == id) return &c;
     return nullptr;
 }
-int env_int(const char* name) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : 0;
-}
-int forced_cfg() { static const int v = env_int("EBC_GEMM_CFG"); return v; }
-int forced_splits() { static const int v = env_int("EBC_GEMM_SPLITS"); return v; }
 
 constexpr int NUM_CU = 256;
 // split-K workspace: [0, GEMM_CNT_BYTES) per-tile arrival counters (zero on entry, left zero),
@@ -888,9 +855,8 @@ inline long ntiles(int M, int N, int bm, int bn) { return (long)((M + bm - 1) / 
 int pick_cfg(int M, int N, int K, bool wide) {
     // Measured on MI355X at the ViT-B/16 shapes (M = 16 x 229; tools/gemm_bench.py, r01): the
     // 128x64 two-stage tile is best or within noise everywhere except the QKV projection (192x192,
-    // 8 waves) and the long-K N = 768 products (128x96, 3 stages).  The 256-wide / split-K tiles
-    // (cfg 20-24) are correct but slower here (their epilogue and split fix-up dominate) and are
-    // kept for forced runs only.
+    // 8 waves) and the long-K N = 768 products (128x96, 3 stages).  Split-K MODE 0 tiles (256x96, 256x256,
+    // 256x128; r01-r03) were slower at every shape here (their epilogue and split fix-up dominate).
     if (!wide) return 2;
     // many-tile shapes (the sliding-window eval batch: M = 140 tiles x 229 tokens = 32060 rows; s5 sweep
     // tools/gpu72.sh): the 256-wide tiles win once they fill >= 1.5 waves of CUs -- qkv 161.6 -> 149.0 us,
@@ -929,80 +895,36 @@ int pick_cfg(int M, int N, int K, bool wide) {
 // of operands, PMC).  Grouping tile rows makes the XCD blocks squarer: the L2-miss bytes
 // A*ntn*GM/C + B*ntm/GM (C = tiles per XCD) are minimal at GM = sqrt(C * BN / BM).
 int group_rows(int M, int N, int bm, int bn, int splits) {
-    static const int forced = env_int("EBC_GEMM_GROUP_M");      // tuning override (-1: row-major)
-    if (forced) return forced > 0 ? forced : 0;
     const long ntm = (M + bm - 1) / bm, ntn = N / bn;
     if (ntn < 12 || splits > 1) return 0;
     const double C = (double)(ntm * ntn) / 8.0;
     const int gm = (int)(sqrt(C * bn / bm) + 0.5);
     return gm > 1 && gm < ntm ? gm : 0;
 }
-// r01: a split-K 256x96 tile (3-stage ring) for the N = 768 products measured 20-25 % slower than cfg 13
-inline bool split_cfg(int id) { return id == 20 || id == 21; }
-int pick_splits(int M, int N, int K, const TileCfg& c, int bk) {
-    if (!split_cfg(c.id)) return 1;
-    const long tiles = ntiles(M, N, c.bm, c.bn);
-    int s = 1;
-    // more splits while the grid stays within ~1.2 waves of CUs and each slice keeps >= 512 of K
-    while (tiles * (s + 1) <= NUM_CU * 6 / 5 && K % (bk * (s + 1)) == 0 && K / (s + 1) >= 512) ++s;
-    return s;
-}
-
-// the tile configuration a MODE 0 product runs (EBC_GEMM_CFG override when it fits, else the heuristic)
-int select_cfg(bool sixteen, int M, int N, int K)
-{
-    int cfg = forced_cfg();
-    const TileCfg* c = find_cfg(cfg);
-    if (!c || N % c->bn != 0 || (cfg >= 8 && !sixteen)) cfg = 0;
-    return cfg ? cfg : pick_cfg(M, N, K, sixteen);
-}
+// the tile configuration a MODE 0 product runs
+int select_cfg(bool sixteen, int M, int N, int K) { return pick_cfg(M, N, K, sixteen); }
 
 template <class E, class TO, int EPI>
-int dispatch_tile(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st)
+int dispatch_tile(GemmArgs g, void* /*ws*/, size_t /*ws_bytes*/, hipStream_t st)
 {
     constexpr bool SIXTEEN = E::BYTES == 2;
     const int cfg = select_cfg(SIXTEEN, g.M, g.N, g.K);
     const TileCfg* c = find_cfg(cfg);
-    const bool r64 = cfg >= 20 && cfg < 30;                   // 64-B K rows (4-stage rings)
-    const int bk = r64 ? 32 : 128 / E::BYTES;
-    int splits = forced_splits() > 0 ? forced_splits() : pick_splits(g.M, g.N, g.K, *c, bk);
-    if (splits > 1) {
-        const int tiles = ((g.M + c->bm - 1) / c->bm) * (g.N / c->bn);
-        const size_t need = GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
-        if (!ws || ws_bytes < need || g.K % (splits * bk) || tiles > GEMM_CNT_BYTES / 4) {
-            splits = 1;
-        } else {
-            g.cnt = reinterpret_cast<int*>(ws);                                   // zero, re-armed by the kernel
-            g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
-        }
-    }
-    g.splits = splits;
-    g.kslice = g.K / splits;
-    g.group_m = group_rows(g.M, g.N, c->bm, c->bn, splits);
+    g.splits = 1;
+    g.kslice = g.K;
+    g.group_m = group_rows(g.M, g.N, c->bm, c->bn, 1);
     switch (cfg) {
         case 1: return launch_gemm<E, TO, EPI, 128, 128, 2>(g, st);
         case 2: return launch_gemm<E, TO, EPI, 128, 64, 2>(g, st);
         case 3: return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2>(g, st);
         case 4: return launch_gemm<E, TO, EPI, 192, 192, 2, 4, 2>(g, st);
         case 5: return launch_gemm<E, TO, EPI, 128, 96, 2>(g, st);
-        case 6: return launch_gemm<E, TO, EPI, 256, 128, 2, 4, 2>(g, st);
         case 7: return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2>(g, st);
     }
     if constexpr (SIXTEEN) {
         switch (cfg) {
-            case 8: return launch_gemm<E, TO, EPI, 128, 64, 3>(g, st);
-            case 9: return launch_gemm<E, TO, EPI, 128, 128, 3>(g, st);
-            case 10: return launch_gemm<E, TO, EPI, 256, 128, 3, 4, 2>(g, st);
-            case 11: return launch_gemm<E, TO, EPI, 192, 128, 3, 4, 2>(g, st);
-            case 12: return launch_gemm<E, TO, EPI, 128, 64, 4>(g, st);
-            case 13: return launch_gemm<E, TO, EPI, 128, 96, 3>(g, st);
-            case 14: return launch_gemm<E, TO, EPI, 128, 192, 3>(g, st);
             case 15: return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, 0, 4>(g, st);
             case 16: return launch_gemm<E, TO, EPI, 128, 96, 4, 2, 2, 128, 0, 4>(g, st);
-            case 20: return launch_gemm<E, TO, EPI, 256, 256, 4, 4, 2, 64>(g, st);
-            case 21: return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64>(g, st);
-            case 22: return launch_gemm<E, TO, EPI, 128, 256, 4, 2, 4, 64>(g, st);
-            case 24: return launch_gemm<E, TO, EPI, 128, 128, 4, 2, 2, 64>(g, st);
         }
     }
     return EBC_E_UNSUPPORTED;
@@ -1038,8 +960,6 @@ int launch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st)
         if (cfg == 3) return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2, 128, MODE>(g, st);
         if (cfg == 7) return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2, 128, MODE>(g, st);
         if (cfg == 13) return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, MODE>(g, st);
-        if (cfg == 20) return launch_gemm<E, TO, EPI, 256, 256, 4, 4, 2, 64, MODE>(g, st);
-        if (cfg == 21) return launch_gemm<E, TO, EPI, 256, 128, 4, 4, 2, 64, MODE>(g, st);
     }
     return EBC_E_UNSUPPORTED;
 }
@@ -1109,14 +1029,9 @@ int splitk_reduce(const float* part, float* C, long MN, int splits, hipStream_t 
     return EBC_OK;
 }
 
-int forced_conv_cfg() { static const int v = env_int("EBC_CONV_CFG"); return v; }
 int conv_cfg(bool sixteen, int mode, int M, int N)
 {
     if (!sixteen) return 2;
-    if (const int f = forced_conv_cfg()) {
-        const TileCfg* c = find_cfg(f);
-        if (c && N % c->bn == 0 && (f == 2 || f == 3 || f == 7 || f == 13 || f == 20 || f == 21)) return f;
-    }
     // ResNet-50 decoder 3x3 conv (C = N = 2048, M = B*56*56): 256x256 tiles, several waves of them
     if (mode == 1 && N % 256 == 0 && N % 192 != 0 && ntiles(M, N, 256, 256) >= 256) return 7;
     // r01: 160x256 tiles (237 instead of 196 tiles at M = 16*784, N = 768) measured only 2-3 % faster on the
@@ -1124,16 +1039,14 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
     if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;
     return N % 96 == 0 ? 13 : 2;
 }
-int forced_conv_splits() { static const int v = env_int("EBC_CONV_SPLITS"); return v; }
 // Split-K tail for the implicit-GEMM convolutions (MODE 1, one 256-wide workgroup per CU): when T tiles are a few
 // more than whole waves (the ResNet-50 decoder: 784 = 3 x 256 + 16 tiles of 256x256), the T mod 256 last tiles
 // would run as a fourth, nearly empty wave of whole-K tiles.  Instead the whole waves run as one launch and the
 // tail tiles as a second with K split s ways (last arriver sums the f32 partials in split order), s from the
-// same fill / MFMA cost model as the weight-gradient plans plus the last arriver's re-read.  EBC_CONV_TAIL=0: off.
+// same fill / MFMA cost model as the weight-gradient plans plus the last arriver's re-read.
 struct TailPlan { int dp, tail, splits; };
 TailPlan tail_plan(int cfg, int M, int N, int K, int bk) {
-    static const int off = getenv("EBC_CONV_TAIL") && atoi(getenv("EBC_CONV_TAIL")) == 0;
-    if (off || (cfg != 3 && cfg != 7)) return TailPlan{0, 0, 1};
+    if (cfg != 3 && cfg != 7) return TailPlan{0, 0, 1};
     const TileCfg* c = find_cfg(cfg);
     const long T = ntiles(M, N, c->bm, c->bn), R = T % NUM_CU, kit = K / bk;
     if (T < NUM_CU || R == 0 || R > (long)(GEMM_CNT_BYTES / 4)) return TailPlan{0, 0, 1};
@@ -1157,7 +1070,6 @@ size_t tail_ws_bytes(int cfg, const TailPlan& p) {
 int conv_splits(int cfg, int mode, int M, int N, int nk)
 {
     if (mode != 2) return 1;
-    if (const int f = forced_conv_splits()) return (f >= 1 && nk % f == 0) ? f : 1;
     const TileCfg* c = find_cfg(cfg);
     const long tiles = ntiles(M, N, c->bm, c->bn);
     int s = 1;
@@ -1169,10 +1081,10 @@ template <class E>
 int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream_t st)
 {
     constexpr bool SIXTEEN = E::BYTES == 2;
-    const bool planned = mode == 2 && !forced_conv_cfg() && !forced_conv_splits();
+    const bool planned = mode == 2;
     const WPlan wp = planned ? wgrad_plan(SIXTEEN, true, g.M, g.N, g.K) : WPlan{0, 1, false};
     const int cfg = planned ? wp.cfg : conv_cfg(SIXTEEN, mode, g.M, g.N);
-    const int BK = cfg >= 20 ? 32 : 128 / E::BYTES;           // 64-B K rows for the 4-stage rings
+    const int BK = 128 / E::BYTES;
     const TileCfg* c = find_cfg(cfg);
     if (g.N % c->bn || g.K % BK) return EBC_E_UNSUPPORTED;
     if (mode == 2) g.kpi *= (128 / E::BYTES) / BK;             // geometry counts 128-B k-tiles
@@ -1238,14 +1150,13 @@ size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K)
         need += conv_stats_bytes(M, N);                                // EPI_STATS partials (BM >= 128)
         if (sixteen) {
             const int cfg = conv_cfg(sixteen, mode, M, N);
-            need += tail_ws_bytes(cfg, tail_plan(cfg, M, N, K, cfg >= 20 ? 32 : 64));
+            need += tail_ws_bytes(cfg, tail_plan(cfg, M, N, K, 64));
         }
     }
-    if (mode == 2 && !forced_conv_cfg() && !forced_conv_splits())
-        return std::max(need, wplan_ws(wgrad_plan(sixteen, true, M, N, K), M, N));
+    if (mode == 2) return std::max(need, wplan_ws(wgrad_plan(sixteen, true, M, N, K), M, N));
     const int cfg = conv_cfg(sixteen, mode, M, N);
     const TileCfg* c = find_cfg(cfg);
-    const int bk = !sixteen ? 32 : (cfg >= 20 ? 32 : 64);
+    const int bk = !sixteen ? 32 : 64;
     const int s = conv_splits(cfg, mode, M, N, K / bk);
     if (s > 1) need = std::max(need, GEMM_CNT_BYTES + (size_t)s * ntiles(M, N, c->bm, c->bn) * c->bm * c->bn * 4);
     return need;
@@ -1262,6 +1173,7 @@ int conv_gemm(int dtype, int mode, int epi, const void* A, const void* B, void* 
     g.cH = geo.H; g.cW = geo.W; g.cC = geo.C; g.cHp = geo.Hp; g.cWp = geo.Wp; g.kpi = geo.kpi;
     g.cQs = geo.Qs; g.cG = geo.G;
     if (mode == 1 && geo.C % bk) return EBC_E_UNSUPPORTED;
+    if (mode == 2 && geo.kpi > 0) g.kalg = (K / (geo.kpi * bk)) * geo.H * geo.W;     // B * H * W interior pixels
     if (epi == EPI_STATS) {
         if (!ws || wsb < conv_gemm_workspace_bytes(dtype, mode, M, N, K)) return EBC_E_ARG;
         g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
@@ -1276,18 +1188,9 @@ int conv_gemm(int dtype, int mode, int epi, const void* A, const void* B, void* 
     return EBC_E_ARG;
 }
 
-size_t gemm_workspace_bytes(int dtype, int M, int N, int K)
+size_t gemm_workspace_bytes(int, int, int, int)
 {
-    if (dtype == EBC_F32 || M <= 0 || N <= 0 || K <= 0) return 0;
-    int cfg = forced_cfg();
-    const TileCfg* c = find_cfg(cfg);
-    if (!c || N % c->bn != 0) cfg = pick_cfg(M, N, K, true);
-    c = find_cfg(cfg);
-    const int bk = (cfg >= 20 && cfg < 30) ? 32 : 64;
-    const int splits = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, bk);
-    if (splits <= 1) return 0;
-    const size_t tiles = (size_t)((M + c->bm - 1) / c->bm) * (N / c->bn);
-    return GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
+    return 0;             // the MODE 0 products never split K (see pick_cfg), so they take no workspace
 }
 
 int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
@@ -1441,10 +1344,9 @@ extern "C" int ebc_gemm_tile_config(int dtype, int M, int N, int K, int* out)
     const int cfg = select_cfg(sixteen, M, N, K);
     const TileCfg* c = find_cfg(cfg);
     if (out) {
-        const int bk = (cfg >= 20 && cfg < 30) ? 32 : (sixteen ? 64 : 32);
         out[0] = c->bm;
         out[1] = c->bn;
-        out[2] = forced_splits() > 0 ? forced_splits() : pick_splits(M, N, K, *c, bk);
+        out[2] = 1;
     }
     return cfg;
 }
@@ -1453,7 +1355,7 @@ extern "C" int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, in
 {
     if (M <= 0 || N <= 0 || K <= 0 || (mode != 1 && mode != 2)) return EBC_E_ARG;
     const bool sixteen = dtype != EBC_F32;
-    if (mode == 2 && !forced_conv_cfg() && !forced_conv_splits()) {
+    if (mode == 2) {
         const WPlan wp = wgrad_plan(sixteen, true, M, N, K);
         const TileCfg* c = find_cfg(wp.cfg);
         if (out) { out[0] = c->bm; out[1] = c->bn; out[2] = wp.splits; }
@@ -1462,7 +1364,7 @@ extern "C" int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, in
     const int cfg = conv_cfg(sixteen, mode, M, N);
     const TileCfg* c = find_cfg(cfg);
     if (out) {
-        const int bk = !sixteen ? 32 : (cfg >= 20 ? 32 : 64);
+        const int bk = !sixteen ? 32 : 64;
         out[0] = c->bm;
         out[1] = c->bn;
         out[2] = conv_splits(cfg, mode, M, N, K / bk);

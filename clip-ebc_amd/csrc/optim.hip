@@ -175,27 +175,28 @@ int make_pack(const EbcAdamTensor* ts, int n0, int n1, AdamPack& k)
 
 }  // namespace
 
-extern "C" int ebc_adam_step(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler,
-                             int scaler_parity, double lr, double beta1, double beta2, double eps, double weight_decay,
-                             double growth_factor, double backoff_factor, int growth_interval, int write_unscaled_grad,
-                             ebc_stream_t stream)
+namespace {
+int amp_check_all(const EbcAdamTensor* tensors, int n, float* found, hipStream_t st)
 {
-    if (!tensors || n <= 0 || !step || (step_parity & ~1) || (scaler_parity & ~1) || growth_interval <= 0) return EBC_E_ARG;
-    hipStream_t st = (hipStream_t)stream;
+    AdamPack k;
+    for (int g0 = 0; g0 < n; g0 += MAXT) {
+        const int rc = make_pack(tensors, g0, g0 + MAXT < n ? g0 + MAXT : n, k);
+        if (rc) return rc;
+        hipLaunchKernelGGL(amp_check_kernel, dim3(k.blk0[k.n]), dim3(256), 0, st, k, found);
+        EBC_CHECK_LAUNCH();
+    }
+    return EBC_OK;
+}
+int adam_update_all(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler, int scaler_parity,
+                    double lr, double beta1, double beta2, double eps, double weight_decay, double growth_factor,
+                    double backoff_factor, int growth_interval, int write_unscaled_grad, hipStream_t st)
+{
     const bool amp = scaler != nullptr;
     float* cur = amp ? scaler + 3 * scaler_parity : nullptr;
     float* nxt = amp ? scaler + 3 * (1 - scaler_parity) : nullptr;
-    AdamPack k;
-    if (amp) {
-        for (int g0 = 0; g0 < n; g0 += MAXT) {
-            const int rc = make_pack(tensors, g0, g0 + MAXT < n ? g0 + MAXT : n, k);
-            if (rc) return rc;
-            hipLaunchKernelGGL(amp_check_kernel, dim3(k.blk0[k.n]), dim3(256), 0, st, k, cur + 2);
-            EBC_CHECK_LAUNCH();
-        }
-    }
     AdamHyper h{lr, beta1, beta2, eps, weight_decay, growth_factor, backoff_factor, growth_interval, amp ? 1 : 0,
                 write_unscaled_grad ? 1 : 0, 0};
+    AdamPack k;
     for (int g0 = 0; g0 < n; g0 += MAXT) {
         const int g1 = g0 + MAXT < n ? g0 + MAXT : n;
         const int rc = make_pack(tensors, g0, g1, k);
@@ -206,4 +207,36 @@ extern "C" int ebc_adam_step(const EbcAdamTensor* tensors, int n, float* step, i
         EBC_CHECK_LAUNCH();
     }
     return EBC_OK;
+}
+}  // namespace
+
+extern "C" int ebc_adam_step(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler,
+                             int scaler_parity, double lr, double beta1, double beta2, double eps, double weight_decay,
+                             double growth_factor, double backoff_factor, int growth_interval, int write_unscaled_grad,
+                             ebc_stream_t stream)
+{
+    if (!tensors || n <= 0 || !step || (step_parity & ~1) || (scaler_parity & ~1) || growth_interval <= 0) return EBC_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (scaler) {
+        const int rc = amp_check_all(tensors, n, scaler + 3 * scaler_parity + 2, st);
+        if (rc) return rc;
+    }
+    return adam_update_all(tensors, n, step, step_parity, scaler, scaler_parity, lr, beta1, beta2, eps, weight_decay,
+                           growth_factor, backoff_factor, growth_interval, write_unscaled_grad, st);
+}
+
+extern "C" int ebc_amp_check(const EbcAdamTensor* tensors, int n, float* scaler, int scaler_parity, ebc_stream_t stream)
+{
+    if (!tensors || n <= 0 || !scaler || (scaler_parity & ~1)) return EBC_E_ARG;
+    return amp_check_all(tensors, n, scaler + 3 * scaler_parity + 2, (hipStream_t)stream);
+}
+
+extern "C" int ebc_adam_update(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler,
+                               int scaler_parity, double lr, double beta1, double beta2, double eps, double weight_decay,
+                               double growth_factor, double backoff_factor, int growth_interval, int write_unscaled_grad,
+                               ebc_stream_t stream)
+{
+    if (!tensors || n <= 0 || !step || (step_parity & ~1) || (scaler_parity & ~1) || growth_interval <= 0) return EBC_E_ARG;
+    return adam_update_all(tensors, n, step, step_parity, scaler, scaler_parity, lr, beta1, beta2, eps, weight_decay,
+                           growth_factor, backoff_factor, growth_interval, write_unscaled_grad, (hipStream_t)stream);
 }

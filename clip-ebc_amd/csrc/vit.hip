@@ -19,11 +19,6 @@
 #include "ebc_common.h"
 #include "kernels.h"
 
-#ifndef EBC_WEIGHT_TOUCH
-// which weights the attention launches read onto the die (A/B builds, tools/build_var.sh): forward 1 w_out, 2 w_fc,
-// 4 w_proj, 8 next block's w_qkv; backward 16 wt_qkv, 32 / 64 / 128 previous block's wt_proj / wt_fc / wt_out
-#define EBC_WEIGHT_TOUCH 0xFF
-#endif
 
 namespace {
 
@@ -163,10 +158,10 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
     auto touch_fwd = [&](int l) {
         ebc::TouchList t{};
         const EbcVitLayer& p = w->layer[l];
-        if (EBC_WEIGHT_TOUCH & 1) t.add(p.w_out, (size_t)WIDTH * WIDTH * es);
-        if (EBC_WEIGHT_TOUCH & 2) t.add(p.w_fc, (size_t)MLP * WIDTH * es);
-        if (EBC_WEIGHT_TOUCH & 4) t.add(p.w_proj, (size_t)WIDTH * MLP * es);
-        if ((EBC_WEIGHT_TOUCH & 8) && l + 1 < layers) t.add(w->layer[l + 1].w_qkv, (size_t)QKVW * WIDTH * es);
+        t.add(p.w_out, (size_t)WIDTH * WIDTH * es);
+        t.add(p.w_fc, (size_t)MLP * WIDTH * es);
+        t.add(p.w_proj, (size_t)WIDTH * MLP * es);
+        if (l + 1 < layers) t.add(w->layer[l + 1].w_qkv, (size_t)QKVW * WIDTH * es);
         return t;
     };
     auto block = [&](int l, int b0, int nb, hipStream_t sx) -> int {
@@ -236,12 +231,12 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
     const size_t es = dtype == EBC_F32 ? 4 : 2;
     auto touch_bwd = [&](int l) {
         ebc::TouchList t{};
-        if (EBC_WEIGHT_TOUCH & 16) t.add(w->layer[l].wt_qkv, (size_t)WIDTH * QKVW * es);
+        t.add(w->layer[l].wt_qkv, (size_t)WIDTH * QKVW * es);
         if (l > 0) {
             const EbcVitLayer& q = w->layer[l - 1];
-            if (EBC_WEIGHT_TOUCH & 32) t.add(q.wt_proj, (size_t)MLP * WIDTH * es);
-            if (EBC_WEIGHT_TOUCH & 64) t.add(q.wt_fc, (size_t)WIDTH * MLP * es);
-            if (EBC_WEIGHT_TOUCH & 128) t.add(q.wt_out, (size_t)WIDTH * WIDTH * es);
+            t.add(q.wt_proj, (size_t)MLP * WIDTH * es);
+            t.add(q.wt_fc, (size_t)WIDTH * MLP * es);
+            t.add(q.wt_out, (size_t)WIDTH * WIDTH * es);
         }
         return t;
     };

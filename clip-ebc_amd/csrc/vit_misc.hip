@@ -76,12 +76,7 @@ __device__ __forceinline__ void ln_row(float4 (&v)[NV], const float4 (&gb)[2 * N
 // Row blocks in XCD order (xcd_remap): each XCD takes a contiguous run of rows, the same rows the GEMM tiles that
 // produce and consume them run on that XCD (gemm.hip maps its tiles the same way), so the row operands a kernel
 // reads were last written on its own XCD
-#ifndef EBC_XCD_ROWS
-#define EBC_XCD_ROWS 1
-#endif
-__device__ __forceinline__ int row_block() {
-    return EBC_XCD_ROWS ? xcd_remap(blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-}
+__device__ __forceinline__ int row_block() { return xcd_remap(blockIdx.x, (int)gridDim.x); }
 
 // deep-VPT insert fused into ln_1 (model.py:131-140, 161-168): rows 1..NV of every crop are read from
 // the prompt (vpt + b * bstride + (l-1) * D) instead of X, and written into X for the residual path

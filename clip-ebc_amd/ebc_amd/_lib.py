@@ -117,6 +117,8 @@ SIGNATURES = {
     "ebc_augment_crops": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, EbcAugConst, _P]),
     "ebc_point_map": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "ebc_adam_step": (_I, [_P, _I, _P, _I, _P, _I, _D, _D, _D, _D, _D, _D, _D, _I, _I, _P]),
+    "ebc_amp_check": (_I, [_P, _I, _P, _I, _P]),
+    "ebc_adam_update": (_I, [_P, _I, _P, _I, _P, _I, _D, _D, _D, _D, _D, _D, _D, _I, _I, _P]),
     "ebc_probe_begin": (_I, [_I]),
     "ebc_probe_end": (_I, [_P, _I]),
     "ebc_marker": (_I, [_I, _P]),

@@ -198,12 +198,13 @@ class DACELoss(nn.Module):
                float(dm.ot_loss.reg) if dm else 10.0, int(dm.ot_loss.num_of_iter_in_ot) if dm else 0,
                1e-9, 10, total, reduced)
         sink = [] if (dm is not None and dm.keep_internals) else None
-        loss, d, _ = _DaceFn.apply(pred_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
+        loss, d, stats = _DaceFn.apply(pred_class, pred_density, target_density, pts, offs, order, lo, hi, cfg, sink)
         if sink:
             dm.internals = sink[0]
         # the 5 terms as one device vector in _INFO_DM order (loss, ot, tv, count, ce): a packed all-reduce
-        # needs no stack launch
+        # needs no stack launch; the per-crop stats [B, 8] (ce, tv*n, count, ot, wd, iterations, rolled back, err)
         self.last_terms = d
+        self.last_stats = stats
         if self.use_dm_loss:
             info = {k: d[i] for i, k in enumerate(_INFO_DM)}
         else:

@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 from collections import OrderedDict
 from typing import Any, Dict, List, Optional, Tuple, Union
 
@@ -301,9 +300,6 @@ class _HeadFn(torch.autograd.Function):
 
 # ----------------------------------------------------------------------------- decoder
 _DEC_WS: Dict[Tuple[torch.device, int], Tensor] = {}
-# EBC_RN50_ENCODER=torch runs clip_resnet50's whole ModifiedResNet on PyTorch-ROCm (MIOpen) instead of the
-# HIP Bottleneck blocks (ebc_amd/resnet.py _ResBlockFn); an A/B switch, not a fallback (both need the GPU)
-_RN50_TORCH_ENCODER = __import__("os").environ.get("EBC_RN50_ENCODER", "") == "torch"
 
 
 def _dec_workspace(dev: torch.device, nbytes: int, slot: int = 0) -> Tensor:
@@ -353,10 +349,6 @@ def _bn_momentum(bn: nn.Module) -> float:
     if bn.momentum is not None:
         return float(bn.momentum)
     return 1.0 / float(bn.num_batches_tracked.item())
-
-
-# EBC_BN_FUSED=0: the three-launch BatchNorm backward statistics path (A/B and debugging)
-_FUSE_BN = os.environ.get("EBC_BN_FUSED", "1") != "0"
 
 
 class _DecoderFn(torch.autograd.Function):
@@ -466,7 +458,7 @@ class _DecoderFn(torch.autograd.Function):
             z, mean, rstd, scale, shift, count, pg, colsum = ctx.outs[i]
             gm = (g1, g2)[i]
             dg, db, coef = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty(3, N, **f32)
-            fused = pg is None and count == float(P) and _FUSE_BN
+            fused = pg is None and count == float(P)
             if fused:
                 # no exchange: column sums and finalize in one launch (ebc_bn_bwd_reduce_finalize, count = P)
                 _lib.check(L.ebc_bn_bwd_reduce_finalize(dt, _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z), _lib.ptr(mean),
@@ -669,10 +661,7 @@ class CLIP_EBC(nn.Module):
         """models/clip/model.py:191-217 for the resnet50 backbone: the trainable ModifiedResNet (stem on PyTorch-ROCm,
         its 16 Bottlenecks on HIP), then the HIP Bottleneck decoder and head."""
         from .resnet import _BottleneckFn, encoder_forward, flush_bn_counters
-        if _RN50_TORCH_ENCODER:                                              # A/B: the whole encoder on MIOpen
-            feat = self.image_encoder(x.contiguous(memory_format=torch.channels_last)).permute(0, 2, 3, 1)
-        else:                                                                # stem on MIOpen, 16 blocks on HIP
-            feat = encoder_forward(self.image_encoder, x, cdt, self.training)
+        feat = encoder_forward(self.image_encoder, x, cdt, self.training)   # stem on MIOpen, 16 blocks on HIP
         feat = feat.float().contiguous()                                     # NHWC rows, f32
         up = self.encoder_reduction // self.reduction
         blk = self.image_decoder[0]

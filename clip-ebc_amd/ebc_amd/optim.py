@@ -14,7 +14,8 @@ The arithmetic is torch's fused Adam's, operation for operation (tests/test_gpu_
 unscaled gradients, parameters and moments to f32 rounding).
 
 Scope: f32 parameters on one HIP device, L2 weight decay (Adam, not AdamW), no amsgrad / maximize; one
-optimizer per GradScaler per iteration (the reference has one).
+optimizer per GradScaler per iteration (the reference has one); several param groups share the scaler's skip decision
+(ebc_amp_check over every group, then ebc_adam_update per group).
 """
 from __future__ import annotations
 
@@ -67,6 +68,13 @@ class Adam(torch.optim.Optimizer):
             if not st:
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            for k in ("exp_avg", "exp_avg_sq"):
+                # moments loaded from a torch.optim.Adam state_dict keep the layout they were saved in (e.g.
+                # contiguous NCHW beside a channels-last conv weight): re-laid out in the parameter's memory order,
+                # values kept, so the elementwise update pairs each parameter element with its own moments
+                m = st[k]
+                if m.stride() != p.stride() or not _dense(m) or m.dtype != torch.float32 or m.device != p.device:
+                    st[k] = torch.empty_like(p).copy_(m)
             out.append(_lib.EbcAdamTensor(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
                                           st["exp_avg_sq"].data_ptr(), p.numel()))
         return out
@@ -80,6 +88,7 @@ class Adam(torch.optim.Optimizer):
     @torch.no_grad()
     def _launch(self, scaler: Optional["GradScaler"]) -> None:
         lib = _lib.lib()
+        groups = []
         for gi, group in enumerate(self.param_groups):
             ts = self._group_tensors(gi, group)
             if not ts:
@@ -88,20 +97,37 @@ class Adam(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.device != dev:
                     raise RuntimeError("ebc_amd.optim.Adam: one device per param group")
-            steps = self._step_buf(gi, dev)
+            groups.append((gi, group, ts, dev))
+        if not groups:
+            return
+        if scaler is not None:
+            devs = {d for _, _, _, d in groups}
+            if len(devs) != 1:
+                raise RuntimeError("ebc_amd.optim.Adam: a GradScaler'd step runs on one device")
+            dev = groups[0][3]
+            sbuf, spar = scaler._state(dev), scaler._parity
+            sc = _lib.ptr(sbuf, dev)
+            gf, bf, gint = scaler._growth_factor, scaler._backoff_factor, scaler._growth_interval
+        else:
+            sc, spar, gf, bf, gint = None, 0, 2.0, 0.5, 1
+        # one group (the reference's case): check + update in one call; several groups sharing a scaler: the inf
+        # check over every group's gradients first, so a non-finite gradient in any group skips them all (torch)
+        split = scaler is not None and len(groups) > 1
+        if split:
+            every = [t for _, _, ts, _ in groups for t in ts]
+            with _lib.on(dev):
+                _lib.check(lib.ebc_amp_check((_lib.EbcAdamTensor * len(every))(*every), len(every), sc, spar,
+                                             _lib.stream(dev)), "ebc_amp_check")
+        fn = lib.ebc_adam_update if split else lib.ebc_adam_step
+        for gi, group, ts, gdev in groups:
+            steps = self._step_buf(gi, gdev)
             arr = (_lib.EbcAdamTensor * len(ts))(*ts)
             b1, b2 = group["betas"]
-            if scaler is not None:
-                sbuf, spar = scaler._state(dev), scaler._parity
-                sc = _lib.ptr(sbuf, dev)
-                gf, bf, gint = scaler._growth_factor, scaler._backoff_factor, scaler._growth_interval
-            else:
-                sc, spar, gf, bf, gint = None, 0, 2.0, 0.5, 1
-            with _lib.on(dev):
-                _lib.check(lib.ebc_adam_step(arr, len(ts), _lib.ptr(steps, dev), self._parity[gi], sc, spar,
-                                             float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                                             float(group["weight_decay"]), float(gf), float(bf), int(gint), 1,
-                                             _lib.stream(dev)), "ebc_adam_step")
+            with _lib.on(gdev):
+                _lib.check(fn(arr, len(ts), _lib.ptr(steps, gdev), self._parity[gi], sc, spar,
+                              float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                              float(group["weight_decay"]), float(gf), float(bf), int(gint), 1,
+                              _lib.stream(gdev)), "ebc_adam_step")
             self._parity[gi] ^= 1
 
     @torch.no_grad()
@@ -161,6 +187,7 @@ class GradScaler:
         self._backoff_factor = float(backoff_factor)
         self._growth_interval = int(growth_interval)
         self._enabled = bool(enabled)
+        self._init_tracker = 0
         self._buf: Optional[torch.Tensor] = None
         self._parity = 0
         self._stepped = False
@@ -170,7 +197,10 @@ class GradScaler:
 
     def _state(self, device) -> torch.Tensor:
         if self._buf is None:
-            self._buf = torch.tensor([[self._init_scale, 0.0, 0.0]] * 2, dtype=torch.float32, device=device)
+            # both entries seeded with the scale and growth tracker (a loaded state_dict's, torch's
+            # _init_growth_tracker, when load_state_dict ran before the first step: utils/train_utils.py:122-123)
+            self._buf = torch.tensor([[self._init_scale, float(self._init_tracker), 0.0]] * 2, dtype=torch.float32,
+                                     device=device)
         return self._buf
 
     def scale(self, outputs):
@@ -194,7 +224,14 @@ class GradScaler:
         if not self._enabled:
             return
         if new_scale is not None:
-            self._state(self._buf.device if self._buf is not None else "cuda")[self._parity, 0].fill_(float(new_scale))
+            # torch.amp.GradScaler.update(new_scale): the scale becomes new_scale, the growth tracker is left as it
+            # was before the step; the step's launch already wrote the other entry, which the next step reads
+            buf = self._state(self._buf.device if self._buf is not None else "cuda")
+            if self._stepped:
+                buf[1 - self._parity, 1].copy_(buf[self._parity, 1])
+                self._parity ^= 1
+                self._stepped = False
+            buf[self._parity, 0].fill_(float(new_scale))
             return
         if self._stepped:
             self._parity ^= 1        # the step's launch wrote the next scale / tracker into the other entry
@@ -219,6 +256,7 @@ class GradScaler:
         self._growth_factor = float(sd["growth_factor"])
         self._backoff_factor = float(sd["backoff_factor"])
         self._growth_interval = int(sd["growth_interval"])
+        self._init_tracker = int(sd["_growth_tracker"])
         if self._buf is not None:
             self._buf[self._parity, 0] = self._init_scale
-            self._buf[self._parity, 1] = float(sd["_growth_tracker"])
+            self._buf[self._parity, 1] = float(self._init_tracker)

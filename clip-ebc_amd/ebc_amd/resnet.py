@@ -17,7 +17,6 @@ except conv2's input, which is the zero-padded image the implicit-GEMM 3x3 conv 
 from __future__ import annotations
 
 import ctypes
-import os
 from collections import OrderedDict
 from typing import Any, List, Optional, Tuple
 
@@ -129,8 +128,6 @@ class Bottleneck(nn.Module):
         self.downsample = nn.Identity()
 
 
-# EBC_BN_FUSED=0: the three-launch BatchNorm statistics path everywhere (A/B and debugging)
-_FUSE_BN = os.environ.get("EBC_BN_FUSED", "1") != "0"
 
 
 def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, training: bool, dev, st, src=None):
@@ -143,7 +140,7 @@ def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, 
     use_batch = colsum is not None
     pg = _bn_group(bn) if use_batch else None
     count = float(P)
-    fused = src is not None and use_batch and pg is None and _FUSE_BN
+    fused = src is not None and use_batch and pg is None
     if src is not None and use_batch and not fused:
         dt, z, ws = src
         _lib.check(L.ebc_bn_stats(dt, _lib.ptr(z), _lib.ptr(colsum), _lib.ptr(ws), ws.numel(), P, N, st), "ebc_bn_stats")
@@ -182,7 +179,7 @@ def _batch_norm_bwd(L, gamma: Tensor, state, dnext: Tensor, mask: Optional[Tenso
     from this rank's sums, the input-gradient coefficients from the all-reduced sums and count."""
     mean, rstd, scale, shift, count, pg, colsum = state
     f32 = dict(device=dev, dtype=torch.float32)
-    if pg is None and _FUSE_BN:                    # no exchange: column sums and finalize in one launch
+    if pg is None:                    # no exchange: column sums and finalize in one launch
         dg, db, coef = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty(3, N, **f32)
         _lib.check(L.ebc_bn_bwd_reduce_finalize(_lib.dtype_code(z.dtype), _lib.ptr(dnext), _lib.ptr(mask), _lib.ptr(z),
                                                 _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),

@@ -382,6 +382,14 @@ typedef struct {
 int ebc_adam_step(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler, int scaler_parity,
                   double lr, double beta1, double beta2, double eps, double weight_decay, double growth_factor,
                   double backoff_factor, int growth_interval, int write_unscaled_grad, ebc_stream_t stream);
+/* The same step in two calls, for several parameter groups sharing one GradScaler (torch skips the WHOLE optimizer
+ * step when any group has a non-finite gradient): ebc_amp_check over every group's tensors first (found_inf of entry
+ * [scaler_parity]), then ebc_adam_update per group (the update launch alone; each call writes the same next scaler
+ * state). */
+int ebc_amp_check(const EbcAdamTensor* tensors, int n, float* scaler, int scaler_parity, ebc_stream_t stream);
+int ebc_adam_update(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler, int scaler_parity,
+                    double lr, double beta1, double beta2, double eps, double weight_decay, double growth_factor,
+                    double backoff_factor, int growth_interval, int write_unscaled_grad, ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Measurement (bench.py): in-step kernel durations and profile windows.  Not on the reference's

@@ -8,7 +8,9 @@ fp32 step by PyTorch's AMP rounding.  Here the same synthetic weights and crops 
   hip    the drop-in model + loss under the same autocast (the HIP kernels).
 Every quantity must satisfy err(hip) <= 1.5 x err(amp) (relative L2 against truth), per quantity, NOT stacked:
 the logits, the expected count, EACH of the 12 layers' prompt gradients (layer 0's comes from the trimmed
-backward, vit.hip), the decoder's two conv weight gradients and the projection weight gradient.
+backward, vit.hip), the decoder's two conv weight gradients and the projection weight gradient.  At 224 (BASELINE
+configs[2]/[3]) and at 448, the reference trainer's default input size (trainer.py:26): 817 tokens through the
+chunked long-sequence attention, a 56x56 density grid.
 """
 import numpy as np
 import pytest
@@ -23,12 +25,12 @@ LAYERS = 12
 PARAMS = ["image_decoder.0.conv1.weight", "image_decoder.0.conv2.weight", "projection.weight"]
 
 
-def _oracle(p_cpu, img, txt, dens, pts, device, amp):
+def _oracle(p_cpu, img, txt, dens, pts, device, amp, size=224):
     p = {k: v.detach().to(device).requires_grad_(v.requires_grad) for k, v in p_cpu.items()}
     x = torch.from_numpy(img).to(device)
     with torch.autocast("cuda", dtype=amp, enabled=amp is not None):
         lg, ex, _ = ref.forward(p, x, txt.to(device), ANCHORS_NWPU, LAYERS)
-        loss, _ = ref.dace_loss(lg, ex, torch.from_numpy(dens).to(device), pts, BINS)
+        loss, _ = ref.dace_loss(lg, ex, torch.from_numpy(dens).to(device), pts, BINS, input_size=size)
     loss.backward()
     out = {"logits": lg.detach().float().cpu(), "exp": ex.detach().float().cpu()}
     for l in range(LAYERS):
@@ -38,14 +40,14 @@ def _oracle(p_cpu, img, txt, dens, pts, device, amp):
     return out
 
 
-def _hip(img, txt, dens, pts, amp):
+def _hip(img, txt, dens, pts, amp, size=224):
     from ebc_amd.losses import DACELoss
     from ebc_amd.model import get_model
-    m = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", text_features=txt,
+    m = get_model("clip_vit_b_16", size, 8, BINS, ANCHORS_NWPU, prompt_type="word", text_features=txt,
                   weights_seed=0).cuda().train()
     with torch.autocast("cuda", dtype=amp):
         lg, ex = m(torch.from_numpy(img).cuda())
-        loss, _ = DACELoss(BINS, 8, count_loss="dmcount", input_size=224)(
+        loss, _ = DACELoss(BINS, 8, count_loss="dmcount", input_size=size)(
             lg, ex, torch.from_numpy(dens).cuda(), [torch.from_numpy(q).cuda() for q in pts])
     loss.backward()
     torch.cuda.synchronize()
@@ -58,14 +60,15 @@ def _hip(img, txt, dens, pts, amp):
     return out
 
 
-@pytest.mark.parametrize("B,amp", [(16, torch.float16), (32, torch.float16), (16, torch.bfloat16)])
-def test_step_error_within_pytorch_amp_error(B, amp):
+@pytest.mark.parametrize("B,amp,size", [(16, torch.float16, 224), (32, torch.float16, 224), (16, torch.bfloat16, 224),
+                                        (4, torch.float16, 448)])
+def test_step_error_within_pytorch_amp_error(B, amp, size):
     txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
-    img, pts, dens = syn.synthetic_crops(B, 224, seed=900 + B)
-    p = ref.params_from_state(syn.full_state(0, layers=LAYERS, include_text=False))
-    truth = _oracle(p, img, txt, dens, pts, torch.device("cpu"), None)
-    torch_amp = _oracle(p, img, txt, dens, pts, torch.device("cuda"), amp)
-    hip = _hip(img, txt, dens, pts, amp)
+    img, pts, dens = syn.synthetic_crops(B, size, seed=900 + B + (size if size != 224 else 0))
+    p = ref.params_from_state(syn.full_state(0, layers=LAYERS, include_text=False, input_size=size))
+    truth = _oracle(p, img, txt, dens, pts, torch.device("cpu"), None, size)
+    torch_amp = _oracle(p, img, txt, dens, pts, torch.device("cuda"), amp, size)
+    hip = _hip(img, txt, dens, pts, amp, size)
     worst, bad = 0.0, []
     for k in truth:
         e_amp, e_hip = rel_l2(torch_amp[k], truth[k]), rel_l2(hip[k], truth[k])
@@ -74,5 +77,5 @@ def test_step_error_within_pytorch_amp_error(B, amp):
         print(f"{k:32s} hip {e_hip:.3e}  torch-amp {e_amp:.3e}  ratio {ratio:.2f}")
         if e_hip > 1.5 * e_amp:
             bad.append((k, e_hip, e_amp))
-    print(f"B={B} {amp}: worst hip / torch-amp error ratio {worst:.2f}")
+    print(f"B={B} {amp} {size}x{size}: worst hip / torch-amp error ratio {worst:.2f}")
     assert not bad, bad

@@ -67,6 +67,13 @@ def test_attention_fwd_bwd(dname, B, L):
     o_flat = o.permute(0, 2, 1, 3).reshape(B * L, H * 64)
     assert _rel(out, o_flat) < TOL[dname]
     assert _rel(lse, torch.logsumexp(s, -1)) < 1e-5
+    # every row on its own (a wrong running maximum in one query lane overflows that row's exp sum: r03's long-kernel
+    # failure was NaN rows), not only the whole tensor's norm
+    ref_lse = torch.logsumexp(s, -1)
+    assert bool(torch.isfinite(out).all()) and bool(torch.isfinite(lse).all())
+    assert float(((lse.double() - ref_lse).abs() / (1.0 + ref_lse.abs())).max()) < 1e-5
+    row_err = (out.double() - o_flat).norm(dim=1) / o_flat.norm(dim=1)
+    assert float(row_err.max()) < 8 * TOL[dname], float(row_err.max())
     dout = torch.randn(B * L, H * 64, device="cuda", generator=g).to(dt)
     delta = torch.empty(B, H, L, device="cuda")
     dqkv = torch.empty_like(qkv)

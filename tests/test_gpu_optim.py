@@ -133,3 +133,117 @@ def test_adam_channels_last_params_and_strided_grads():
         res[kind] = (p1.detach().clone(), p2.detach().clone())
     for a, b in zip(res["ebc"], res["torch"]):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9)
+
+
+def test_adam_resume_torch_state_into_channels_last_params():
+    """a torch.optim.Adam checkpoint's moments are contiguous NCHW; resumed into channels-last parameters
+    they are re-laid out in the parameter's memory order (values kept), so the next steps match torch resuming the
+    same state."""
+    from ebc_amd import optim as eo
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(11)
+    w0 = torch.randn(8, 3, 5, 5, generator=g)
+    src = torch.nn.Parameter(w0.clone().to(dev))                                # contiguous, as a checkpoint holds it
+    topt = torch.optim.Adam([src], lr=1e-3, weight_decay=1e-4)
+    for i in range(2):
+        src.grad = torch.randn(8, 3, 5, 5, generator=torch.Generator().manual_seed(200 + i)).to(dev)
+        topt.step()
+    sd = topt.state_dict()
+    res = {}
+    for kind in ("ebc", "torch"):
+        p = torch.nn.Parameter(src.detach().clone().to(memory_format=torch.channels_last))
+        opt = eo.Adam([p], lr=1e-3, weight_decay=1e-4) if kind == "ebc" else \
+            torch.optim.Adam([p], lr=1e-3, weight_decay=1e-4, foreach=True)
+        opt.load_state_dict(sd)
+        for i in range(3):
+            p.grad = torch.randn(8, 3, 5, 5, generator=torch.Generator().manual_seed(300 + i)).to(dev)
+            opt.step()
+        res[kind] = p.detach().clone()
+    assert not res["ebc"].is_contiguous()
+    torch.testing.assert_close(res["ebc"], res["torch"], rtol=1e-6, atol=1e-9)
+
+
+def test_grad_scaler_resume_before_first_step_keeps_tracker():
+    """the reference loads the scaler state right after building it (utils/train_utils.py:122-123),
+    before any step; the growth tracker must survive, as torch keeps it (_init_growth_tracker)."""
+    from ebc_amd import optim as eo
+    dev = torch.device("cuda:0")
+    seq = {}
+    for kind in ("ebc", "torch"):
+        p = torch.nn.Parameter(torch.ones(64, device=dev))
+        if kind == "ebc":
+            opt, sc = eo.Adam([p], lr=1e-3), eo.GradScaler(growth_interval=4)
+        else:
+            opt, sc = torch.optim.Adam([p], lr=1e-3, fused=True), torch.amp.GradScaler("cuda", growth_interval=4)
+        sc.load_state_dict({"scale": 1024.0, "growth_factor": 2.0, "backoff_factor": 0.5, "growth_interval": 4,
+                            "_growth_tracker": 3})
+        out = []
+        for i in range(3):
+            sc.scale(torch.ones((), device=dev))
+            p.grad = torch.full((64,), 0.5, device=dev) * sc.get_scale()
+            sc.step(opt)
+            sc.update()
+            out.append(sc.get_scale())
+        seq[kind] = out
+    assert seq["ebc"] == seq["torch"] == [2048.0, 2048.0, 2048.0], seq
+
+
+def test_grad_scaler_update_new_scale_after_step():
+    """update(new_scale) after a step: the scale is set, the tracker stays where it was before that step, and the
+    next step runs (it raised 'step() has already been called')."""
+    from ebc_amd import optim as eo
+    dev = torch.device("cuda:0")
+    seq = {}
+    for kind in ("ebc", "torch"):
+        p = torch.nn.Parameter(torch.ones(64, device=dev))
+        if kind == "ebc":
+            opt, sc = eo.Adam([p], lr=1e-3), eo.GradScaler(init_scale=256.0, growth_interval=2)
+        else:
+            opt, sc = torch.optim.Adam([p], lr=1e-3, fused=True), torch.amp.GradScaler("cuda", init_scale=256.0,
+                                                                                          growth_interval=2)
+        out = []
+        for i in range(4):
+            sc.scale(torch.ones((), device=dev))
+            p.grad = torch.full((64,), 0.5, device=dev) * sc.get_scale()
+            sc.step(opt)
+            if i == 1:
+                sc.update(64.0)
+            else:
+                sc.update()
+            out.append((sc.get_scale(), int(sc.state_dict()["_growth_tracker"])))
+        seq[kind] = (out, p.detach().clone())
+    assert seq["ebc"][0] == seq["torch"][0], (seq["ebc"][0], seq["torch"][0])
+    torch.testing.assert_close(seq["ebc"][1], seq["torch"][1], rtol=1e-6, atol=1e-9)
+
+
+def test_adam_two_groups_inf_in_second_group_skips_both():
+    """with several param groups under one scaler, a non-finite gradient in ANY group skips every group's
+    update (torch skips the whole optimizer step); the step counts advance together afterwards."""
+    from ebc_amd import optim as eo
+    dev = torch.device("cuda:0")
+    res = {}
+    for kind in ("ebc", "torch"):
+        a = torch.nn.Parameter(torch.linspace(-1, 1, 100, device=dev))
+        b = torch.nn.Parameter(torch.linspace(2, 3, 50, device=dev))
+        groups = [{"params": [a], "lr": 1e-3}, {"params": [b], "lr": 2e-3, "weight_decay": 1e-2}]
+        if kind == "ebc":
+            opt, sc = eo.Adam(groups), eo.GradScaler(init_scale=8.0, growth_interval=100)
+        else:
+            opt, sc = torch.optim.Adam(groups, fused=True), torch.amp.GradScaler("cuda", init_scale=8.0, growth_interval=100)
+        snaps = []
+        for i in range(3):
+            sc.scale(torch.ones((), device=dev))
+            s = sc.get_scale()
+            a.grad = torch.full((100,), 0.25, device=dev) * s
+            b.grad = torch.full((50,), -0.5, device=dev) * s
+            if i == 1:
+                b.grad[7] = float("inf")
+            sc.step(opt)
+            sc.update()
+            snaps.append((a.detach().clone(), b.detach().clone(), sc.get_scale()))
+        res[kind] = snaps
+    for (ea, eb, es), (ta, tb, ts) in zip(res["ebc"], res["torch"]):
+        assert es == ts
+        torch.testing.assert_close(ea, ta, rtol=1e-6, atol=1e-9)
+        torch.testing.assert_close(eb, tb, rtol=1e-6, atol=1e-9)
+    assert torch.equal(res["ebc"][0][0], res["ebc"][1][0])           # group 0 untouched at the skipped step

@@ -71,14 +71,15 @@ for what in "$@"; do
       tail -1 $O/${TAG}_ptrace.log | cut -c1-300
       i=0
       for ctrs in "FETCH_SIZE GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES" \
-                  "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+                  "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" \
+                  "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
         i=$((i+1))
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctrs -d $O/${TAG}_pmc$i -o run -- \
           python3 $B > $O/${TAG}_pmc$i.log 2>&1) || { tail -30 $O/${TAG}_pmc$i.log; exit 1; }
       done
-      python3 $R/tools/pmc_step.py --classes $O/${TAG}_classes.json $O/${TAG}_pmc1 $O/${TAG}_pmc2 \
+      python3 $R/tools/pmc_step.py --classes $O/${TAG}_classes.json $O/${TAG}_pmc1 $O/${TAG}_pmc2 $O/${TAG}_pmc3 \
         --json $O/${TAG}_pmc_step.json > $O/${TAG}_pmc_step.txt || { echo "pmc_step failed"; exit 1; }
-      rm -rf $O/${TAG}_pmc1 $O/${TAG}_pmc2
+      rm -rf $O/${TAG}_pmc1 $O/${TAG}_pmc2 $O/${TAG}_pmc3
       head -12 $O/${TAG}_pmc_step.txt | cut -c1-400 ;;
     lab:*)
       # a lab binary (tools/lab/bin/NAME, built here), its stdout -> gpurun_out/TAG_NAME.txt; LAB_ARGS passes arguments

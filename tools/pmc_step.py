@@ -10,8 +10,14 @@ launch order.  Per class: the mean of every counter and of the dispatch duration
   fetch_bytes  = FETCH_SIZE x 1024 x 2   (gfx950 FETCH_SIZE counts half of wide coalesced reads, MI355X_MICROARCH.md §HBM)
   write_bytes  = WRITE_SIZE x 1024
   traffic      = fetch_bytes + write_bytes          (L2 <-> fabric bytes per launch: MALL hits included)
-  mfma_busy    = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 256 CUs x 4 SIMDs)
-  clock_ghz    = GRBM_GUI_ACTIVE / 8 / duration (the effective clock of that dispatch)
+  mfma_busy    = SQ_VALU_MFMA_BUSY_CYCLES / (duration x 2.4 GHz x 1024 SIMDs): the fraction of the launch's SIMD
+                 cycles the matrix pipes were busy, at the 2.4 GHz maximum clock (the chip runs at or below it, so
+                 this is a lower bound; SQ_VALU_MFMA_BUSY_CYCLES counts 16 per v_mfma_f32_16x16x32_f16)
+  mfma_busy_sq = SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CYCLES / 32 x 1024): the same over the cycles the shader
+                 engines held waves (32 SEs; also low for a launch that leaves CUs idle)
+  sq_clock_ghz = SQ_BUSY_CYCLES / 32 / duration (<= 2.4; r03's GRBM_GUI_ACTIVE / 8 read up to 6.9 GHz on launches
+                 shorter than the counter window, so it is no longer used)
+  valu_per_mfma= SQ_INSTS_VALU / SQ_INSTS_MFMA (third pass)
   l2_hit       = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
 """
 import argparse
@@ -89,10 +95,15 @@ def main():
             r["write_bytes"] = m["WRITE_SIZE"] * 1024
         if "fetch_bytes" in r and "write_bytes" in r:
             r["traffic_bytes_per_launch"] = r["fetch_bytes"] + r["write_bytes"]
-        if m.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-            r["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 256 * 4)
-        if m.get("GRBM_GUI_ACTIVE") and c["dur_n"]:
-            r["clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8 / (c["dur_sum"] / c["dur_n"])
+        dur_ns = c["dur_sum"] / c["dur_n"] if c["dur_n"] else 0.0
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and dur_ns:
+            r["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (dur_ns * 1e-9 * 2.4e9 * 1024)
+        if m.get("SQ_BUSY_CYCLES") and dur_ns:
+            r["sq_clock_ghz"] = m["SQ_BUSY_CYCLES"] / 32 / dur_ns
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+                r["mfma_busy_sq"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["SQ_BUSY_CYCLES"] / 32 * 1024)
+        if m.get("SQ_INSTS_MFMA"):
+            r["valu_per_mfma"] = m.get("SQ_INSTS_VALU", 0.0) / m["SQ_INSTS_MFMA"]
         if m.get("TCC_HIT_sum") is not None and m.get("TCC_MISS_sum") is not None:
             r["l2_hit"] = m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
         out.append(r)
