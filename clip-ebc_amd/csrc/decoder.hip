@@ -11,9 +11,12 @@
 //   xpad   [B][Hp][Wp][C] T            zero-padded NHWC conv input (Hp = H+2, Wp >= W+2, see geo)
 //   z      [B*H*W][N] T                conv output before BatchNorm
 //   y      [B*H*W][C] T                block output (the projection GEMM's A operand)
-//   xT3    [3][C][Qs] T                kx-shifted transposed copies for the weight gradient:
-//                                      xT3[kx][c][G + q] = xpad[q + kx - 1][c] (0 outside)
-//   dzT    [N][Qs] T                   transposed padded dz (0 outside the interior)
+//   xT3    [3][C][Qs] T                kx-shifted transposed row-padded copies for the weight gradient:
+//                                      xT3[kx][c][b*Pimg + yp*W + x] = x[b][yp - 1][x + kx - 1] (0 outside),
+//                                      Pimg = (H + 2) * W rounded up to 8 and >= HWp (a zero row above and below
+//                                      every image, zeros to the next image)
+//   dzT    [N][Qs] T                   transposed dz over the weight gradient's K: column b*HWp + r = interior
+//                                      pixel r of image b (HWp = H*W rounded up to 8; 0 beyond H*W)
 //   dw     [N][C][3][3] f32            weight gradient, nn.Conv2d layout
 // Every kernel is HBM-bound elementwise / transpose work (4-wide vector accesses).
 //
@@ -80,29 +83,35 @@ __device__ __forceinline__ float4 relu4(float4 a) {
     return make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
 }
 
-// Decoder geometry shared by every entry point (the transposed images' guards and row stride let the
-// weight-gradient GEMM run its K loop over whole 64-pixel slabs with 16-B aligned rows).
+// Decoder geometry shared by every entry point.  MODE 1 (convs, data gradient): zero-padded NHWC images
+// [B][Hp][Wp][C], Wp a multiple of 8 (16-B aligned tap shifts).  MODE 2 (weight gradient): its K runs over the
+// interior pixels only -- B*H*W of them, each image's rounded up to HWp = a multiple of 8 (and >= 64) so a 16-B K
+// chunk never spans two images -- (r03's K loop ran over the padded rows of pitch Wp: 12.5 % of its MFMA work multiplied zeros
+// at 28x28); the kx shift of a tap is baked into three transposed copies of the input, the ky shift is a row offset
+// into their row-padded images (Pimg >= (H + 2) * W positions each).  Kq = the GEMM's K (B*HWp rounded up to 64),
+// Qs = the row stride of dz^T and of the x^T copies (room for the K tail's reads past the last image).
 struct Geo {
-    int B, H, W, C, Hp, Wp, G, kpi, bk;
-    long Q, Qs;
+    int B, H, W, C, Hp, Wp, HWp;
+    long Q, Kq, Pimg, Qs;
 };
-Geo make_geo(int dtype, int B, int H, int W, int C) {
+Geo make_geo(int /*dtype*/, int B, int H, int W, int C) {
     Geo g;
     g.B = B; g.H = H; g.W = W; g.C = C;
     g.Hp = H + 2;
-    g.Wp = std::max(((W + 2 + 7) / 8) * 8, 32);      // >= bk/2: a slab overshoots into pad rows only
-    g.bk = dtype == EBC_F32 ? 32 : 64;
-    g.G = ((g.Wp + 1 + 63) / 64) * 64;
+    g.Wp = std::max(((W + 2 + 7) / 8) * 8, 32);
     g.Q = (long)B * g.Hp * g.Wp;
-    g.kpi = (H * g.Wp + g.bk - 1) / g.bk;
-    g.Qs = ((g.G + g.Q + g.bk + g.Wp + 63) / 64) * 64;
+    g.HWp = std::max(((H * W + 7) / 8) * 8, 64);        // >= 64: a 64-wide K tile crosses at most one image edge
+    g.Kq = (((long)B * g.HWp + 63) / 64) * 64;
+    g.Pimg = ((std::max((long)(H + 2) * W, (long)g.HWp) + 7) / 8) * 8;    // image bases 16-B aligned, >= HWp
+    const long tail = (long)(B + 2 + 64 / g.HWp) * g.Pimg + g.HWp + 2L * W + 64;
+    g.Qs = ((std::max(g.Kq, tail) + 63) / 64) * 64;
     return g;
 }
 struct DGeo {               // device copy
-    int B, H, W, C, Hp, Wp, G;
-    long Q, Qs;
+    int B, H, W, C, Hp, Wp, HWp;
+    long Q, Kq, Pimg, Qs;
 };
-DGeo dgeo(const Geo& g) { return DGeo{g.B, g.H, g.W, g.C, g.Hp, g.Wp, g.G, g.Q, g.Qs}; }
+DGeo dgeo(const Geo& g) { return DGeo{g.B, g.H, g.W, g.C, g.Hp, g.Wp, g.HWp, g.Q, g.Kq, g.Pimg, g.Qs}; }
 
 // padded position q -> interior pixel index p = (b*H + y)*W + x, or -1
 __device__ __forceinline__ long interior(const DGeo& g, long q) {
@@ -608,9 +617,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_flat_kernel(const T* __restr
 // (rows of channels) and the transposed image (rows of positions) are written with contiguous rows.
 constexpr int TQ = 64, TC = 64;
 
-// dz = gamma*rstd * (g - mean(g) - xhat * mean(g*xhat)) -> dzpad [Q][C] and dzT [C][Qs].  A 64-pixel x
-// 64-channel tile per block: the per-channel factors staged in LDS once, every thread's 16 channels of
-// gy / mask / z loaded up front (row-clamped: no load behind a branch), 16-B stores both ways.
+// dz = gamma*rstd * (g - mean(g) - xhat * mean(g*xhat)) -> dzpad [Q][C] (interior pixels) and dzT [C][Kq] (the
+// weight gradient's K columns, 0 past each image's H*W).  A 64-column x 64-channel tile per block: the per-channel
+// factors staged in LDS once, every thread's 16 channels of gy / mask / z loaded up front (row-clamped: no load
+// behind a branch), 16-B stores both ways.  Blocks past Kq / 64 write dzpad's zero border (the data-gradient
+// conv reads it as its zero padding).
 template <class T, bool HAS_MY>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ gy, const T* __restrict__ my,
                                                            const T* __restrict__ z, const float* __restrict__ mean,
@@ -623,11 +634,25 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     __shared__ float sm[TQ][TC + 1];
     __shared__ float cf[7][TC];                   // gamma*rstd, mean(g), mean(g*xhat), mean, rstd, scale, shift
     const int t = threadIdx.x;
-    const long j0 = (long)blockIdx.x * TQ;
     const int c0 = blockIdx.y * TC;
     const int ql = t >> 2, cl = (t & 3) * 16;
-    const long q = j0 + ql - g.G;
-    const long p = interior(g, q);
+    const long nkb = g.Kq / TQ;
+    if (blockIdx.x >= nkb) {                      // dzpad's border: zeros
+        const long q = (blockIdx.x - nkb) * TQ + ql;
+        if (q < g.Q && interior(g, q) < 0) {
+            const float z16[16] = {};
+            st8(dzpad + q * g.C + c0 + cl, z16);
+            st8(dzpad + q * g.C + c0 + cl + 8, z16 + 8);
+        }
+        return;
+    }
+    const long j0 = (long)blockIdx.x * TQ;
+    const long j = j0 + ql;                       // K column: image b, interior pixel r
+    const int hw = g.H * g.W;
+    const long bimg = j / g.HWp;
+    const int r = (int)(j - bimg * g.HWp);
+    const long p = (bimg < g.B && r < hw) ? bimg * hw + r : -1;
+    const long q = p >= 0 ? (bimg * g.Hp + r / g.W + 1) * g.Wp + r % g.W + 1 : -1;
     const long off = (p >= 0 ? p : 0) * g.C + c0 + cl;
     float gv[16], zv[16], mv[HAS_MY ? 16 : 1];
 #pragma unroll
@@ -652,7 +677,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
         v[i] = p >= 0 ? cf[0][cc] * (gg - cf[1][cc] - (zv[i] - cf[3][cc]) * cf[4][cc] * cf[2][cc]) : 0.f;
         sm[ql][cc] = v[i];
     }
-    if (q >= 0 && q < g.Q) {
+    if (q >= 0) {
         st8(dzpad + q * g.C + c0 + cl, v);
         st8(dzpad + q * g.C + c0 + cl + 8, v + 8);
     }
@@ -668,43 +693,41 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     }
 }
 
-// xT3[kx][c][G + q] = xpad[q + kx - 1][c]  (xpad is zero outside the interior; 0 beyond [0, Q))
+// xT3[kx][c][pos] = xpad[(b * Hp + yp) * Wp + x + kx][c] for pos = b * Pimg + yp * W + x (b < B), else 0: every
+// position of a row (the zero guard rows, the tail past the last image included).  A 64-position x 64-channel tile
+// per block: the three taps' 16-B loads all issued first, then one LDS transpose per tap (both sides 16-B vectors).
 template <class T>
 __global__ __launch_bounds__(256) void transpose3_kernel(const T* __restrict__ xpad, T* __restrict__ xT3, DGeo g)
 {
-    __shared__ float sm[TQ + 2][TC + 1];
+    __shared__ float sm[TQ][TC + 1];
     const int t = threadIdx.x;
     const long j0 = (long)blockIdx.x * TQ;
     const int c0 = blockIdx.y * TC;
-    constexpr int NE = (TQ + 2) * (TC / 4), PER = (NE + 255) / 256;
-    float4 v[PER];
+    const int ql = t >> 2, cl = (t & 3) * 16;
+    const long pos = j0 + ql;
+    const long b = pos / g.Pimg;
+    const int rem = (int)(pos - b * g.Pimg), yp = rem / g.W, x = rem - yp * g.W;
+    const bool valid = b < g.B && yp < g.Hp;
+    const long q0 = valid ? (b * g.Hp + yp) * g.Wp + x : 0;
+    float v[3][16];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {                // all loads in flight before the LDS writes (clamped
-        const int e = min(t + 256 * k, NE - 1), ql = e / (TC / 4), cl = (e % (TC / 4)) * 4;   // addresses,
-        const long q = j0 - g.G + ql - 1;                                                       // no branch)
-        v[k] = ld4(xpad + std::min<long>(std::max<long>(q, 0), g.Q - 1) * g.C + c0 + cl);
+    for (int kx = 0; kx < 3; ++kx) {
+        ld8(xpad + (q0 + kx) * g.C + c0 + cl, v[kx]);
+        ld8(xpad + (q0 + kx) * g.C + c0 + cl + 8, v[kx] + 8);
     }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int e = min(t + 256 * k, NE - 1), ql = e / (TC / 4);
-        const long q = j0 - g.G + ql - 1;
-        if (q < 0 || q >= g.Q) v[k] = f4(0.f);
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int e = t + 256 * k, ql = e / (TC / 4), cl = (e % (TC / 4)) * 4;
-        if (e < NE) { sm[ql][cl] = v[k].x; sm[ql][cl + 1] = v[k].y; sm[ql][cl + 2] = v[k].z; sm[ql][cl + 3] = v[k].w; }
-    }
-    __syncthreads();
     const int cr = t >> 2, jl = (t & 3) * 16;
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
-        T* dst = xT3 + ((size_t)kx * g.C + c0 + cr) * g.Qs + j0 + jl;
+        if (kx) __syncthreads();                  // every thread done reading the previous tap's tile
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int s = jl + 4 * k + kx;
-            st4(dst + 4 * k, make_float4(sm[s][cr], sm[s + 1][cr], sm[s + 2][cr], sm[s + 3][cr]));
-        }
+        for (int i = 0; i < 16; ++i) sm[ql][cl + i] = valid ? v[kx][i] : 0.f;
+        __syncthreads();
+        float w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = sm[jl + i][cr];
+        T* dst = xT3 + ((size_t)kx * g.C + c0 + cr) * g.Qs + j0 + jl;
+        st8(dst, w);
+        st8(dst + 8, w + 8);
     }
 }
 
@@ -883,7 +906,7 @@ extern "C" int ebc_dec_geometry(int dtype, int B, int H, int W, int C, long* out
 {
     if (B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || !out) return EBC_E_ARG;
     const Geo g = make_geo(dtype, B, H, W, C);
-    out[0] = g.Hp; out[1] = g.Wp; out[2] = g.G; out[3] = g.kpi; out[4] = g.Q; out[5] = g.Qs;
+    out[0] = g.Hp; out[1] = g.Wp; out[2] = g.HWp; out[3] = g.Kq; out[4] = g.Q; out[5] = g.Qs;
     return EBC_OK;
 }
 
@@ -893,7 +916,7 @@ extern "C" size_t ebc_dec_workspace_bytes(int dtype, int B, int H, int W, int C,
     const int M = B * H * W;
     size_t need = ebc::conv_gemm_workspace_bytes(dtype, 1, M, N, 9 * C);
     need = std::max(need, ebc::conv_gemm_workspace_bytes(dtype, 1, M, C, 9 * N));
-    need = std::max(need, ebc::conv_gemm_workspace_bytes(dtype, 2, N, 9 * C, B * g.kpi * g.bk));
+    need = std::max(need, ebc::conv_gemm_workspace_bytes(dtype, 2, N, 9 * C, (int)g.Kq));
     const int rpb = std::min(bn_partial_rows(C), bn_partial_rows(N));
     const long nb = std::max(((long)M + 63) / 64, ((long)M + rpb - 1) / rpb);
     need = std::max(need, CONV_WS_STATS_OFFSET + (size_t)nb * 2 * std::max(C, N) * 4);
@@ -918,7 +941,7 @@ extern "C" int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, 
 {
     if (!xpad || !weight || !out || C % 64 || N % 64 || (colsum && add_gy) || (!add_gy != !add_y)) return EBC_E_ARG;
     const Geo g = make_geo(dtype, B, H, W, C);
-    ebc::ConvGeom cg{H, W, C, g.Hp, g.Wp, 0, 0, 0};
+    ebc::ConvGeom cg{H, W, C, g.Hp, g.Wp, 0, 0, 0, B};
     const int M = B * H * W;
     int tiles = 0;
     const hipStream_t st = (hipStream_t)stream;
@@ -937,9 +960,8 @@ extern "C" int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, fl
 {
     if (!dzT || !xT3 || !dw || C % 64 || N % 64) return EBC_E_ARG;
     const Geo g = make_geo(dtype, B, H, W, C);
-    ebc::ConvGeom cg{H, W, C, g.Hp, g.Wp, g.kpi, g.Qs, g.G};
-    return ebc::conv_gemm(dtype, 2, 0, dzT, xT3, dw, cg, N, 9 * C, B * g.kpi * g.bk, ws, wsb, nullptr,
-                          (hipStream_t)stream);
+    ebc::ConvGeom cg{H, W, C, g.Hp, g.Wp, g.HWp, g.Qs, g.Pimg, B};
+    return ebc::conv_gemm(dtype, 2, 0, dzT, xT3, dw, cg, N, 9 * C, (int)g.Kq, ws, wsb, nullptr, (hipStream_t)stream);
 }
 
 extern "C" int ebc_bn_finalize(const double* colsum, double count, float eps, float momentum, const float* gamma,
@@ -1013,7 +1035,7 @@ extern "C" int ebc_bn_bwd_apply(int dtype, const void* gy, const void* mask_y, c
         return EBC_E_ARG;
     const Geo g = make_geo(dtype, B, H, W, C);
     const DGeo d = dgeo(g);
-    const dim3 grid((unsigned)(g.Qs / TQ), (unsigned)(C / TC));
+    const dim3 grid((unsigned)(g.Kq / TQ + (g.Q + TQ - 1) / TQ), (unsigned)(C / TC));
     if (mask_y) {
         EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), grid, dim3(256), 0, (hipStream_t)stream,
                                                    (const T*)gy, (const T*)mask_y, (const T*)z, mean, rstd, scale,

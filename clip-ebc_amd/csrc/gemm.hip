@@ -43,11 +43,12 @@ struct GemmArgs {
     //  MODE 1 (forward / data gradient): A row m = output pixel (b, y, x) of a [B][cHp][cWp][cC]
     //    zero-padded NHWC image, K = 9 taps x cC (tap-major), k-tile kt reads the row shifted by
     //    tap (ky, kx): ((ky-1)*cWp + kx-1) pixels;  B = weights [N][3][3][cC].
-    //  MODE 2 (weight gradient): A = dz^T [M][cQs], B = three kx-shifted copies x^T [3][cC][cQs] of
-    //    the padded image (x_kx^T[c][cG + q] = x[q + kx - 1][c]), row n = (c, ky, kx) (the nn.Conv2d
-    //    weight layout) starts at (ky-1)*cWp; K runs over the interior image rows, kpi k-tiles per image.
-    int cH = 0, cW = 0, cC = 0, cHp = 0, cWp = 0, kpi = 0;
-    long cQs = 0, cG = 0;
+    //  MODE 2 (weight gradient): K runs over the interior pixels (column b*cHWp + r: pixel r < H*W of image b).
+    //    A = dz^T [M][cQs]; B = three kx-shifted copies x^T [3][cC][cQs] of the row-padded input images
+    //    (x_kx^T[c][b*cPimg + yp*cW + x] = x[b][yp-1][x+kx-1]); row n = (c, ky, kx) (the nn.Conv2d weight layout)
+    //    starts at ky*cW, and a K chunk at column q = b*cHWp + r reads position b*cPimg + r of it.
+    int cH = 0, cW = 0, cC = 0, cHp = 0, cWp = 0, cHWp = 0;
+    long cQs = 0, cPimg = 0;
     float* stats = nullptr;  // EPI_STATS: [ceil(M/BM)][2][N] per-tile column sums / sums of squares
     int group_m = 0;         // > 1: tiles ordered in groups of group_m tile rows, column-major inside a group
     const void* aux2 = nullptr;   // EPI_ADD_RELU_GRAD: ReLU output y (mask y > 0): C = acc + gy * (y > 0)
@@ -241,6 +242,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
     // per-lane source rows for the LDS-DMA staging (fixed across k; the k-tile offset is added by stage())
     const T* src[NLD];
     bool isa[NLD];
+    // MODE 2: each piece's 16-B chunk index inside its row (the lane's K offset in the tile / (16 / EB)), 4 bits a
+    // piece in one register (r04: a K offset per piece made the 256x192 weight-gradient tiles spill)
+    unsigned cpk = 0;
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
         const bool tail = TAIL && i >= NLDF;
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 const int b = gr / hw, r = gr - b * hw, y = r / g.cW, x = r - y * g.cW;
                 base = A + ((size_t)(b * g.cHp + y + 1) * g.cWp + x + 1) * g.cC;
             } else if constexpr (MODE == 2) {
-                base = A + (size_t)gr * g.cQs + g.cG;
+                base = A + (size_t)gr * g.cQs;
             } else {
                 if (g.a_rpg) gr = (gr / g.a_rpg) * g.a_gstride + g.a_goff + gr % g.a_rpg;
                 base = A + (size_t)gr * K;
@@ -269,12 +273,14 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             const int n = n0 + (MODE == 0 ? bcol<WN, TN>(row - BM) : row - BM);
             if constexpr (MODE == 2) {
                 const int cc = n / 9, t = n - 9 * cc, ky = t / 3, kx = t - 3 * ky;   // nn.Conv2d [o][c][ky][kx]
-                base = Bw + (size_t)(kx * g.cC + cc) * g.cQs + g.cG + (long)(ky - 1) * g.cWp;
+                base = Bw + (size_t)(kx * g.cC + cc) * g.cQs + (long)ky * g.cW;
             } else {
                 base = Bw + (size_t)n * K;
             }
         }
-        src[i] = base + c * (16 / EB) + (tail ? (lane & 3) * (4 / EB) : 0);
+        const int ko = c * (16 / EB) + (tail ? (lane & 3) * (4 / EB) : 0);
+        src[i] = base + ko;
+        if constexpr (MODE == 2) cpk |= (unsigned)(ko / (16 / EB)) << (4 * i);
     }
     auto stage_pieces = [&](int buf, int kt) {
         const int ktg = ktbase + kt;
@@ -285,23 +291,40 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             oa = ((long)(ky - 1) * g.cWp + (kx - 1)) * g.cC + (long)(ktg - tap * tpc) * BK;
             ob = (long)ktg * BK;
         } else if constexpr (MODE == 2) {
-            const int img = ktg / g.kpi;
-            oa = ob = (long)img * g.cHp * g.cWp + g.cWp + (long)(ktg - img * g.kpi) * BK;
+            oa = ob = (long)ktg * BK;
         } else {
             oa = ob = (long)ktg * BK;
         }
+        // MODE 2: a B chunk at K column q sits at position b * cPimg + (q - b * cHWp) of its x^T row (image b = q / cHWp).
+        // cHWp >= 64 (conv_gemm), so a tile of BK <= 64 columns starting in image b0 (wave-uniform) ends in b0 or b0 + 1:
+        // a lane's chunk is in b0 + 1 when its column offset reaches the boundary d (a multiple of the chunk width)
+        int b0 = 0, dch = 0;
+        long shift0 = 0, dP = 0;
+        if constexpr (MODE == 2) {
+            b0 = (int)(ob / g.cHWp);
+            dch = (int)(((long)(b0 + 1) * g.cHWp - ob) / (16 / EB));
+            dP = g.cPimg - g.cHWp;
+            shift0 = ob + (long)b0 * dP;
+        }
+        auto piece = [&](int i) -> const T* {
+            if constexpr (MODE == 2) {
+                if (isa[i]) return src[i] + oa;
+                const int c = (int)((cpk >> (4 * i)) & 15u);
+                return src[i] + shift0 + (c >= dch ? dP : 0);
+            } else {
+                return src[i] + (isa[i] ? oa : ob);
+            }
+        };
         char* dst = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < NLDF; ++i) {
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src[i] + (isa[i] ? oa : ob)),
-                EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(i),
+                                             EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < NT4; ++j) {
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src[NLDF + j] + (isa[NLDF + j] ? oa : ob)),
-                EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(NLDF + j),
+                                             EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, 0);
         }
     };
     // the compute waves stage the ring themselves unless loader waves do
@@ -1087,7 +1110,6 @@ int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream
     const int BK = 128 / E::BYTES;
     const TileCfg* c = find_cfg(cfg);
     if (g.N % c->bn || g.K % BK) return EBC_E_UNSUPPORTED;
-    if (mode == 2) g.kpi *= (128 / E::BYTES) / BK;             // geometry counts 128-B k-tiles
     if (planned && wp.partials) {
         if (!ws || wsb < wplan_ws(wp, g.M, g.N)) return EBC_E_ARG;
         g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);
@@ -1170,10 +1192,14 @@ int conv_gemm(int dtype, int mode, int epi, const void* A, const void* B, void* 
     if (M <= 0 || N <= 0 || K <= 0 || K % bk || N % 64 || !A || !B || !C || (mode != 1 && mode != 2)) return EBC_E_ARG;
     GemmArgs g{A, B, C, nullptr, nullptr, const_cast<void*>(gy), M, N, K};
     g.aux2 = y;
-    g.cH = geo.H; g.cW = geo.W; g.cC = geo.C; g.cHp = geo.Hp; g.cWp = geo.Wp; g.kpi = geo.kpi;
-    g.cQs = geo.Qs; g.cG = geo.G;
+    g.cH = geo.H; g.cW = geo.W; g.cC = geo.C; g.cHp = geo.Hp; g.cWp = geo.Wp;
     if (mode == 1 && geo.C % bk) return EBC_E_UNSUPPORTED;
-    if (mode == 2 && geo.kpi > 0) g.kalg = (K / (geo.kpi * bk)) * geo.H * geo.W;     // B * H * W interior pixels
+    if (mode == 2) {
+        // a 16-B K chunk (8 16-bit / 4 f32 columns) must stay inside one image
+        if (geo.HWp < 64 || geo.HWp % 8 || geo.Pimg < (long)geo.HWp || geo.Qs < (long)K) return EBC_E_ARG;
+        g.cHWp = geo.HWp; g.cQs = geo.Qs; g.cPimg = geo.Pimg;
+        g.kalg = geo.nimg * geo.H * geo.W;                                    // B * H * W interior pixels
+    }
     if (epi == EPI_STATS) {
         if (!ws || wsb < conv_gemm_workspace_bytes(dtype, mode, M, N, K)) return EBC_E_ARG;
         g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_CNT_BYTES);

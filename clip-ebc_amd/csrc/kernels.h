@@ -25,9 +25,10 @@ size_t gemm_workspace_bytes(int dtype, int M, int N, int K);
 // implicit-GEMM 3x3 convolution geometry (gemm.hip MODE 1 / MODE 2)
 struct ConvGeom {
     int H, W, C;      // output image (stride 1, pad 1), channels per tap
-    int Hp, Wp;       // padded operand image geometry (MODE 1: NHWC [B][Hp][Wp][C]; MODE 2: transposed rows)
-    int kpi;          // MODE 2: k-tiles per image
-    long Qs, G;       // MODE 2: row stride and leading guard (elements) of the transposed images
+    int Hp, Wp;       // MODE 1: padded NHWC operand image [B][Hp][Wp][C]
+    int HWp;          // MODE 2: K columns per image (H*W rounded up to 8)
+    long Qs, Pimg;    // MODE 2: row stride of dz^T / x^T (elements), positions per row-padded x^T image ((H+2)*W)
+    int nimg;         // images (B): the algorithmic K of a weight gradient is nimg * H * W
 };
 // mode 1: C[M = B*H*W, N] = conv(A = padded NHWC image, B = weights [N][9*C]), epi 0 store / 4 + BN stats
 //         (per-tile column partials at ws + 16 KiB: [stats_tiles][2][N]);

@@ -45,7 +45,10 @@ def _block(C):
 
 @pytest.mark.parametrize("dtype,B,h,C,up", [(torch.float32, 2, 14, 768, 2), (torch.float16, 2, 14, 768, 2),
                                             (torch.bfloat16, 2, 14, 768, 2), (torch.float32, 3, 7, 128, 1),
-                                            (torch.float16, 3, 10, 192, 2)])
+                                            (torch.float16, 3, 10, 192, 2),
+                                            # H = W = 14: 196 pixels per image, the weight gradient's K padded to 200
+                                            # per image (a 16-B K chunk never spans two images), K tail past 5 images
+                                            (torch.bfloat16, 5, 7, 128, 2)])
 def test_decoder_train_fwd_bwd(dtype, B, h, C, up):
     from ebc_amd.model import _DecoderFn
     blk = _block(C)

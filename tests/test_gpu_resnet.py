@@ -171,7 +171,7 @@ def test_bench_shape_tile_configs():
     assert L.ebc_gemm_tile_config(bf, 25088, 1024, 2048, out) == 7          # projection
     assert L.ebc_gemm_tile_config(bf, 25088, 2048, 1024, out) == 7          # projection dX
     assert L.ebc_conv_tile_config(bf, 1, 25088, 2048, 9 * 2048, out) == 7   # conv2 fwd / dgrad
-    assert L.ebc_conv_tile_config(bf, 2, 2048, 9 * 2048, 8 * 56 * 64, out) == 3   # conv2 wgrad (K = B*kpi*64)
+    assert L.ebc_conv_tile_config(bf, 2, 2048, 9 * 2048, 8 * 56 * 56, out) == 3   # conv2 wgrad (K = B*H*W)
 
 
 def test_bottleneck_bench_shape_bf16():

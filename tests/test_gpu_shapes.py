@@ -150,9 +150,10 @@ def test_decoder_at_bench_batch(dname, B):
     C, h = 768, 14
     M = B * 784
     assert conv_cfg(dt, 1, M, C, 9 * C)[0] == 3
-    geo = (ctypes.c_long * 6)()                         # {Hp, Wp, G, kpi, Q, Qs}: K of the wgrad = B * kpi * 64
+    geo = (ctypes.c_long * 6)()                         # {Hp, Wp, HWp, Kq, Q, Qs}: K of the wgrad = Kq
     _lib.check(_lib.lib().ebc_dec_geometry(_lib.dtype_code(dt), B, 2 * h, 2 * h, C, geo), "ebc_dec_geometry")
-    cfg2, (_, _, splits) = conv_cfg(dt, 2, C, 9 * C, B * geo[3] * 64)
+    assert geo[3] == B * 784                            # the interior pixels only (r03: B * 14 * 64 padded)
+    cfg2, (_, _, splits) = conv_cfg(dt, 2, C, 9 * C, geo[3])
     assert cfg2 == 3 and splits == 2, (cfg2, splits)
     blk = _block(C)
     g = torch.Generator(device="cuda").manual_seed(B)
