@@ -179,6 +179,30 @@ __device__ __forceinline__ void touch_issue(const TouchList& t, TouchSink& s)
 }
 __device__ __forceinline__ void touch_wait(const TouchSink& s) { asm volatile("" :: "v"(s.a), "v"(s.b)); }
 
+// Softmax row arithmetic in the swapped layout (a query's 256 keys on the lanes fr, fr + 16, fr + 32, fr + 48, four
+// per lane per 16-key tile).  r03's PMC put the forward at 9.2 VALU instructions per MFMA; per score it issued a
+// canonicalising v_max before every fmaxf (IEEE maxNum), one v_fma and one v_add, and per row reduction two
+// ds_bpermute round trips with their lane-index arithmetic.  Here: v_maximum3_f32 (IEEE maximum: no canonicalise, 2
+// scores an instruction), packed f32 FMA / add (v_pk_fma_f32, v_pk_add_f32: 2 scores an instruction) and the row
+// reductions across the four 16-lane rows by v_permlane16_swap / v_permlane32_swap (each lane receives its own and its
+// partner's value, in either order, so max / + of the pair is the same on both lanes).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+__device__ __forceinline__ float rows_max(float x) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __builtin_elementwise_maximum(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __builtin_elementwise_maximum(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rows_sum(float x) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // ------------------------------------------------------------------------------ forward
 // QT query tiles of 16 per wave: every K row fragment and V column fragment read from LDS feeds QT MFMAs (the LDS
 // reads per query halve at QT = 2; with one tile per wave the forward was bound by re-reading K and V per 16 queries)
@@ -247,7 +271,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     float mx[QT], sum[QT];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
-        mx[t] = -INFINITY;
+        float m0 = -INFINITY, m1 = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt) {
             if (kt < nkt) {
@@ -256,22 +280,29 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
                     for (int i = 0; i < 4; ++i)
                         if (16 * kt + 4 * fg + i >= L) s[t][kt][i] = -INFINITY;
                 }
-                mx[t] = fmaxf(mx[t], fmaxf(fmaxf(s[t][kt][0], s[t][kt][1]), fmaxf(s[t][kt][2], s[t][kt][3])));
+                m0 = max3f(m0, s[t][kt][0], s[t][kt][1]);
+                m1 = max3f(m1, s[t][kt][2], s[t][kt][3]);
             }
         }
-        mx[t] = fmaxf(mx[t], __shfl_xor(mx[t], 16, 64));
-        mx[t] = fmaxf(mx[t], __shfl_xor(mx[t], 32, 64));
+        mx[t] = rows_max(__builtin_elementwise_maximum(m0, m1));
         const float mc = mx[t] * c2;
-        sum[t] = 0.f;
+        const f32x2 c2v = {c2, c2}, mcv = {-mc, -mc};
+        f32x2 acc = {0.f, 0.f};
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt) {
             if (kt < nkt) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) { s[t][kt][i] = __builtin_amdgcn_exp2f(fmaf(s[t][kt][i], c2, -mc)); sum[t] += s[t][kt][i]; }
+                for (int i = 0; i < 4; i += 2) {
+                    f32x2 e = __builtin_elementwise_fma(f32x2{s[t][kt][i], s[t][kt][i + 1]}, c2v, mcv);
+                    e.x = __builtin_amdgcn_exp2f(e.x);
+                    e.y = __builtin_amdgcn_exp2f(e.y);
+                    s[t][kt][i] = e.x;
+                    s[t][kt][i + 1] = e.y;
+                    acc += e;
+                }
             }
         }
-        sum[t] += __shfl_xor(sum[t], 16, 64);
-        sum[t] += __shfl_xor(sum[t], 32, 64);
+        sum[t] = rows_sum(acc.x + acc.y);
     }
 
     f32x4 o[QT][HD / 16];
@@ -445,6 +476,31 @@ __device__ __forceinline__ float attn_delta_row(const typename E::T* drow, const
     return (p[0] + p[1]) + (p[2] + p[3]);
 }
 
+// delta of one query for the one-workgroup backward: 4 lanes a query (16 columns each, v_dot2 products accumulated in
+// f32), the quad's partial sums added by DPP.  Its bits differ from attn_delta_row's; only this kernel uses it, for
+// both the dQ and the dK / dV products, so they agree with each other.  (r03: one lane a query, 64 conversions and 32
+// FMAs per row on 4 of the 16 waves, ahead of the workgroup's first barrier.)
+template <class E>
+__device__ __forceinline__ float attn_delta_quad(const typename E::T* drow, const typename E::T* orow) {
+    const typename E::Frag d0 = load8<E>(drow), d1 = load8<E>(drow + 8), o0 = load8<E>(orow), o1 = load8<E>(orow + 8);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        if constexpr (std::is_same<E, EF16>::value) {
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            acc = __builtin_amdgcn_fdot2(h2{d0[j], d0[j + 1]}, h2{o0[j], o0[j + 1]}, acc, false);
+            acc = __builtin_amdgcn_fdot2(h2{d1[j], d1[j + 1]}, h2{o1[j], o1[j + 1]}, acc, false);
+        } else {
+            typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+            acc = __builtin_amdgcn_fdot2_f32_bf16(b2{d0[j], d0[j + 1]}, b2{o0[j], o0[j + 1]}, acc, false);
+            acc = __builtin_amdgcn_fdot2_f32_bf16(b2{d1[j], d1[j + 1]}, b2{o1[j], o1[j + 1]}, acc, false);
+        }
+    }
+    acc += __builtin_amdgcn_update_dpp(0.f, acc, 0xB1, 0xF, 0xF, false);      // quad_perm [1, 0, 3, 2]
+    acc += __builtin_amdgcn_update_dpp(0.f, acc, 0x4E, 0xF, 0xF, false);      // quad_perm [2, 3, 0, 1]
+    return acc;
+}
+
 template <class E, int NWV, int LFIX>
 __device__ __forceinline__ void attn_bwd_dkv_body(int bid, const typename E::T* __restrict__ qkv, const typename E::T* __restrict__ dout,
                                                   const typename E::T* __restrict__ out, const float* __restrict__ lse,
@@ -611,17 +667,18 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     rows_fetch<E, NWV>(fv, base + 2 * D, D3, L);
     rows_fetch<E, NWV>(fq, base, D3, L);
     rows_fetch<E, NWV>(fd, dob, D, L);
-    const int tq = threadIdx.x;
+    const int qd = threadIdx.x >> 2, qj = threadIdx.x & 3;    // lse / delta of query qd, a quarter of its row
     float lsv = INFINITY, dlv = 0.f;                            // padding queries: p = 0, delta 0
-    if (tq < L) {
-        lsv = lse[((size_t)b * H + h) * L + tq] * LOG2E;       // lse pre-scaled by log2(e)
-        dlv = attn_delta_row<E>(dob + (size_t)tq * D, out + ((size_t)b * L + tq) * D + h * HD);
+    if (qd < L) {                                               // (a lane quad is all in or all out)
+        if (qj == 0) lsv = lse[((size_t)b * H + h) * L + qd] * LOG2E;       // lse pre-scaled by log2(e)
+        dlv = attn_delta_quad<E>(dob + (size_t)qd * D + 16 * qj, out + ((size_t)b * L + qd) * D + h * HD + 16 * qj);
     }
     rows_store<E, NWV>(Ks, fk);
     rows_store<E, NWV>(Vs, fv);
     rows_store<E, NWV>(Qs, fq);
     rows_store<E, NWV>(Ds, fd);
-    if (tq < LP) { ls[tq] = lsv; dl[tq] = dlv; }
+    static_assert(64 * NWV >= 4 * LP, "a lane quad per padded query");
+    if (qj == 0) { ls[qd] = lsv; dl[qd] = dlv; }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
@@ -690,15 +747,22 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
                 sdp(2 * st + 2, sv[cur ^ 1][0], pv[cur ^ 1][0]);
                 sdp(2 * st + 3, sv[cur ^ 1][1], pv[cur ^ 1][1]);
             }
+            // packed f32 (softmax arithmetic note above the forward): p = 2^(s c - lse c), dS = p (dP - delta)
             float ds[8];
+            const f32x2 c2v = {c2, c2}, nlv = {-lq2, -lq2}, ndv = {-dq, -dq};
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 const int kt = 2 * st + hf;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float p = __builtin_amdgcn_exp2f(fmaf(sv[cur][hf][i], c2, -lq2));
-                    if (kt >= nkt || (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i >= L)) p = 0.f;
-                    ds[4 * hf + i] = p * (pv[cur][hf][i] - dq);
+                for (int i = 0; i < 4; i += 2) {
+                    f32x2 p = __builtin_elementwise_fma(f32x2{sv[cur][hf][i], sv[cur][hf][i + 1]}, c2v, nlv);
+                    p.x = __builtin_amdgcn_exp2f(p.x);
+                    p.y = __builtin_amdgcn_exp2f(p.y);
+                    if (kt >= nkt || (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i >= L)) p.x = 0.f;
+                    if (kt >= nkt || (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i + 1 >= L)) p.y = 0.f;
+                    const f32x2 d = p * (f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]} + ndv);
+                    ds[4 * hf + i] = d.x;
+                    ds[4 * hf + i + 1] = d.y;
                 }
             }
             const typename E::Frag dsf = pack8<E>(ds);
@@ -750,17 +814,24 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
                 sdp(2 * st + 3, sv[cur ^ 1][1], pv[cur ^ 1][1]);
             }
             float pp[8], ds[8];
+            const f32x2 c2v = {c2, c2};
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 const int qt = 2 * st + hf;
                 const float4 l4 = *reinterpret_cast<const float4*>(ls + 16 * qt + 4 * fg);
                 const float4 d4 = *reinterpret_cast<const float4*>(dl + 16 * qt + 4 * fg);
-                const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
+                const f32x2 lq[2] = {{l4.x, l4.y}, {l4.z, l4.w}}, dq[2] = {{d4.x, d4.y}, {d4.z, d4.w}};
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(sv[cur][hf][i], c2, -lq[i]));   // lse = +inf (padding) -> 0
-                    pp[4 * hf + i] = p;
-                    ds[4 * hf + i] = p * (pv[cur][hf][i] - dq[i]);
+                for (int i = 0; i < 4; i += 2) {
+                    // lse = +inf (padding) -> p = 0
+                    f32x2 p = __builtin_elementwise_fma(f32x2{sv[cur][hf][i], sv[cur][hf][i + 1]}, c2v, -lq[i / 2]);
+                    p.x = __builtin_amdgcn_exp2f(p.x);
+                    p.y = __builtin_amdgcn_exp2f(p.y);
+                    const f32x2 d = p * (f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]} - dq[i / 2]);
+                    pp[4 * hf + i] = p.x;
+                    pp[4 * hf + i + 1] = p.y;
+                    ds[4 * hf + i] = d.x;
+                    ds[4 * hf + i + 1] = d.y;
                 }
             }
             const typename E::Frag pf = pack8<E>(pp), dsf = pack8<E>(ds);
@@ -1148,7 +1219,12 @@ template <class E> int attn_bwd_long(const void* qkv, const void* dout, const vo
     return EBC_OK;
 }
 
+// 16 waves (one workgroup per (crop, head), K / V staged once) while the (crop, head) units fit one pass of the 256 CUs;
+// with more units (32 crops: 384, 1.5 passes of 16-wave workgroups, one a CU) the forward takes 8-wave workgroups of
+// 128 queries, two a CU (768 halves: 1.5 passes of the 512 slots, each half half the work)
+constexpr int ATTN_CUS = 256;
 int attn_waves(int L) { return L > 128 ? 16 : 8; }
+int attn_fwd_waves(int B, int L, int H) { return attn_waves(L) == 16 && B * H <= ATTN_CUS ? 16 : 8; }
 
 // the CLIP ViT-B/16 + 32-prompt sequence (1 + 32 + 196 tokens) gets kernels compiled for it
 constexpr int L_VPT32 = 229;
@@ -1171,10 +1247,11 @@ template <class E, int NW, int LFIX, int QT = 1> int attn_fwd_nw(const void* qkv
 template <class E> int attn_fwd_t(const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,
                                   const TouchList* touch)
 {
-    if (attn_waves(L) == 16)
+    if (attn_fwd_waves(B, L, H) == 16)
         return L == L_VPT32 ? attn_fwd_nw<E, 16, L_VPT32>(qkv, out, lse, B, L, H, st, touch)
                             : attn_fwd_nw<E, 16, 0>(qkv, out, lse, B, L, H, st, touch);
-    return attn_fwd_nw<E, 8, 0>(qkv, out, lse, B, L, H, st, touch);
+    return L == L_VPT32 ? attn_fwd_nw<E, 8, L_VPT32>(qkv, out, lse, B, L, H, st, touch)
+                        : attn_fwd_nw<E, 8, 0>(qkv, out, lse, B, L, H, st, touch);
 }
 
 template <class E, int NW, int LFIX> int attn_bwd_nw(const void* qkv, const void* dout, const void* out, const float* lse,

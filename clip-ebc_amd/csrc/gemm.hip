@@ -57,6 +57,10 @@ struct GemmArgs {
     int tile0 = 0, ntile = 0;
     // MODE 0 row-mapped A operand: A row of output row r = (r / a_rpg) * a_gstride + a_goff + r % a_rpg (a_rpg 0: r)
     int a_rpg = 0, a_gstride = 0, a_goff = 0;
+    // stream-K (conv instances): the sk_grid workgroups share the sk_total = tiles x sk_nk k-tiles (0: off); the
+    // partial slots (2 per workgroup) in `part`, the per-tile arrival counters in `cnt`
+    long sk_total = 0;
+    int sk_nk = 0, sk_grid = 0;
     // algorithmic K the probe records (0: K).  MODE 2's K loop runs over padded image rows; its algorithmic K is
     // the interior pixel count B*H*W (bench.py counts 2*M*N*kalg FLOP)
     int kalg = 0;
@@ -221,597 +225,649 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
     const int wm = wave / WGN, wn = wave % WGN;
     const int ntn = g.N / BN, ntm = (g.M + BM - 1) / BM;
     const int wg = xcd_remap(blockIdx.x, (int)gridDim.x);
-    const int ltile = wg / g.splits, split = wg - ltile * g.splits;   // a tile's splits are adjacent
-    const int tile = g.tile0 + ltile;
-    int tm = tile / ntn, tn = tile % ntn;
-    if (g.group_m > 1) {
-        // each XCD's contiguous run of tiles (xcd_remap) then covers a group_m-tall block of tile rows and a
-        // few tile columns instead of one or two whole tile rows: the B (weight) panels are fetched into
-        // fewer XCD L2s (the wide-N products re-fetched B once per XCD)
-        const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
-        const int gm = min(ntm - first, g.group_m), r = tile - grp * per;
-        tm = first + r % gm;
-        tn = r / gm;
-    }
-    const int m0 = tm * BM, n0 = tn * BN;
-
     const T* A = reinterpret_cast<const T*>(g.A);
     const T* Bw = reinterpret_cast<const T*>(g.B);
-    const int K = g.K, nk = g.kslice / BK, ktbase = split * nk;
+    const int K = g.K;
+    // Stream-K (the conv instances, g.sk_total > 0): workgroup w takes the contiguous share [R(w), R(w+1)) of the
+    // launch's tiles' k-tiles (tile-major, R(w) = w * sk_total / grid; no more tiles than workgroups, so a share of
+    // at most sk_nk k-tiles) and runs it as one segment per tile touched, at most two; a tile cut between workgroups
+    // is finished by the last of its pieces to arrive.  Otherwise one segment: one tile, or one split-K slice of it.
+    constexpr bool SKM = SPL && MODE != 0;
+    const bool skr = SKM && g.sk_total > 0;
+    // (32-bit: (sk_total + 1) * grid < 2^31, launch_gemm_k)
+    const unsigned G = gridDim.x, skt = (unsigned)g.sk_total, sknk = (unsigned)g.sk_nk;
+    const unsigned it_beg = skr ? (unsigned)wg * skt / G : 0u, it_end = skr ? (unsigned)(wg + 1) * skt / G : 0u;
+    if (skr && it_beg >= it_end) return;
+    // a segment: k-tiles [it, it + nk) of one tile (always inlined: a loop over the segments, or a call per segment,
+    // made the 8-wave tiles spill 60-230 registers)
+    auto segment = [&](const unsigned it) __attribute__((always_inline)) -> int {
+        int ltile, split = 0, nk, ktbase;
+        if (skr) {
+            ltile = (int)(it / sknk);
+            ktbase = (int)(it - (unsigned)ltile * sknk);
+            nk = (int)min(sknk - (unsigned)ktbase, it_end - it);
+        } else {
+            ltile = wg / g.splits;                    // a tile's splits are adjacent
+            split = wg - ltile * g.splits;
+            nk = g.kslice / BK;
+            ktbase = split * nk;
+        }
+        const int tile = g.tile0 + ltile;
+        int tm = tile / ntn, tn = tile % ntn;
+        if (g.group_m > 1) {
+            // each XCD's contiguous run of tiles (xcd_remap) then covers a group_m-tall block of tile rows and a
+            // few tile columns instead of one or two whole tile rows: the B (weight) panels are fetched into
+            // fewer XCD L2s (the wide-N products re-fetched B once per XCD)
+            const int per = g.group_m * ntn, grp = tile / per, first = grp * g.group_m;
+            const int gm = min(ntm - first, g.group_m), r = tile - grp * per;
+            tm = first + r % gm;
+            tn = r / gm;
+        }
+        const int m0 = tm * BM, n0 = tn * BN;
 
-    // per-lane source rows for the LDS-DMA staging (fixed across k; the k-tile offset is added by stage())
-    const T* src[NLD];
-    bool isa[NLD];
-    // MODE 2: each piece's 16-B chunk index inside its row (the lane's K offset in the tile / (16 / EB)), 4 bits a
-    // piece in one register (r04: a K offset per piece made the 256x192 weight-gradient tiles spill)
-    unsigned cpk = 0;
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-        const bool tail = TAIL && i >= NLDF;
-        // full pieces: rows (wave*NLDF + i)*RPI + lane/CPR; tail piece j: 4-B lanes, rows
-        // NLDF*RPI*NW + (wave*NT4 + j)*R4 + lane/(4*CPR)
-        const int row = tail ? NLDF * RPI * NLDR + (lw * NT4 + (i - NLDF)) * R4 + lane / (4 * CPR)
-                             : (lw * NLDF + i) * RPI + lane / CPR;
-        const int slot = tail ? (lane % (4 * CPR)) / 4 : lane % CPR;
-        const int c = slot ^ swz_row<ROWB>(row);
-        const T* base;
-        isa[i] = row < BM;
-        if (row < BM) {
-            int gr = m0 + row;
-            gr = gr < g.M ? gr : g.M - 1;           // clamp: rows >= M are computed, never stored
+        // per-lane source rows for the LDS-DMA staging (fixed across k; the k-tile offset is added by stage())
+        const T* src[NLD];
+        bool isa[NLD];
+        // MODE 2: each piece's 16-B chunk index inside its row (the lane's K offset in the tile / (16 / EB)), 4 bits a
+        // piece in one register (r04: a K offset per piece made the 256x192 weight-gradient tiles spill)
+        unsigned cpk = 0;
+    #pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            const bool tail = TAIL && i >= NLDF;
+            // full pieces: rows (wave*NLDF + i)*RPI + lane/CPR; tail piece j: 4-B lanes, rows
+            // NLDF*RPI*NW + (wave*NT4 + j)*R4 + lane/(4*CPR)
+            const int row = tail ? NLDF * RPI * NLDR + (lw * NT4 + (i - NLDF)) * R4 + lane / (4 * CPR)
+                                 : (lw * NLDF + i) * RPI + lane / CPR;
+            const int slot = tail ? (lane % (4 * CPR)) / 4 : lane % CPR;
+            const int c = slot ^ swz_row<ROWB>(row);
+            const T* base;
+            isa[i] = row < BM;
+            if (row < BM) {
+                int gr = m0 + row;
+                gr = gr < g.M ? gr : g.M - 1;           // clamp: rows >= M are computed, never stored
+                if constexpr (MODE == 1) {
+                    const int hw = g.cH * g.cW;
+                    const int b = gr / hw, r = gr - b * hw, y = r / g.cW, x = r - y * g.cW;
+                    base = A + ((size_t)(b * g.cHp + y + 1) * g.cWp + x + 1) * g.cC;
+                } else if constexpr (MODE == 2) {
+                    base = A + (size_t)gr * g.cQs;
+                } else {
+                    if (g.a_rpg) gr = (gr / g.a_rpg) * g.a_gstride + g.a_goff + gr % g.a_rpg;
+                    base = A + (size_t)gr * K;
+                }
+            } else {
+                const int n = n0 + (MODE == 0 ? bcol<WN, TN>(row - BM) : row - BM);
+                if constexpr (MODE == 2) {
+                    const int cc = n / 9, t = n - 9 * cc, ky = t / 3, kx = t - 3 * ky;   // nn.Conv2d [o][c][ky][kx]
+                    base = Bw + (size_t)(kx * g.cC + cc) * g.cQs + (long)ky * g.cW;
+                } else {
+                    base = Bw + (size_t)n * K;
+                }
+            }
+            const int ko = c * (16 / EB) + (tail ? (lane & 3) * (4 / EB) : 0);
+            src[i] = base + ko;
+            if constexpr (MODE == 2) cpk |= (unsigned)(ko / (16 / EB)) << (4 * i);
+        }
+        auto stage_pieces = [&](int buf, int kt) {
+            const int ktg = ktbase + kt;
+            long oa, ob;
             if constexpr (MODE == 1) {
-                const int hw = g.cH * g.cW;
-                const int b = gr / hw, r = gr - b * hw, y = r / g.cW, x = r - y * g.cW;
-                base = A + ((size_t)(b * g.cHp + y + 1) * g.cWp + x + 1) * g.cC;
+                const int tpc = g.cC / BK;                // k-tiles per tap
+                const int tap = ktg / tpc, ky = tap / 3, kx = tap - 3 * ky;
+                oa = ((long)(ky - 1) * g.cWp + (kx - 1)) * g.cC + (long)(ktg - tap * tpc) * BK;
+                ob = (long)ktg * BK;
             } else if constexpr (MODE == 2) {
-                base = A + (size_t)gr * g.cQs;
+                oa = ob = (long)ktg * BK;
             } else {
-                if (g.a_rpg) gr = (gr / g.a_rpg) * g.a_gstride + g.a_goff + gr % g.a_rpg;
-                base = A + (size_t)gr * K;
+                oa = ob = (long)ktg * BK;
             }
-        } else {
-            const int n = n0 + (MODE == 0 ? bcol<WN, TN>(row - BM) : row - BM);
+            // MODE 2: a B chunk at K column q sits at position b * cPimg + (q - b * cHWp) of its x^T row (image b = q / cHWp).
+            // cHWp >= 64 (conv_gemm), so a tile of BK <= 64 columns starting in image b0 (wave-uniform) ends in b0 or b0 + 1:
+            // a lane's chunk is in b0 + 1 when its column offset reaches the boundary d (a multiple of the chunk width)
+            int b0 = 0, dch = 0;
+            long shift0 = 0, dP = 0;
             if constexpr (MODE == 2) {
-                const int cc = n / 9, t = n - 9 * cc, ky = t / 3, kx = t - 3 * ky;   // nn.Conv2d [o][c][ky][kx]
-                base = Bw + (size_t)(kx * g.cC + cc) * g.cQs + (long)ky * g.cW;
-            } else {
-                base = Bw + (size_t)n * K;
+                b0 = (int)((unsigned)ob / (unsigned)g.cHWp);        // 32-bit: K < 2^31
+                dch = ((b0 + 1) * g.cHWp - (int)ob) / (16 / EB);
+                dP = g.cPimg - g.cHWp;
+                shift0 = ob + (long)b0 * dP;
             }
-        }
-        const int ko = c * (16 / EB) + (tail ? (lane & 3) * (4 / EB) : 0);
-        src[i] = base + ko;
-        if constexpr (MODE == 2) cpk |= (unsigned)(ko / (16 / EB)) << (4 * i);
-    }
-    auto stage_pieces = [&](int buf, int kt) {
-        const int ktg = ktbase + kt;
-        long oa, ob;
-        if constexpr (MODE == 1) {
-            const int tpc = g.cC / BK;                // k-tiles per tap
-            const int tap = ktg / tpc, ky = tap / 3, kx = tap - 3 * ky;
-            oa = ((long)(ky - 1) * g.cWp + (kx - 1)) * g.cC + (long)(ktg - tap * tpc) * BK;
-            ob = (long)ktg * BK;
-        } else if constexpr (MODE == 2) {
-            oa = ob = (long)ktg * BK;
-        } else {
-            oa = ob = (long)ktg * BK;
-        }
-        // MODE 2: a B chunk at K column q sits at position b * cPimg + (q - b * cHWp) of its x^T row (image b = q / cHWp).
-        // cHWp >= 64 (conv_gemm), so a tile of BK <= 64 columns starting in image b0 (wave-uniform) ends in b0 or b0 + 1:
-        // a lane's chunk is in b0 + 1 when its column offset reaches the boundary d (a multiple of the chunk width)
-        int b0 = 0, dch = 0;
-        long shift0 = 0, dP = 0;
-        if constexpr (MODE == 2) {
-            b0 = (int)(ob / g.cHWp);
-            dch = (int)(((long)(b0 + 1) * g.cHWp - ob) / (16 / EB));
-            dP = g.cPimg - g.cHWp;
-            shift0 = ob + (long)b0 * dP;
-        }
-        auto piece = [&](int i) -> const T* {
-            if constexpr (MODE == 2) {
-                if (isa[i]) return src[i] + oa;
-                const int c = (int)((cpk >> (4 * i)) & 15u);
-                return src[i] + shift0 + (c >= dch ? dP : 0);
-            } else {
-                return src[i] + (isa[i] ? oa : ob);
+            auto piece = [&](int i) -> const T* {
+                if constexpr (MODE == 2) {
+                    if (isa[i]) return src[i] + oa;
+                    const int c = (int)((cpk >> (4 * i)) & 15u);
+                    return src[i] + shift0 + (c >= dch ? dP : 0);
+                } else {
+                    return src[i] + (isa[i] ? oa : ob);
+                }
+            };
+            char* dst = smem + buf * STAGE;
+    #pragma unroll
+            for (int i = 0; i < NLDF; ++i) {
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(i),
+                                                 EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, 0);
+            }
+    #pragma unroll
+            for (int j = 0; j < NT4; ++j) {
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(NLDF + j),
+                                                 EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, 0);
             }
         };
-        char* dst = smem + buf * STAGE;
-#pragma unroll
-        for (int i = 0; i < NLDF; ++i) {
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(i),
-                                             EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < NT4; ++j) {
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(NLDF + j),
-                                             EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, 0);
-        }
-    };
-    // the compute waves stage the ring themselves unless loader waves do
-    auto stage = [&](int buf, int kt) {
-        if constexpr (NLW == 0) stage_pieces(buf, kt);
-    };
+        // the compute waves stage the ring themselves unless loader waves do
+        auto stage = [&](int buf, int kt) {
+            if constexpr (NLW == 0) stage_pieces(buf, kt);
+        };
 
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // S-deep LDS ring + register double-buffered fragments.  Tiles kt+1 .. kt+S-1 are in flight
-    // while tile kt is consumed; the wait is a counted vmcnt (LDS-DMA loads count on it) and the
-    // barrier a raw s_barrier, so no vmcnt(0) drain happens in the K loop (cdna_hip_programming.md
-    // §5 "Pipelining across barriers").  The next k32 step's ds_reads are issued before the current
-    // step's MFMAs; at a tile boundary the wait+barrier sit before the last step's MFMAs so the
-    // next tile's first fragments load underneath them.
-    constexpr int KS = BK / 32;                   // k32 steps per tile
-    // two fragment register sets (next step's reads under this step's MFMAs) unless the wave tile's
-    // accumulators leave no room (2 waves/SIMD: 256 registers per lane in all)
-    constexpr bool DB = TM * TN * 4 + 2 * (TM + TN) * (EB == 2 ? 4 : 8) <= 200;
-    static_assert(!DB || KS == 2 || S % 2 == 0, "register-set alternation");
-    const int fr = lane & 15, fg = lane >> 4;
-    // Fragment addressing is lane-constant: every fragment row is 16-aligned + fr, so the XOR
-    // swizzle term is swz_row(fr) for all of them.  Per lane one VGPR offset per (k32 step,
-    // 16-B half); the wave's row block, the sub-tile and the stage buffer are immediates.
-    const int xs = swz_row<ROWB>(fr);
-    int loff[KS][EB == 2 ? 1 : 2];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-        for (int c = 0; c < (EB == 2 ? 1 : 2); ++c) {
-            const int ch = ((kk * 32 + 8 * fg) * EB >> 4) + c;
-            loff[kk][c] = fr * ROWB + ((ch ^ xs) << 4);
-        }
-    const char* abase = smem + wm * WM * ROWB;
-    const char* bbase = smem + (BM + wn * WN) * ROWB;
-    auto load_frags = [&](auto bufc, int kk, typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
-        constexpr int buf = decltype(bufc)::value;
-#pragma unroll
-        for (int a = 0; a < TM; ++a) {
-            const char* rp = abase + buf * STAGE + a * 16 * ROWB;
-            if constexpr (EB == 2) {
-                af[a] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
-            } else {
-                const float4 x0 = *reinterpret_cast<const float4*>(rp + loff[kk][0]);
-                const float4 x1 = *reinterpret_cast<const float4*>(rp + loff[kk][EB == 2 ? 0 : 1]);
-                af[a] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const char* rp = bbase + buf * STAGE + b * 16 * ROWB;
-            if constexpr (EB == 2) {
-                bf[b] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
-            } else {
-                const float4 x0 = *reinterpret_cast<const float4*>(rp + loff[kk][0]);
-                const float4 x1 = *reinterpret_cast<const float4*>(rp + loff[kk][EB == 2 ? 0 : 1]);
-                bf[b] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            }
-        }
-    };
-    // tile next_kt landed (count the later tiles still in flight): the issuing wave's counted vmcnt
-    auto wait_tile = [&](int next_kt, auto tailc) {
-        if constexpr (decltype(tailc)::value) {
-            const int later = (nk - 1 - next_kt) < (S - 2) ? (nk - 1 - next_kt) : (S - 2);
-            wait_vmcnt<NLD, S - 2>(later);
-        } else {
-            asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * NLD) : "memory");
-        }
-    };
-    auto sync_tile = [&](int next_kt, auto tailc) {
-        // tile next_kt landed, every wave done reading the buffer that the refill below overwrites.
-        // Outside the tail S-2 later tiles are in flight.
-        if constexpr (NLW == 0) wait_tile(next_kt, tailc);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    if constexpr (NLW > 0) {
-        if (wave >= NW) {
-            // loader wave: the compute waves' ring schedule (one barrier per k-tile, the buffer of tile kt
-            // refilled with tile kt + S right after the barrier that retires its reads), then exit
-            for (int s = 0; s < S - 1; ++s)
-                if (s < nk) stage_pieces(s, s);
-            wait_tile(0, std::true_type{});
-            __builtin_amdgcn_s_barrier();
-            if (S - 1 < nk) stage_pieces(S - 1, S - 1);
-            for (int kt = 0; kt + 1 < nk; ++kt) {
-                wait_tile(kt + 1, std::true_type{});
-                __builtin_amdgcn_s_barrier();
-                if (kt + S < nk) stage_pieces(kt % S, kt + S);
-            }
-            return;
-        }
-    }
-
-    // 4-wave RESID tiles (one wave per SIMD: registers to spare): the f32 residual operand of the epilogue is
-    // loaded before the ring fills, so its latency hides under the first tiles' instead of being paid after the
-    // K loop (vmcnt retires loads in order: issued any later, a counted ring wait would block on it mid-loop)
-    constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && NW + NLW <= 8;
-    typedef float rp8_t __attribute__((ext_vector_type(8)));
-    typedef float rp4_t __attribute__((ext_vector_type(4)));
-    rp8_t rp8[PREF ? TM : 1][TN / 2 > 0 ? TN / 2 : 1];
-    rp4_t rp4[PREF && (TN & 1) ? TM : 1];
-    // 8-wave GELU' tiles (256 registers a wave): the first half of the rows' pre-activation operand the same way
-    constexpr bool PREF_G = MODE == 0 && EPI == EPI_GELU_BWD && NW >= 8 && TM % 2 == 0 && (TN & 1) == 0;
-    typedef T gp8_t __attribute__((ext_vector_type(8)));
-    gp8_t gp8[PREF_G ? TM / 2 : 1][TN / 2 > 0 ? TN / 2 : 1];
-    if constexpr (PREF_G) {
-        const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
-        const T* aux = reinterpret_cast<const T*>(g.aux);
-#pragma unroll
-        for (int a = 0; a < TM / 2; ++a) {
-            const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
-#pragma unroll
-            for (int q = 0; q < TN / 2; ++q) gp8[a][q] = *reinterpret_cast<const gp8_t*>(aux + ro + q * 32 + fq * 8);
-        }
-    }
-    if constexpr (PREF) {
-        const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
-#pragma unroll
-        for (int a = 0; a < TM; ++a) {
-            const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
-#pragma unroll
-            for (int q = 0; q < TN / 2; ++q) rp8[a][q] = *reinterpret_cast<const rp8_t*>(g.resid + ro + q * 32 + fq * 8);
-            if constexpr (TN & 1) rp4[a] = *reinterpret_cast<const rp4_t*>(g.resid + ro + (TN / 2) * 32 + fq * 4);
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < S - 1; ++s)
-        if (s < nk) stage(s, s);
-    sync_tile(0, std::true_type{});
-    if (S - 1 < nk) stage(S - 1, S - 1);
-    typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
-    load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
-    auto mma_all = [&](typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
-#pragma unroll
+        f32x4 acc[TM][TN];
+    #pragma unroll
         for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int b = 0; b < TN; ++b) acc[a][b] = mma(bf[b], af[a], acc[a][b]);   // swapped: C^T tile
-    };
-    // step body: prefetch the fragments of the step after (kt, kk) into (an, bn), then MMA (ac, bc);
-    // the K loop is unrolled by S so the stage buffer of every fragment load is a constant.
-    // The main loop runs whole groups of S tiles that are followed by at least S more, so it has no
-    // bounds tests (a branch-free body keeps the accumulators in place across the back edge);
-    // the last one or two groups run the same body with the tests.
-    auto step = [&](auto bufc, auto tailc, int kt, int kk, typename E::Frag (&ac)[TM], typename E::Frag (&bc)[TN],
-                    typename E::Frag (&an)[TM], typename E::Frag (&bn)[TN]) {
-        constexpr int buf = decltype(bufc)::value;
-        constexpr bool tail = decltype(tailc)::value;
-        if constexpr (!DB) mma_all(ac, bc);      // single fragment set: consume, then refill it
-        if (kk + 1 < KS) {
-            load_frags(bufc, kk + 1, an, bn);
-        } else if (!tail || kt + 1 < nk) {
-            sync_tile(kt + 1, tailc);
-            if (!tail || kt + S < nk) stage(buf, kt + S);
-            load_frags(std::integral_constant<int, (buf + 1) % S>{}, 0, an, bn);
-        }
-        if constexpr (!DB) {
-            __builtin_amdgcn_sched_barrier(0);
-            return;
-        }
-        mma_all(ac, bc);
-        // keep the next step's fragment reads ahead of (interleaved with) this step's MFMAs and
-        // stop the scheduler from sinking them next to their first use
-        // (all of them within the first half of the MFMAs, two per MFMA)
-        constexpr int NRD = (TM + TN) * (EB == 2 ? 1 : 2), NG = (NRD + 1) / 2;
-        static_assert(NG <= TM * TN, "read/MFMA interleave");
-        static_for<0, NG>([&](auto) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);                 // DS reads
-        });
-        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - NG, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto group = [&](int kt0, auto tailc) {
-        static_for<0, S>([&](auto sc) {
-            constexpr int s = decltype(sc)::value;
-            const int kt = kt0 + s;
-            if (!decltype(tailc)::value || kt < nk) {
-                if constexpr (!DB) {
-                    static_for<0, KS>([&](auto kc) { step(sc, tailc, kt, decltype(kc)::value, a0, b0, a0, b0); });
-                } else if constexpr (KS == 2) {
-                    step(sc, tailc, kt, 0, a0, b0, a1, b1);
-                    step(sc, tailc, kt, 1, a1, b1, a0, b0);
-                } else if constexpr ((s & 1) == 0) {
-                    step(sc, tailc, kt, 0, a0, b0, a1, b1);
+    #pragma unroll
+            for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        // S-deep LDS ring + register double-buffered fragments.  Tiles kt+1 .. kt+S-1 are in flight
+        // while tile kt is consumed; the wait is a counted vmcnt (LDS-DMA loads count on it) and the
+        // barrier a raw s_barrier, so no vmcnt(0) drain happens in the K loop (cdna_hip_programming.md
+        // §5 "Pipelining across barriers").  The next k32 step's ds_reads are issued before the current
+        // step's MFMAs; at a tile boundary the wait+barrier sit before the last step's MFMAs so the
+        // next tile's first fragments load underneath them.
+        constexpr int KS = BK / 32;                   // k32 steps per tile
+        // two fragment register sets (next step's reads under this step's MFMAs) unless the wave tile's
+        // accumulators leave no room (2 waves/SIMD: 256 registers per lane in all)
+        constexpr bool DB = TM * TN * 4 + 2 * (TM + TN) * (EB == 2 ? 4 : 8) <= 200;
+        static_assert(!DB || KS == 2 || S % 2 == 0, "register-set alternation");
+        const int fr = lane & 15, fg = lane >> 4;
+        // Fragment addressing is lane-constant: every fragment row is 16-aligned + fr, so the XOR
+        // swizzle term is swz_row(fr) for all of them.  Per lane one VGPR offset per (k32 step,
+        // 16-B half); the wave's row block, the sub-tile and the stage buffer are immediates.
+        const int xs = swz_row<ROWB>(fr);
+        int loff[KS][EB == 2 ? 1 : 2];
+    #pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+    #pragma unroll
+            for (int c = 0; c < (EB == 2 ? 1 : 2); ++c) {
+                const int ch = ((kk * 32 + 8 * fg) * EB >> 4) + c;
+                loff[kk][c] = fr * ROWB + ((ch ^ xs) << 4);
+            }
+        const char* abase = smem + wm * WM * ROWB;
+        const char* bbase = smem + (BM + wn * WN) * ROWB;
+        auto load_frags = [&](auto bufc, int kk, typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
+            constexpr int buf = decltype(bufc)::value;
+    #pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const char* rp = abase + buf * STAGE + a * 16 * ROWB;
+                if constexpr (EB == 2) {
+                    af[a] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
                 } else {
-                    step(sc, tailc, kt, 0, a1, b1, a0, b0);
+                    const float4 x0 = *reinterpret_cast<const float4*>(rp + loff[kk][0]);
+                    const float4 x1 = *reinterpret_cast<const float4*>(rp + loff[kk][EB == 2 ? 0 : 1]);
+                    af[a] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
                 }
             }
-        });
-    };
-    int kt0 = 0;
-    for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
-    for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
-
-    if (SPL && g.splits > 1 && g.cnt == nullptr) {
-        // split-K without a last arriver (deep splits of the weight-gradient products): every split stores its
-        // f32 partial row-major into part[split][M][N] (columns as the epilogue maps them), a separate launch
-        // (splitk_reduce_kernel) sums the splits in split order -- deterministic, and the sum is spread over
-        // the whole GPU instead of re-read through one CU
-        float* P = g.part + (size_t)split * g.M * g.N;
-        const int mb = m0 + wm * WM + fr;
-#pragma unroll
-        for (int a = 0; a < TM; ++a) {
-            const int m = mb + a * 16;
-            if (m >= g.M) break;
-#pragma unroll
+    #pragma unroll
             for (int b = 0; b < TN; ++b) {
-                int n;
-                if constexpr (MODE == 0) {
-                    constexpr int NP = TN / 2;
-                    const int nb = n0 + wn * WN;
-                    n = (b / 2 < NP) ? nb + (b / 2) * 32 + fg * 8 + (b & 1) * 4 : nb + NP * 32 + fg * 4;
+                const char* rp = bbase + buf * STAGE + b * 16 * ROWB;
+                if constexpr (EB == 2) {
+                    bf[b] = __builtin_bit_cast(typename E::Frag, *reinterpret_cast<const uint4*>(rp + loff[kk][0]));
                 } else {
-                    n = n0 + wn * WN + b * 16 + 4 * fg;
+                    const float4 x0 = *reinterpret_cast<const float4*>(rp + loff[kk][0]);
+                    const float4 x1 = *reinterpret_cast<const float4*>(rp + loff[kk][EB == 2 ? 0 : 1]);
+                    bf[b] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
                 }
-                *reinterpret_cast<f32x4*>(P + (size_t)m * g.N + n) = acc[a][b];
+            }
+        };
+        // tile next_kt landed (count the later tiles still in flight): the issuing wave's counted vmcnt
+        auto wait_tile = [&](int next_kt, auto tailc) {
+            if constexpr (decltype(tailc)::value) {
+                const int later = (nk - 1 - next_kt) < (S - 2) ? (nk - 1 - next_kt) : (S - 2);
+                wait_vmcnt<NLD, S - 2>(later);
+            } else {
+                asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * NLD) : "memory");
+            }
+        };
+        auto sync_tile = [&](int next_kt, auto tailc) {
+            // tile next_kt landed, every wave done reading the buffer that the refill below overwrites.
+            // Outside the tail S-2 later tiles are in flight.
+            if constexpr (NLW == 0) wait_tile(next_kt, tailc);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        };
+        if constexpr (NLW > 0) {
+            if (wave >= NW) {
+                // loader wave: the compute waves' ring schedule (one barrier per k-tile, the buffer of tile kt
+                // refilled with tile kt + S right after the barrier that retires its reads), then exit
+                for (int s = 0; s < S - 1; ++s)
+                    if (s < nk) stage_pieces(s, s);
+                wait_tile(0, std::true_type{});
+                __builtin_amdgcn_s_barrier();
+                if (S - 1 < nk) stage_pieces(S - 1, S - 1);
+                for (int kt = 0; kt + 1 < nk; ++kt) {
+                    wait_tile(kt + 1, std::true_type{});
+                    __builtin_amdgcn_s_barrier();
+                    if (kt + S < nk) stage_pieces(kt % S, kt + S);
+                }
+                return nk;
             }
         }
-        return;
-    }
-    if (SPL && g.splits > 1) {
-        // split-K: publish this split's f32 partial (lane-major: the reader has the same lane map,
-        // so every access is a coalesced 16-B per lane), count the arrival; the last arriver sums
-        // the others and runs the epilogue, the rest exit.  Agent-scope fences order the partial
-        // stores before the count and the count before the reads (L2s are per XCD).
-        constexpr int PT = NW * TM * TN * 64;     // f32x4 per partial tile
-        // one buffer resource over this tile's `splits` partials; aux 16 = sc1
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<f32x4*>(g.part) + (size_t)ltile * g.splits * PT, 0, 0x7fffffff, 0x00020000);
-        // MI355X_MICROARCH.md cross-CU hand-off, sc1 form: sc1 (write-through) 16-B stores, every
-        // wave's vmcnt(0), a barrier, ONE agent-scope atomic add; the last adder's waves read with
-        // sc1 loads after a barrier.  No agent fences (a buffer_wbl2 per workgroup costs ~microseconds).
-        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int b = 0; b < TN; ++b)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rs,
-                                                       ((split * PT) + ((wave * TM + a) * TN + b) * 64 + lane) * 16, 0, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        __shared__ int last;
-        if (tid == 0) last = atomicAdd(&g.cnt[ltile], 1) == g.splits - 1;
-        __syncthreads();
-        if (!last) return;
-        // bit-reproducible sum whichever split arrives last: two splits add the other's partial (f32
-        // addition commutes); more splits re-read every partial, this one's too, in split order
-        // loaded in row-group chunks of at most 64 registers: the whole partial at once (TM*TN*4 registers on top of
-        // the accumulators) spilled the 256-wide tiles' epilogues (256x256: 150-430 registers)
-        constexpr int PCH = [] { int c = TM; while (c > 1 && (TM % c || c * TN * 4 > 64)) --c; return c; }();
-        auto add_partial = [&](int sp) {
-            static_for<0, TM / PCH>([&](auto cc) {
-                constexpr int a0 = decltype(cc)::value * PCH;
-                f32x4 t[PCH][TN];
-#pragma unroll
-                for (int a = 0; a < PCH; ++a)
-#pragma unroll
-                    for (int b = 0; b < TN; ++b)
-                        t[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                            rs, ((sp * PT) + ((wave * TM + a0 + a) * TN + b) * 64 + lane) * 16, 0, 16));
-#pragma unroll
-                for (int a = 0; a < PCH; ++a)
-#pragma unroll
-                    for (int b = 0; b < TN; ++b) acc[a0 + a][b] += t[a][b];
-                // keep the next chunk's loads below this one's adds (a sched_barrier alone did not: the DAG
-                // scheduler hoisted all 32 loads of a 256x256 partial)
-                asm volatile("" ::: "memory");
+
+        // 4-wave RESID tiles (one wave per SIMD: registers to spare): the f32 residual operand of the epilogue is
+        // loaded before the ring fills, so its latency hides under the first tiles' instead of being paid after the
+        // K loop (vmcnt retires loads in order: issued any later, a counted ring wait would block on it mid-loop)
+        constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && NW + NLW <= 8;
+        typedef float rp8_t __attribute__((ext_vector_type(8)));
+        typedef float rp4_t __attribute__((ext_vector_type(4)));
+        rp8_t rp8[PREF ? TM : 1][TN / 2 > 0 ? TN / 2 : 1];
+        rp4_t rp4[PREF && (TN & 1) ? TM : 1];
+        // 8-wave GELU' tiles (256 registers a wave): the first half of the rows' pre-activation operand the same way
+        constexpr bool PREF_G = MODE == 0 && EPI == EPI_GELU_BWD && NW >= 8 && TM % 2 == 0 && (TN & 1) == 0;
+        typedef T gp8_t __attribute__((ext_vector_type(8)));
+        gp8_t gp8[PREF_G ? TM / 2 : 1][TN / 2 > 0 ? TN / 2 : 1];
+        if constexpr (PREF_G) {
+            const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
+            const T* aux = reinterpret_cast<const T*>(g.aux);
+    #pragma unroll
+            for (int a = 0; a < TM / 2; ++a) {
+                const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
+    #pragma unroll
+                for (int q = 0; q < TN / 2; ++q) gp8[a][q] = *reinterpret_cast<const gp8_t*>(aux + ro + q * 32 + fq * 8);
+            }
+        }
+        if constexpr (PREF) {
+            const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
+    #pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
+    #pragma unroll
+                for (int q = 0; q < TN / 2; ++q) rp8[a][q] = *reinterpret_cast<const rp8_t*>(g.resid + ro + q * 32 + fq * 8);
+                if constexpr (TN & 1) rp4[a] = *reinterpret_cast<const rp4_t*>(g.resid + ro + (TN / 2) * 32 + fq * 4);
+            }
+        }
+    #pragma unroll
+        for (int s = 0; s < S - 1; ++s)
+            if (s < nk) stage(s, s);
+        sync_tile(0, std::true_type{});
+        if (S - 1 < nk) stage(S - 1, S - 1);
+        typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
+        load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
+        auto mma_all = [&](typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
+    #pragma unroll
+            for (int a = 0; a < TM; ++a)
+    #pragma unroll
+                for (int b = 0; b < TN; ++b) acc[a][b] = mma(bf[b], af[a], acc[a][b]);   // swapped: C^T tile
+        };
+        // step body: prefetch the fragments of the step after (kt, kk) into (an, bn), then MMA (ac, bc);
+        // the K loop is unrolled by S so the stage buffer of every fragment load is a constant.
+        // The main loop runs whole groups of S tiles that are followed by at least S more, so it has no
+        // bounds tests (a branch-free body keeps the accumulators in place across the back edge);
+        // the last one or two groups run the same body with the tests.
+        auto step = [&](auto bufc, auto tailc, int kt, int kk, typename E::Frag (&ac)[TM], typename E::Frag (&bc)[TN],
+                        typename E::Frag (&an)[TM], typename E::Frag (&bn)[TN]) {
+            constexpr int buf = decltype(bufc)::value;
+            constexpr bool tail = decltype(tailc)::value;
+            if constexpr (!DB) mma_all(ac, bc);      // single fragment set: consume, then refill it
+            if (kk + 1 < KS) {
+                load_frags(bufc, kk + 1, an, bn);
+            } else if (!tail || kt + 1 < nk) {
+                sync_tile(kt + 1, tailc);
+                if (!tail || kt + S < nk) stage(buf, kt + S);
+                load_frags(std::integral_constant<int, (buf + 1) % S>{}, 0, an, bn);
+            }
+            if constexpr (!DB) {
                 __builtin_amdgcn_sched_barrier(0);
+                return;
+            }
+            mma_all(ac, bc);
+            // keep the next step's fragment reads ahead of (interleaved with) this step's MFMAs and
+            // stop the scheduler from sinking them next to their first use
+            // (all of them within the first half of the MFMAs, two per MFMA)
+            constexpr int NRD = (TM + TN) * (EB == 2 ? 1 : 2), NG = (NRD + 1) / 2;
+            static_assert(NG <= TM * TN, "read/MFMA interleave");
+            static_for<0, NG>([&](auto) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);                 // DS reads
+            });
+            __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - NG, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto group = [&](int kt0, auto tailc) {
+            static_for<0, S>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                const int kt = kt0 + s;
+                if (!decltype(tailc)::value || kt < nk) {
+                    if constexpr (!DB) {
+                        static_for<0, KS>([&](auto kc) { step(sc, tailc, kt, decltype(kc)::value, a0, b0, a0, b0); });
+                    } else if constexpr (KS == 2) {
+                        step(sc, tailc, kt, 0, a0, b0, a1, b1);
+                        step(sc, tailc, kt, 1, a1, b1, a0, b0);
+                    } else if constexpr ((s & 1) == 0) {
+                        step(sc, tailc, kt, 0, a0, b0, a1, b1);
+                    } else {
+                        step(sc, tailc, kt, 0, a1, b1, a0, b0);
+                    }
+                }
             });
         };
-        if (g.splits == 2) {
-            add_partial(1 - split);
-        } else {
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (int sp = 0; sp < g.splits; ++sp) add_partial(sp);
-        }
-        if (tid == 0) atomicExch(&g.cnt[ltile], 0);   // re-armed for the next launch
-    }
+        int kt0 = 0;
+        for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
+        for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
 
-    if constexpr (MODE == 0) {
-        // direct epilogue (bcol above): lane (fr, fg) holds rows m0 + wm*WM + a*16 + fr and, per column
-        // group q, 8 (a sub-tile pair) or 4 (odd last sub-tile) consecutive columns.  Operands
-        // (resid / aux) are loaded for the whole wave tile first (row-clamped, unconditional), then each
-        // group is finished and stored; rows >= M are never stored.
-        static_assert(EPI <= EPI_GELU_BWD, "MODE 0 epilogues");
-        TO* C = reinterpret_cast<TO*>(g.C);
-        constexpr int NP = TN / 2, ODD = TN & 1;
-        constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID;
-        using PA = typename std::conditional<EPI == EPI_RESID, float, T>::type;
-        typedef PA pa8 __attribute__((ext_vector_type(8)));
-        typedef PA pa4 __attribute__((ext_vector_type(4)));
-        const int mb = m0 + wm * WM + fr;
-        const int nb = n0 + wn * WN;
-        // 8-wave tiles run two waves per SIMD (256 registers each): their operands are loaded for half of the
-        // row groups at a time (the whole wave tile at once spilled: GELU' 256x192, 27 registers), with a scheduling
-    // fence per row group
-        constexpr int PREG = PRE ? TM * (NP * (int)sizeof(pa8) + ODD * (int)sizeof(pa4)) / 4 : 0;
-        constexpr int PH = (NW >= 8 && PREG > 24 && TM % 2 == 0) ? 2 : 1;
-        constexpr int TMP = TM / PH;
-        float bv[NP > 0 ? NP : 1][8], bo[4];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) {
-            if (g.bias) load8f<float>(g.bias + nb + q * 32 + fg * 8, bv[q]);
-            else for (int i = 0; i < 8; ++i) bv[q][i] = 0.f;
-        }
-        if constexpr (ODD) {
-            if (g.bias) load4<float>(g.bias + nb + NP * 32 + fg * 4, bo);
-            else for (int i = 0; i < 4; ++i) bo[i] = 0.f;
-        }
-        auto finish = [&](float* v, int w, const float* bias, const auto& pre, size_t off) {
-            for (int i = 0; i < w; ++i) v[i] += bias[i];
-            if constexpr (EPI == EPI_GELU) {
-                if (g.aux) {
-                    if (w == 8) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
-                    else store4<T>(reinterpret_cast<T*>(g.aux) + off, v);
-                }
-                for (int i = 0; i < w; ++i) v[i] = quick_gelu(v[i]);
-            } else if constexpr (EPI == EPI_GELU_BWD) {
-                for (int i = 0; i < w; ++i) v[i] *= quick_gelu_grad((float)pre[i]);
-            } else if constexpr (EPI == EPI_RESID) {
-                for (int i = 0; i < w; ++i) v[i] += pre[i];
-            }
-            if (w == 8) store8<TO>(C + off, v);
-            else store4<TO>(C + off, v);
-        };
-        static_for<0, PH>([&](auto phc) {
-            constexpr int a0 = decltype(phc)::value * TMP;
-            pa8 p8[PRE ? TMP : 1][NP > 0 ? NP : 1];
-            pa4 p4[PRE && ODD ? TMP : 1];
-            if constexpr (PREF) {
-#pragma unroll
-                for (int a = 0; a < TMP; ++a) {
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) p8[a][q] = rp8[a0 + a][q];
-                    if constexpr (ODD) p4[a] = rp4[a0 + a];
-                }
-            } else if constexpr (PREF_G && a0 == 0 && TMP == TM / 2) {
-#pragma unroll
-                for (int a = 0; a < TMP; ++a)
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) p8[a][q] = __builtin_convertvector(gp8[a][q], pa8);
-            } else if constexpr (PRE) {
-                const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
-#pragma unroll
-                for (int a = 0; a < TMP; ++a) {
-                    const size_t ro = (size_t)min(mb + (a0 + a) * 16, g.M - 1) * g.N + nb;
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) p8[a][q] = *reinterpret_cast<const pa8*>(src + ro + q * 32 + fg * 8);
-                    if constexpr (ODD) p4[a] = *reinterpret_cast<const pa4*>(src + ro + NP * 32 + fg * 4);
+        if (SPL && g.splits > 1 && g.cnt == nullptr) {
+            // split-K without a last arriver (deep splits of the weight-gradient products): every split stores its
+            // f32 partial row-major into part[split][M][N] (columns as the epilogue maps them), a separate launch
+            // (splitk_reduce_kernel) sums the splits in split order -- deterministic, and the sum is spread over
+            // the whole GPU instead of re-read through one CU
+            float* P = g.part + (size_t)split * g.M * g.N;
+            const int mb = m0 + wm * WM + fr;
+    #pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const int m = mb + a * 16;
+                if (m >= g.M) break;
+    #pragma unroll
+                for (int b = 0; b < TN; ++b) {
+                    int n;
+                    if constexpr (MODE == 0) {
+                        constexpr int NP = TN / 2;
+                        const int nb = n0 + wn * WN;
+                        n = (b / 2 < NP) ? nb + (b / 2) * 32 + fg * 8 + (b & 1) * 4 : nb + NP * 32 + fg * 4;
+                    } else {
+                        n = n0 + wn * WN + b * 16 + 4 * fg;
+                    }
+                    *reinterpret_cast<f32x4*>(P + (size_t)m * g.N + n) = acc[a][b];
                 }
             }
-#pragma unroll
-            for (int a = 0; a < TMP; ++a) {
-                const int m = mb + (a0 + a) * 16;
-                if (m >= g.M) break;                 // rows ascend with a
-                const size_t ro = (size_t)m * g.N + nb;
-#pragma unroll
+            return nk;
+        }
+        bool fin = true;                              // this segment ends its tile: run the epilogue
+        if (SPL && (skr ? (ktbase != 0 || nk != g.sk_nk) : g.splits > 1)) {
+            // split-K / a stream-K piece: publish this piece's f32 partial (lane-major: the reader has the same lane
+            // map, so every access is a coalesced 16-B per lane), count the arrival; the last arriver sums the pieces
+            // and runs the epilogue, the rest go on (stream-K) or exit.
+            // MI355X_MICROARCH.md cross-CU hand-off, sc1 form: sc1 (write-through) 16-B stores, every wave's vmcnt(0), a
+            // barrier, ONE agent-scope atomic add; the last adder's waves read with sc1 loads after a barrier.  No agent
+            // fences (a buffer_wbl2 per workgroup costs ~microseconds).
+            constexpr int PT = NW * TM * TN * 64;     // f32x4 per partial tile
+            // partial slots: split-K, tile ltile's `splits` slots; stream-K, two per workgroup (2w: its first segment,
+            // 2w + 1: its last), pieces p = 0.. of a tile are workgroups wf + p
+            int mine, mypiece, wf = 0, np = g.splits;
+            const unsigned i0 = (unsigned)ltile * sknk;
+            if (skr) {
+                wf = (int)(((i0 + 1) * G - 1) / skt);
+                np = (int)(((i0 + sknk) * G - 1) / skt) - wf + 1;
+                mine = it == it_beg ? 2 * wg : 2 * wg + 1;
+                mypiece = wg - wf;
+            } else {
+                mine = mypiece = split;
+            }
+            auto slot = [&](int piece) -> int {
+                if (!skr) return piece;
+                const int w = wf + piece;
+                return piece == 0 && (unsigned)w * skt / G < i0 ? 2 * w + 1 : 2 * w;
+            };
+            // one buffer resource over the partials; aux 16 = sc1
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<f32x4*>(g.part) + (skr ? 0 : (size_t)ltile * g.splits * PT), 0, 0x7fffffff, 0x00020000);
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    #pragma unroll
+            for (int a = 0; a < TM; ++a)
+    #pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rs,
+                                                           ((mine * PT) + ((wave * TM + a) * TN + b) * 64 + lane) * 16, 0, 16);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            __shared__ int last;
+            if (tid == 0) last = atomicAdd(&g.cnt[ltile], 1) == np - 1;
+            __syncthreads();
+            fin = last;
+            if (fin) {
+                // bit-reproducible sum whichever piece arrives last: two pieces add the other's partial (f32 addition
+                // commutes); more re-read every partial, this one's too, in piece order.  Loaded in row-group chunks of
+                // at most 64 registers: the whole partial at once (TM*TN*4 registers on top of the accumulators)
+                // spilled the 256-wide tiles' epilogues (256x256: 150-430 registers)
+                constexpr int PCH = [] { int c = TM; while (c > 1 && (TM % c || c * TN * 4 > 64)) --c; return c; }();
+                auto add_partial = [&](int sp) {
+                    static_for<0, TM / PCH>([&](auto cc) {
+                        constexpr int a0 = decltype(cc)::value * PCH;
+                        f32x4 t[PCH][TN];
+    #pragma unroll
+                        for (int a = 0; a < PCH; ++a)
+    #pragma unroll
+                            for (int b = 0; b < TN; ++b)
+                                t[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                    rs, ((sp * PT) + ((wave * TM + a0 + a) * TN + b) * 64 + lane) * 16, 0, 16));
+    #pragma unroll
+                        for (int a = 0; a < PCH; ++a)
+    #pragma unroll
+                            for (int b = 0; b < TN; ++b) acc[a0 + a][b] += t[a][b];
+                        // keep the next chunk's loads below this one's adds (a sched_barrier alone did not: the DAG
+                        // scheduler hoisted all 32 loads of a 256x256 partial)
+                        asm volatile("" ::: "memory");
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                };
+                if (np == 2) {
+                    add_partial(slot(1 - mypiece));
+                } else {
+    #pragma unroll
+                    for (int a = 0; a < TM; ++a)
+    #pragma unroll
+                        for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int p = 0; p < np; ++p) add_partial(slot(p));
+                }
+                if (tid == 0) atomicExch(&g.cnt[ltile], 0);   // re-armed for the next launch
+            }
+        }
+
+        if (fin) {
+            if constexpr (MODE == 0) {
+                // direct epilogue (bcol above): lane (fr, fg) holds rows m0 + wm*WM + a*16 + fr and, per column
+                // group q, 8 (a sub-tile pair) or 4 (odd last sub-tile) consecutive columns.  Operands
+                // (resid / aux) are loaded for the whole wave tile first (row-clamped, unconditional), then each
+                // group is finished and stored; rows >= M are never stored.
+                static_assert(EPI <= EPI_GELU_BWD, "MODE 0 epilogues");
+                TO* C = reinterpret_cast<TO*>(g.C);
+                constexpr int NP = TN / 2, ODD = TN & 1;
+                constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID;
+                using PA = typename std::conditional<EPI == EPI_RESID, float, T>::type;
+                typedef PA pa8 __attribute__((ext_vector_type(8)));
+                typedef PA pa4 __attribute__((ext_vector_type(4)));
+                const int mb = m0 + wm * WM + fr;
+                const int nb = n0 + wn * WN;
+                // 8-wave tiles run two waves per SIMD (256 registers each): their operands are loaded for half of the
+                // row groups at a time (the whole wave tile at once spilled: GELU' 256x192, 27 registers), with a scheduling
+            // fence per row group
+                constexpr int PREG = PRE ? TM * (NP * (int)sizeof(pa8) + ODD * (int)sizeof(pa4)) / 4 : 0;
+                constexpr int PH = (NW >= 8 && PREG > 24 && TM % 2 == 0) ? 2 : 1;
+                constexpr int TMP = TM / PH;
+                float bv[NP > 0 ? NP : 1][8], bo[4];
+        #pragma unroll
                 for (int q = 0; q < NP; ++q) {
-                    float v[8] = {acc[a0 + a][2 * q][0], acc[a0 + a][2 * q][1], acc[a0 + a][2 * q][2], acc[a0 + a][2 * q][3],
-                                  acc[a0 + a][2 * q + 1][0], acc[a0 + a][2 * q + 1][1], acc[a0 + a][2 * q + 1][2],
-                                  acc[a0 + a][2 * q + 1][3]};
-                    if constexpr (PRE) finish(v, 8, bv[q], p8[a][q], ro + q * 32 + fg * 8);
-                    else finish(v, 8, bv[q], 0, ro + q * 32 + fg * 8);
+                    if (g.bias) load8f<float>(g.bias + nb + q * 32 + fg * 8, bv[q]);
+                    else for (int i = 0; i < 8; ++i) bv[q][i] = 0.f;
                 }
                 if constexpr (ODD) {
-                    float v[4] = {acc[a0 + a][TN - 1][0], acc[a0 + a][TN - 1][1], acc[a0 + a][TN - 1][2], acc[a0 + a][TN - 1][3]};
-                    if constexpr (PRE) finish(v, 4, bo, p4[a], ro + NP * 32 + fg * 4);
-                    else finish(v, 4, bo, 0, ro + NP * 32 + fg * 4);
+                    if (g.bias) load4<float>(g.bias + nb + NP * 32 + fg * 4, bo);
+                    else for (int i = 0; i < 4; ++i) bo[i] = 0.f;
                 }
-                if constexpr (NW >= 8) __builtin_amdgcn_sched_barrier(0);
-            }
-        });
-    } else {
-    // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i].
-    // Staged through LDS in passes of EPR rows (row pitch BN+4 floats: conflict-free b128 writes),
-    // then every thread finishes 8 consecutive columns of a row: coalesced 16-B loads of resid/aux
-    // and 16-B (or 2x16-B) stores, 4-8x fewer store instructions than the fragment layout.
-    TO* C = reinterpret_cast<TO*>(g.C);
-    constexpr int EPR = ep_rows<BM, BN, S, ROWB, WM>();
-    static_assert(EPR % WM == 0 && BM % EPR == 0, "epilogue passes");
-    constexpr int EPL = BN + 4;
-    constexpr int NT = 64 * NW;
-    constexpr int C8 = BN / 8;
-    float* ep = reinterpret_cast<float*>(smem);
-    float col_s = 0.f, col_q = 0.f;               // EPI_STATS: column tid's sums over the tile's rows
-    // Epilogue operands (resid / aux / aux2) of a pass are all loaded before the tile is staged through
-    // LDS (unconditional, row-clamped loads: no per-element branch or vmcnt(0)), so their latency
-    // hides under the staging stores and barriers instead of being paid per row chunk.
-    constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID || EPI == EPI_ADD_RELU_GRAD;
-    constexpr int NCH = EPR * C8;                // 8-column chunks per pass
-    constexpr int NIT = (NCH + NT - 1) / NT;
-    using PA = typename std::conditional<EPI == EPI_RESID, float, T>::type;
-    typedef PA pa8 __attribute__((ext_vector_type(8)));
-    typedef T t8v __attribute__((ext_vector_type(8)));
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#pragma unroll 1
-    for (int pass = 0; pass < BM / EPR; ++pass) {
-        pa8 pre[PRE ? NIT : 1];
-        t8v pre2[EPI == EPI_ADD_RELU_GRAD ? NIT : 1];
-        if constexpr (PRE) {
-            const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
-#pragma unroll
-            for (int k = 0; k < NIT; ++k) {
-                const int c = min(tid + k * NT, NCH - 1), r = c / C8, col = (c % C8) * 8;
-                const int m = min(m0 + pass * EPR + r, g.M - 1);
-                const size_t off = (size_t)m * g.N + n0 + col;
-                pre[k] = *reinterpret_cast<const pa8*>(src + off);
-                if constexpr (EPI == EPI_ADD_RELU_GRAD)
-                    pre2[k] = *reinterpret_cast<const t8v*>(reinterpret_cast<const T*>(g.aux2) + off);
-            }
-        }
-        __syncthreads();
-        if ((wm * WM) / EPR == pass) {
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b)
-                    *reinterpret_cast<float4*>(ep + (wm * WM - pass * EPR + a * 16 + fr) * EPL + wn * WN + b * 16 + 4 * fg) =
-                        make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) {
-            const int c = tid + k * NT;
-            if (NCH % NT != 0 && c >= NCH) break;
-            const int r = c / C8, col = (c % C8) * 8;
-            const int m = m0 + pass * EPR + r;
-            if (m >= g.M) continue;
-            const int n = n0 + col;
-            const size_t off = (size_t)m * g.N + n;
-            const float4 x0 = *reinterpret_cast<const float4*>(ep + r * EPL + col);
-            const float4 x1 = *reinterpret_cast<const float4*>(ep + r * EPL + col + 4);
-            float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            if (g.bias) {
-                const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
-                const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
-                v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-                v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-            }
-            if constexpr (EPI == EPI_GELU) {
-                if (g.aux) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] = quick_gelu(v[i]);
-            } else if constexpr (EPI == EPI_GELU_BWD) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] *= quick_gelu_grad((float)pre[k][i]);
-            } else if constexpr (EPI == EPI_ADD_RELU_GRAD) {
-                // decoder: conv1's input gradient plus the residual branch's (models/utils.py:300-302)
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] += (float)pre2[k][i] > 0.f ? (float)pre[k][i] : 0.f;
-            } else if constexpr (EPI == EPI_RESID) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] += pre[k][i];
-            }
-            store8<TO>(C + off, v);
-        }
-        if constexpr (EPI == EPI_STATS) {
-            // BatchNorm batch statistics of the conv output (models/utils.py:254-303 bn1/bn2): per-tile
-            // column partials of sum and sum of squares, from the f32 accumulators (+ bias)
-            const int rows = min(EPR, g.M - (m0 + pass * EPR));
-            if (tid < BN) {
-                const float bc = g.bias ? g.bias[n0 + tid] : 0.f;
-#pragma unroll 4
-                for (int r = 0; r < rows; ++r) {
-                    const float x = ep[r * EPL + tid] + bc;
-                    col_s += x;
-                    col_q = fmaf(x, x, col_q);
+                auto finish = [&](float* v, int w, const float* bias, const auto& pre, size_t off) {
+                    for (int i = 0; i < w; ++i) v[i] += bias[i];
+                    if constexpr (EPI == EPI_GELU) {
+                        if (g.aux) {
+                            if (w == 8) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
+                            else store4<T>(reinterpret_cast<T*>(g.aux) + off, v);
+                        }
+                        for (int i = 0; i < w; ++i) v[i] = quick_gelu(v[i]);
+                    } else if constexpr (EPI == EPI_GELU_BWD) {
+                        for (int i = 0; i < w; ++i) v[i] *= quick_gelu_grad((float)pre[i]);
+                    } else if constexpr (EPI == EPI_RESID) {
+                        for (int i = 0; i < w; ++i) v[i] += pre[i];
+                    }
+                    if (w == 8) store8<TO>(C + off, v);
+                    else store4<TO>(C + off, v);
+                };
+                static_for<0, PH>([&](auto phc) {
+                    constexpr int a0 = decltype(phc)::value * TMP;
+                    pa8 p8[PRE ? TMP : 1][NP > 0 ? NP : 1];
+                    pa4 p4[PRE && ODD ? TMP : 1];
+                    if constexpr (PREF) {
+        #pragma unroll
+                        for (int a = 0; a < TMP; ++a) {
+        #pragma unroll
+                            for (int q = 0; q < NP; ++q) p8[a][q] = rp8[a0 + a][q];
+                            if constexpr (ODD) p4[a] = rp4[a0 + a];
+                        }
+                    } else if constexpr (PREF_G && a0 == 0 && TMP == TM / 2) {
+        #pragma unroll
+                        for (int a = 0; a < TMP; ++a)
+        #pragma unroll
+                            for (int q = 0; q < NP; ++q) p8[a][q] = __builtin_convertvector(gp8[a][q], pa8);
+                    } else if constexpr (PRE) {
+                        const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
+        #pragma unroll
+                        for (int a = 0; a < TMP; ++a) {
+                            const size_t ro = (size_t)min(mb + (a0 + a) * 16, g.M - 1) * g.N + nb;
+        #pragma unroll
+                            for (int q = 0; q < NP; ++q) p8[a][q] = *reinterpret_cast<const pa8*>(src + ro + q * 32 + fg * 8);
+                            if constexpr (ODD) p4[a] = *reinterpret_cast<const pa4*>(src + ro + NP * 32 + fg * 4);
+                        }
+                    }
+        #pragma unroll
+                    for (int a = 0; a < TMP; ++a) {
+                        const int m = mb + (a0 + a) * 16;
+                        if (m >= g.M) break;                 // rows ascend with a
+                        const size_t ro = (size_t)m * g.N + nb;
+        #pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            float v[8] = {acc[a0 + a][2 * q][0], acc[a0 + a][2 * q][1], acc[a0 + a][2 * q][2], acc[a0 + a][2 * q][3],
+                                          acc[a0 + a][2 * q + 1][0], acc[a0 + a][2 * q + 1][1], acc[a0 + a][2 * q + 1][2],
+                                          acc[a0 + a][2 * q + 1][3]};
+                            if constexpr (PRE) finish(v, 8, bv[q], p8[a][q], ro + q * 32 + fg * 8);
+                            else finish(v, 8, bv[q], 0, ro + q * 32 + fg * 8);
+                        }
+                        if constexpr (ODD) {
+                            float v[4] = {acc[a0 + a][TN - 1][0], acc[a0 + a][TN - 1][1], acc[a0 + a][TN - 1][2], acc[a0 + a][TN - 1][3]};
+                            if constexpr (PRE) finish(v, 4, bo, p4[a], ro + NP * 32 + fg * 4);
+                            else finish(v, 4, bo, 0, ro + NP * 32 + fg * 4);
+                        }
+                        if constexpr (NW >= 8) __builtin_amdgcn_sched_barrier(0);
+                    }
+                });
+            } else {
+            // epilogue: acc[a][b][i] = C[m = m0 + wm*WM + a*16 + fr][n = n0 + wn*WN + b*16 + 4*fg + i].
+            // Staged through LDS in passes of EPR rows (row pitch BN+4 floats: conflict-free b128 writes),
+            // then every thread finishes 8 consecutive columns of a row: coalesced 16-B loads of resid/aux
+            // and 16-B (or 2x16-B) stores, 4-8x fewer store instructions than the fragment layout.
+            TO* C = reinterpret_cast<TO*>(g.C);
+            constexpr int EPR = ep_rows<BM, BN, S, ROWB, WM>();
+            static_assert(EPR % WM == 0 && BM % EPR == 0, "epilogue passes");
+            constexpr int EPL = BN + 4;
+            constexpr int NT = 64 * NW;
+            constexpr int C8 = BN / 8;
+            float* ep = reinterpret_cast<float*>(smem);
+            float col_s = 0.f, col_q = 0.f;               // EPI_STATS: column tid's sums over the tile's rows
+            // Epilogue operands (resid / aux / aux2) of a pass are all loaded before the tile is staged through
+            // LDS (unconditional, row-clamped loads: no per-element branch or vmcnt(0)), so their latency
+            // hides under the staging stores and barriers instead of being paid per row chunk.
+            constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID || EPI == EPI_ADD_RELU_GRAD;
+            constexpr int NCH = EPR * C8;                // 8-column chunks per pass
+            constexpr int NIT = (NCH + NT - 1) / NT;
+            using PA = typename std::conditional<EPI == EPI_RESID, float, T>::type;
+            typedef PA pa8 __attribute__((ext_vector_type(8)));
+            typedef T t8v __attribute__((ext_vector_type(8)));
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        #pragma unroll 1
+            for (int pass = 0; pass < BM / EPR; ++pass) {
+                pa8 pre[PRE ? NIT : 1];
+                t8v pre2[EPI == EPI_ADD_RELU_GRAD ? NIT : 1];
+                if constexpr (PRE) {
+                    const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
+        #pragma unroll
+                    for (int k = 0; k < NIT; ++k) {
+                        const int c = min(tid + k * NT, NCH - 1), r = c / C8, col = (c % C8) * 8;
+                        const int m = min(m0 + pass * EPR + r, g.M - 1);
+                        const size_t off = (size_t)m * g.N + n0 + col;
+                        pre[k] = *reinterpret_cast<const pa8*>(src + off);
+                        if constexpr (EPI == EPI_ADD_RELU_GRAD)
+                            pre2[k] = *reinterpret_cast<const t8v*>(reinterpret_cast<const T*>(g.aux2) + off);
+                    }
+                }
+                __syncthreads();
+                if ((wm * WM) / EPR == pass) {
+        #pragma unroll
+                    for (int a = 0; a < TM; ++a)
+        #pragma unroll
+                        for (int b = 0; b < TN; ++b)
+                            *reinterpret_cast<float4*>(ep + (wm * WM - pass * EPR + a * 16 + fr) * EPL + wn * WN + b * 16 + 4 * fg) =
+                                make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+                }
+                __syncthreads();
+        #pragma unroll
+                for (int k = 0; k < NIT; ++k) {
+                    const int c = tid + k * NT;
+                    if (NCH % NT != 0 && c >= NCH) break;
+                    const int r = c / C8, col = (c % C8) * 8;
+                    const int m = m0 + pass * EPR + r;
+                    if (m >= g.M) continue;
+                    const int n = n0 + col;
+                    const size_t off = (size_t)m * g.N + n;
+                    const float4 x0 = *reinterpret_cast<const float4*>(ep + r * EPL + col);
+                    const float4 x1 = *reinterpret_cast<const float4*>(ep + r * EPL + col + 4);
+                    float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                    if (g.bias) {
+                        const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
+                        const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
+                        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+                        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+                    }
+                    if constexpr (EPI == EPI_GELU) {
+                        if (g.aux) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
+        #pragma unroll
+                        for (int i = 0; i < 8; ++i) v[i] = quick_gelu(v[i]);
+                    } else if constexpr (EPI == EPI_GELU_BWD) {
+        #pragma unroll
+                        for (int i = 0; i < 8; ++i) v[i] *= quick_gelu_grad((float)pre[k][i]);
+                    } else if constexpr (EPI == EPI_ADD_RELU_GRAD) {
+                        // decoder: conv1's input gradient plus the residual branch's (models/utils.py:300-302)
+        #pragma unroll
+                        for (int i = 0; i < 8; ++i) v[i] += (float)pre2[k][i] > 0.f ? (float)pre[k][i] : 0.f;
+                    } else if constexpr (EPI == EPI_RESID) {
+        #pragma unroll
+                        for (int i = 0; i < 8; ++i) v[i] += pre[k][i];
+                    }
+                    store8<TO>(C + off, v);
+                }
+                if constexpr (EPI == EPI_STATS) {
+                    // BatchNorm batch statistics of the conv output (models/utils.py:254-303 bn1/bn2): per-tile
+                    // column partials of sum and sum of squares, from the f32 accumulators (+ bias)
+                    const int rows = min(EPR, g.M - (m0 + pass * EPR));
+                    if (tid < BN) {
+                        const float bc = g.bias ? g.bias[n0 + tid] : 0.f;
+        #pragma unroll 4
+                        for (int r = 0; r < rows; ++r) {
+                            const float x = ep[r * EPL + tid] + bc;
+                            col_s += x;
+                            col_q = fmaf(x, x, col_q);
+                        }
+                    }
                 }
             }
+            if constexpr (EPI == EPI_STATS) {
+                if (tid < BN) {
+                    g.stats[(size_t)tm * 2 * g.N + n0 + tid] = col_s;
+                    g.stats[((size_t)tm * 2 + 1) * g.N + n0 + tid] = col_q;
+                }
+            }
+            }   // staged epilogue (MODE 1 / 2)
+        }   // fin
+        return nk;
+    };
+    const unsigned nk1 = (unsigned)segment(it_beg);
+    if constexpr (SKM) {
+        if (skr && it_beg + nk1 < it_end) {
+            __syncthreads();     // every wave done with the ring and the epilogue's LDS before the next segment fills it
+            segment(it_beg + nk1);
         }
     }
-    if constexpr (EPI == EPI_STATS) {
-        if (tid < BN) {
-            g.stats[(size_t)tm * 2 * g.N + n0 + tid] = col_s;
-            g.stats[((size_t)tm * 2 + 1) * g.N + n0 + tid] = col_q;
-        }
-    }
-    }   // staged epilogue (MODE 1 / 2)
 }
 
 template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, int ROWB, int MODE, bool SPL, int NLW = 0>
@@ -825,7 +881,13 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
     if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
     const int tiles = g.ntile ? g.ntile : ((g.M + BM - 1) / BM) * (g.N / BN) - g.tile0;
     if (tiles <= 0 || g.tile0 + tiles > ((g.M + BM - 1) / BM) * (g.N / BN)) return EBC_E_ARG;
-    const int nwg = tiles * g.splits;
+    if (g.sk_total) {
+        if (!SPL || MODE == 0 || g.splits != 1 || g.sk_nk * BK != g.K || (long)tiles * g.sk_nk != g.sk_total ||
+            g.sk_grid < tiles || g.sk_grid > g.sk_total || (g.sk_total + 1) * g.sk_grid >= (1L << 31) || !g.cnt ||
+            !g.part || tiles > 4096)
+            return EBC_E_ARG;
+    }
+    const int nwg = g.sk_total ? g.sk_grid : tiles * g.splits;
     const int pi = probe_on() ? probe_start(EBC_PROBE_GEMM, EPI, BM, BN, MODE, g.M, g.N, g.kalg ? g.kalg : g.K, st) : -1;
     hipLaunchKernelGGL((gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL, NLW>), dim3(nwg),
                        dim3(64 * (WGM * WGN + NLW)), LDS, st, g);
@@ -839,7 +901,7 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
 template <class E, class TO, int EPI, int BM, int BN, int S, int WGM = 2, int WGN = 2, int ROWB = 128, int MODE = 0, int NLW = 0>
 int launch_gemm(const GemmArgs& g, hipStream_t st)
 {
-    if (g.splits > 1) {
+    if (g.splits > 1 || g.sk_total) {
         if constexpr (NLW == 0 && (MODE != 0 || EPI == EPI_STORE))
             return launch_gemm_k<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, true>(g, st);
         else return EBC_E_UNSUPPORTED;
@@ -1062,34 +1124,36 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
     if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;
     return N % 96 == 0 ? 13 : 2;
 }
-// Split-K tail for the implicit-GEMM convolutions (MODE 1, one 256-wide workgroup per CU): when T tiles are a few
-// more than whole waves (the ResNet-50 decoder: 784 = 3 x 256 + 16 tiles of 256x256), the T mod 256 last tiles
-// would run as a fourth, nearly empty wave of whole-K tiles.  Instead the whole waves run as one launch and the
-// tail tiles as a second with K split s ways (last arriver sums the f32 partials in split order), s from the
-// same fill / MFMA cost model as the weight-gradient plans plus the last arriver's re-read.
-struct TailPlan { int dp, tail, splits; };
-TailPlan tail_plan(int cfg, int M, int N, int K, int bk) {
-    if (cfg != 3 && cfg != 7) return TailPlan{0, 0, 1};
+// Stream-K for the implicit-GEMM convolutions (one 256-wide 8-wave workgroup per CU): when the launch's workgroups
+// fill their last wave of CUs poorly, a grid of up to NUM_CU workgroups shares the k-tiles of the tiles past the
+// last whole wave evenly (the whole waves run first as a plain launch of whole tiles, `dp`); a tile cut between
+// workgroups is summed by the last piece to arrive (gemm_nt_kernel, SKM), at most 4 pieces a tile: the last piece
+// re-reads the others' partials through one CU (the ResNet-50 decoder's 16 tail tiles of 288 k-tiles: 64
+// workgroups, not 256 pieces of 18 k-tiles re-read 16-deep).  Where it is taken, measured (tools/lab/conv_lab.hip,
+// interleaved, profiles/r04d_conv_lab_*.txt):
+//   MODE 1 with more tiles than CUs: 32 crops, 392 256x192 tiles (1.53 waves): 244-248 us vs 266-278 plain
+//     (fewer tiles than CUs, 16 crops' 196: 140-143 us vs 138-142 plain -- no gain, not taken)
+//   MODE 2 up to 256 k-tiles a tile: the 16-crop weight gradient (108 tiles x 196 k-tiles): 140-143 us vs 144-152
+//     on 2 splits (216 workgroups); 32 crops (392 k-tiles): 269-272 us vs 247-253 on 2 splits, not taken
+struct SkPlan { int dp; long total; int nk, grid; };
+SkPlan sk_plan(int mode, int cfg, int M, int N, int K, int bk, long wgs) {
+    if (cfg != 3 && cfg != 7) return SkPlan{0, 0, 0, 0};
     const TileCfg* c = find_cfg(cfg);
-    const long T = ntiles(M, N, c->bm, c->bn), R = T % NUM_CU, kit = K / bk;
-    if (T < NUM_CU || R == 0 || R > (long)(GEMM_CNT_BYTES / 4)) return TailPlan{0, 0, 1};
-    auto piece = [&](double k) { return std::max((c->bm + c->bn) * k * 2 / 70e9, 2.0 * c->bm * c->bn * k / 8e12); };
-    double best = piece(K);
-    int bs = 1;
-    for (int sp = 2; sp <= 64; ++sp) {
-        if (kit % sp || R * sp > NUM_CU || kit / sp < 8) continue;
-        const double t = piece((double)K / sp) + (double)sp * c->bm * c->bn * 4 / 70e9 + 4e-6;
-        if (t < best) { best = t; bs = sp; }
-    }
-    if (bs == 1) return TailPlan{0, 0, 1};
-    return TailPlan{(int)(T - R), (int)R, bs};
+    const long T = ntiles(M, N, c->bm, c->bn), nk = K / bk;
+    const long waves = (wgs + NUM_CU - 1) / NUM_CU;
+    const double fill = (double)wgs / (double)(waves * NUM_CU);
+    const long dp = T / NUM_CU * NUM_CU, rest = T - dp;
+    if (mode == 1 ? dp == 0 : nk > 256) return SkPlan{0, 0, 0, 0};
+    const int grid = (int)std::min<long>(NUM_CU, rest * 4);
+    if (fill >= 0.92 || rest == 0 || rest * nk < 16L * grid) return SkPlan{0, 0, 0, 0};
+    return SkPlan{(int)dp, rest * nk, (int)nk, grid};
 }
-// conv workspace: [arrival counters][EPI_STATS per-tile-row partials (BM >= 128)][split-K tail partials]
+size_t sk_ws_bytes(int cfg, const SkPlan& p) {
+    const TileCfg* c = find_cfg(cfg);
+    return p.total ? (size_t)2 * p.grid * c->bm * c->bn * 4 : 0;
+}
+// conv workspace: [arrival counters][EPI_STATS per-tile-row partials (BM >= 128)][stream-K partials]
 size_t conv_stats_bytes(int M, int N) { return (((size_t)((M + 127) / 128) * 2 * N * 4 + 255) / 256) * 256; }
-size_t tail_ws_bytes(int cfg, const TailPlan& p) {
-    const TileCfg* c = find_cfg(cfg);
-    return p.splits > 1 ? (size_t)p.tail * p.splits * c->bm * c->bn * 4 : 0;
-}
 int conv_splits(int cfg, int mode, int M, int N, int nk)
 {
     if (mode != 2) return 1;
@@ -1120,6 +1184,35 @@ int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream
         return splitk_reduce(g.part, reinterpret_cast<float*>(g.C), (long)g.M * g.N, wp.splits, st);
     }
     int splits = planned ? wp.splits : conv_splits(cfg, mode, g.M, g.N, g.K / BK);
+    using T = typename E::T;
+    if (SIXTEEN) {
+        const SkPlan sk = sk_plan(mode, cfg, g.M, g.N, g.K, BK, ntiles(g.M, g.N, c->bm, c->bn) * splits);
+        const size_t off = GEMM_CNT_BYTES + (mode == 1 ? conv_stats_bytes(g.M, g.N) : 0);
+        if (sk.total && ws && wsb >= off + sk_ws_bytes(cfg, sk)) {
+            g.splits = 1;
+            g.kslice = g.K;
+            if (sk.dp) {
+                GemmArgs d = g;
+                d.ntile = sk.dp;
+                if (mode == 1 && epi == EPI_STORE) EBC_TRY((launch_conv_tile<E, T, EPI_STORE, 1>(d, cfg, st)));
+                else if (mode == 1 && epi == EPI_STATS) EBC_TRY((launch_conv_tile<E, T, EPI_STATS, 1>(d, cfg, st)));
+                else if (mode == 1 && epi == EPI_ADD_RELU_GRAD) EBC_TRY((launch_conv_tile<E, T, EPI_ADD_RELU_GRAD, 1>(d, cfg, st)));
+                else if (mode == 2 && epi == EPI_STORE) EBC_TRY((launch_conv_tile<E, float, EPI_STORE, 2>(d, cfg, st)));
+                else return EBC_E_UNSUPPORTED;
+                g.tile0 = sk.dp;
+            }
+            g.sk_total = sk.total;
+            g.sk_nk = sk.nk;
+            g.sk_grid = sk.grid;
+            g.cnt = reinterpret_cast<int*>(ws);
+            g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + off);
+            if (mode == 1 && epi == EPI_STORE) return launch_conv_tile<E, T, EPI_STORE, 1>(g, cfg, st);
+            if (mode == 1 && epi == EPI_STATS) return launch_conv_tile<E, T, EPI_STATS, 1>(g, cfg, st);
+            if (mode == 1 && epi == EPI_ADD_RELU_GRAD) return launch_conv_tile<E, T, EPI_ADD_RELU_GRAD, 1>(g, cfg, st);
+            if (mode == 2 && epi == EPI_STORE) return launch_conv_tile<E, float, EPI_STORE, 2>(g, cfg, st);
+            return EBC_E_UNSUPPORTED;
+        }
+    }
     if (splits > 1) {
         const size_t tiles = (size_t)ntiles(g.M, g.N, c->bm, c->bn);
         const size_t need = GEMM_CNT_BYTES + (size_t)splits * tiles * c->bm * c->bn * 4;
@@ -1132,28 +1225,6 @@ int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream
     }
     g.splits = splits;
     g.kslice = g.K / splits;
-    using T = typename E::T;
-    if (mode == 1 && SIXTEEN && splits == 1) {
-        const TailPlan tp = tail_plan(cfg, g.M, g.N, g.K, BK);
-        const size_t off = GEMM_CNT_BYTES + conv_stats_bytes(g.M, g.N);
-        if (tp.splits > 1 && ws && wsb >= off + tail_ws_bytes(cfg, tp)) {
-            GemmArgs d = g, t = g;
-            d.ntile = tp.dp;
-            t.tile0 = tp.dp;
-            t.ntile = tp.tail;
-            t.splits = tp.splits;
-            t.kslice = g.K / tp.splits;
-            t.cnt = reinterpret_cast<int*>(ws);
-            t.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + off);
-            for (const GemmArgs* a : {&d, &t}) {
-                if (epi == EPI_STORE) EBC_TRY((launch_conv_tile<E, T, EPI_STORE, 1>(*a, cfg, st)));
-                else if (epi == EPI_STATS) EBC_TRY((launch_conv_tile<E, T, EPI_STATS, 1>(*a, cfg, st)));
-                else if (epi == EPI_ADD_RELU_GRAD) EBC_TRY((launch_conv_tile<E, T, EPI_ADD_RELU_GRAD, 1>(*a, cfg, st)));
-                else return EBC_E_UNSUPPORTED;
-            }
-            return EBC_OK;
-        }
-    }
     if (mode == 1 && epi == EPI_STORE) return launch_conv_tile<E, T, EPI_STORE, 1>(g, cfg, st);
     if (mode == 1 && epi == EPI_STATS) return launch_conv_tile<E, T, EPI_STATS, 1>(g, cfg, st);
     if (mode == 1 && epi == EPI_ADD_RELU_GRAD) return launch_conv_tile<E, T, EPI_ADD_RELU_GRAD, 1>(g, cfg, st);
@@ -1172,10 +1243,19 @@ size_t conv_gemm_workspace_bytes(int dtype, int mode, int M, int N, int K)
         need += conv_stats_bytes(M, N);                                // EPI_STATS partials (BM >= 128)
         if (sixteen) {
             const int cfg = conv_cfg(sixteen, mode, M, N);
-            need += tail_ws_bytes(cfg, tail_plan(cfg, M, N, K, 64));
+            const TileCfg* c = find_cfg(cfg);
+            need += sk_ws_bytes(cfg, sk_plan(mode, cfg, M, N, K, 64, ntiles(M, N, c->bm, c->bn)));
         }
     }
-    if (mode == 2) return std::max(need, wplan_ws(wgrad_plan(sixteen, true, M, N, K), M, N));
+    if (mode == 2) {
+        const WPlan wp = wgrad_plan(sixteen, true, M, N, K);
+        size_t skb = 0;
+        if (sixteen && !wp.partials) {
+            const TileCfg* c = find_cfg(wp.cfg);
+            skb = GEMM_CNT_BYTES + sk_ws_bytes(wp.cfg, sk_plan(2, wp.cfg, M, N, K, 64, ntiles(M, N, c->bm, c->bn) * wp.splits));
+        }
+        return std::max({need, wplan_ws(wp, M, N), skb});
+    }
     const int cfg = conv_cfg(sixteen, mode, M, N);
     const TileCfg* c = find_cfg(cfg);
     const int bk = !sixteen ? 32 : 64;
@@ -1381,20 +1461,26 @@ extern "C" int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, in
 {
     if (M <= 0 || N <= 0 || K <= 0 || (mode != 1 && mode != 2)) return EBC_E_ARG;
     const bool sixteen = dtype != EBC_F32;
+    const int bk = !sixteen ? 32 : 64;
+    int cfg, splits;
     if (mode == 2) {
         const WPlan wp = wgrad_plan(sixteen, true, M, N, K);
-        const TileCfg* c = find_cfg(wp.cfg);
-        if (out) { out[0] = c->bm; out[1] = c->bn; out[2] = wp.splits; }
-        return wp.cfg;
+        cfg = wp.cfg;
+        splits = wp.splits;
+        if (wp.partials) splits = -splits;           // never stream-K: reported as split-K
+    } else {
+        cfg = conv_cfg(sixteen, mode, M, N);
+        splits = conv_splits(cfg, mode, M, N, K / bk);
     }
-    const int cfg = conv_cfg(sixteen, mode, M, N);
     const TileCfg* c = find_cfg(cfg);
-    if (out) {
-        const int bk = !sixteen ? 32 : 64;
-        out[0] = c->bm;
-        out[1] = c->bn;
-        out[2] = conv_splits(cfg, mode, M, N, K / bk);
+    if (splits < 0) {
+        splits = -splits;
+    } else if (sixteen) {
+        // dispatch_conv: stream-K whenever sk_plan takes the launch (a workspace of conv_gemm_workspace_bytes)
+        const SkPlan sk = sk_plan(mode, cfg, M, N, K, bk, ntiles(M, N, c->bm, c->bn) * splits);
+        if (sk.total) splits = -sk.grid;
     }
+    if (out) { out[0] = c->bm; out[1] = c->bn; out[2] = splits; }
     return cfg;
 }
 #endif  // EBC_GEMM_LAB

@@ -276,7 +276,9 @@ int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, void* out, 
                     const void* add_y, void* ws, size_t wsb, int B, int H, int W, int C, int N, ebc_stream_t stream);
 /* The implicit-GEMM tile configuration of a decoder conv product (mode 1: forward / data gradient,
  * M = B*H*W rows, N output channels, K = 9*C; mode 2: weight gradient, M = N channels, N = 9*C,
- * K = interior pixel rows): returns its id, out[3] = {tile rows, tile columns, split-K}. Host-only. */
+ * K = interior pixel rows): returns its id, out[3] = {tile rows, tile columns, split-K ways}; out[2] = -G: stream-K,
+ * G workgroups share the k-tiles of the tiles past the last whole wave of 256 (those run first as a plain
+ * launch). Host-only. */
 int ebc_conv_tile_config(int dtype, int mode, int M, int N, int K, int* out);
 /* dw[N][C][3][3] f32 = weight gradient from dzT and xT3 */
 int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, float* dw, void* ws, size_t wsb, int B, int H,

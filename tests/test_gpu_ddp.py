@@ -63,13 +63,26 @@ def test_ddp_syncbn_step_matches_single_process(tmp_path):
         infos.append(info)
         b0 += n
     total.backward()
+    # Bar: rel-L2 3e-3.  The two decompositions sum the decoder's BatchNorm statistics over different row tiles (each
+    # rank's last conv tile is partial), so the f32 mean / rstd can differ in the last bit, and a ReLU pre-activation
+    # within that of zero then takes the other mask value: the gradient moves by O(gy) at one pixel and channel and
+    # carries into every parameter upstream.  r04: the attention forward's new summation order (packed f32 row sums)
+    # moved this test from 1.6e-6 to 1.1e-3 on bn1.bias; bisected by swapping that one source file between builds
+    # (tools/dbg/ddp_bisect.sh), and the attention itself is bitwise repeatable and batch-invariant per (crop, head)
+    # (tools/dbg/attn_inv.py), so the ranks and the single process see the same encoder outputs.
+    # A wrong SyncBatchNorm exchange (count weighting, a missing all-reduce) is off by 1e-1 or more.
+    bad, worst = [], (None, 0.0)
     for k, p in m.named_parameters():
         if not p.requires_grad:
             continue
         g = p.grad.detach().cpu().numpy()
-        for r in (r0, r1):
+        for rank, r in enumerate((r0, r1)):
             err = rel_l2(r[k].numpy(), g)
-            assert err < 2e-4, (k, err)
+            worst = max(worst, (k, err), key=lambda e: e[1])
+            if err >= 3e-3:
+                bad.append((k, rank, err))
+    print("worst gradient rel-L2", worst)
+    assert not bad, bad
     for k, b in m.named_buffers():
         if "running" in k:
             for r in (r0, r1):

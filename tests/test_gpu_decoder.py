@@ -44,6 +44,9 @@ def _block(C):
 
 
 @pytest.mark.parametrize("dtype,B,h,C,up", [(torch.float32, 2, 14, 768, 2), (torch.float16, 2, 14, 768, 2),
+                                            # one crop: the weight gradient's K = 784 columns in 832 (its last k-tile
+                                            # past the image)
+                                            (torch.float32, 1, 14, 768, 2),
                                             (torch.bfloat16, 2, 14, 768, 2), (torch.float32, 3, 7, 128, 1),
                                             (torch.float16, 3, 10, 192, 2),
                                             # H = W = 14: 196 pixels per image, the weight gradient's K padded to 200
@@ -160,13 +163,15 @@ def test_conv3x3_abi_matches_torch():
     np.testing.assert_allclose(colsum[1].cpu().numpy(), (ref ** 2).sum(0).numpy(), rtol=2e-3)
 
 
-@pytest.mark.parametrize("B,H,C,N", [(16, 28, 256, 768),    # 196 tiles of 256x192 < 256 CUs: one launch
-                                     (8, 56, 256, 2048),    # 784 tiles of 256x256: 768 whole + 16 split-K tail tiles
-                                     (8, 56, 128, 1024)])   # 392 tiles: 256 whole + 136 tail tiles
-def test_conv3x3_split_tail(B, H, C, N):
-    """ebc_conv3x3_fwd at shapes whose last wave of tiles would leave CUs idle (gemm.hip tail_plan): whole waves in
-    one launch, the tail tiles split-K in a second (last arriver sums the partials), with and without the BN
-    column-sum epilogue, vs torch conv2d."""
+@pytest.mark.parametrize("B,H,C,N,plan", [
+    (16, 28, 256, 768, (256, 192, 1)),       # 196 tiles of 256x192 < 256 CUs: one plain launch (measured no gain)
+    (8, 56, 512, 2048, (256, 256, -64)),     # 784 tiles of 256x256: 768 whole, then 16 tiles on 64 workgroups
+    (8, 56, 256, 1024, (256, 256, -256)),    # 392 tiles: 256 whole, then 136 tiles on 256 workgroups
+    (8, 56, 128, 1024, (256, 256, 1))])      # 18 k-tiles a tile: too short to share, plain launch
+def test_conv3x3_stream_k(B, H, C, N, plan):
+    """ebc_conv3x3_fwd at shapes whose last wave of tiles would leave CUs idle (gemm.hip sk_plan): the whole waves
+    as a plain launch, the other tiles' k-tiles shared by the stream-K grid (a tile cut between workgroups summed by
+    its last piece), with and without the BN column-sum epilogue, vs torch conv2d; bitwise equal across launches."""
     from ebc_amd import _lib
     import ctypes
     L = _lib.lib()
@@ -183,15 +188,22 @@ def test_conv3x3_split_tail(B, H, C, N):
     xpad = xpad.reshape(Q, C)
     wk = wt.permute(0, 2, 3, 1).contiguous()
     ref = F.conv2d(x.float(), wt.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, N).double()
+    cfg_out = (ctypes.c_int * 3)()
+    L.ebc_conv_tile_config(_lib.EBC_F16, 1, B * H * W, N, 9 * C, cfg_out)
+    assert tuple(cfg_out) == plan
     ws = torch.zeros(L.ebc_dec_workspace_bytes(_lib.EBC_F16, B, H, W, C, N), dtype=torch.uint8, device=dev)
     for stats in (True, False):
-        out = torch.empty(B * H * W, N, dtype=torch.float16, device=dev)
+        outs = []
         colsum = torch.empty(2, N, dtype=torch.float64, device=dev)
         for _ in range(2):                         # twice: the arrival counters must come back re-armed
+            out = torch.empty(B * H * W, N, dtype=torch.float16, device=dev)
             _lib.check(L.ebc_conv3x3_fwd(_lib.EBC_F16, _lib.ptr(xpad), _lib.ptr(wk), _lib.ptr(out),
                                          _lib.ptr(colsum) if stats else None, None, None, _lib.ptr(ws), ws.numel(),
                                          B, H, W, C, N, _lib.stream()), "conv")
+            outs.append(out)
         torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])       # the pieces' sum order is fixed: deterministic
+        out = outs[1]
         assert rel_l2(out.double(), ref) < 2e-3
         if stats:
             torch.testing.assert_close(colsum[0], ref.sum(0), rtol=1e-2, atol=2.0)

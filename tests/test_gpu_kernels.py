@@ -48,10 +48,12 @@ def test_layernorm_fwd_bwd(dname):
 
 
 @pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
-@pytest.mark.parametrize("B,L", [(3, 229), (2, 197), (1, 5), (2, 256), (2, 257), (1, 300), (2, 513), (1, 817)])
+@pytest.mark.parametrize("B,L", [(3, 229), (2, 197), (1, 5), (2, 256), (2, 257), (1, 300), (2, 513), (1, 817),
+                                 (22, 229)])
 def test_attention_fwd_bwd(dname, B, L):
     """L > 256: K / V (Q / dO) streamed through LDS in 256-row chunks, online softmax in the forward (817 = 448x448
-    inputs with 32 prompts, the reference trainer's default input_size)."""
+    inputs with 32 prompts, the reference trainer's default input_size).  22 crops x 12 heads = 264 (crop, head) units,
+    more than the 256 CUs: the forward's 8-wave workgroups of 128 queries (the 32-crop step's instance)."""
     dt = DT[dname]
     H = 12
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + L)

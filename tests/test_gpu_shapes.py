@@ -11,7 +11,7 @@ result against torch float64:
   * the 1x1 projection at 16 crops (M = 12544, 128x128, cfg 1) and its dX (128x64, cfg 2)
   * the eval batch (140 tiles, M = 32060): 256x256 (cfg 7) and 256x192 (cfg 3)
   * the decoder BasicBlock at 16 crops (M = 12544: 256x192 implicit GEMM with the BN-statistics,
-    store and ReLU-masked gradient-add epilogues, 2-way split-K weight gradient) in fp16 and bf16:
+    store and ReLU-masked gradient-add epilogues, stream-K weight gradient; 32 crops: stream-K convs) in fp16 and bf16:
     forward, every gradient, batch and running statistics
   * a whole 12-layer fp16 training step at 16 and 32 crops against the CPU oracle.
 """
@@ -144,17 +144,19 @@ def _decoder_ref(feat, w1, g1, b1, w2, g2, b2, rm, rv):
 def test_decoder_at_bench_batch(dname, B):
     """BasicBlock(768) after the x2 bilinear adapt at the bench's crop counts (M = B*784 rows): the 256x192
     implicit-GEMM tile for the forward convs (BN statistics epilogue), the data gradients (store and
-    ReLU-masked residual-gradient add) and the split-K weight gradients."""
+    ReLU-masked residual-gradient add) and the weight gradients, stream-K where gemm.hip sk_plan takes it."""
     from ebc_amd.model import _DecoderFn
     dt = DT[dname]
     C, h = 768, 14
     M = B * 784
-    assert conv_cfg(dt, 1, M, C, 9 * C)[0] == 3
+    # 196 tiles of 256x192: one plain launch; 32 crops, 392: 256 whole tiles, then 136 shared by 256 (stream-K)
+    assert conv_cfg(dt, 1, M, C, 9 * C) == (3, (256, 192, 1 if B == 16 else -256))
     geo = (ctypes.c_long * 6)()                         # {Hp, Wp, HWp, Kq, Q, Qs}: K of the wgrad = Kq
     _lib.check(_lib.lib().ebc_dec_geometry(_lib.dtype_code(dt), B, 2 * h, 2 * h, C, geo), "ebc_dec_geometry")
     assert geo[3] == B * 784                            # the interior pixels only (r03: B * 14 * 64 padded)
     cfg2, (_, _, splits) = conv_cfg(dt, 2, C, 9 * C, geo[3])
-    assert cfg2 == 3 and splits == 2, (cfg2, splits)
+    # 108 tiles x 196 k-tiles: stream-K over 256; x 392 k-tiles (32 crops): 2-way split-K (gemm.hip sk_plan)
+    assert cfg2 == 3 and splits == (-256 if B == 16 else 2), (cfg2, splits)
     blk = _block(C)
     g = torch.Generator(device="cuda").manual_seed(B)
     feat = torch.randn(B, h, h, C, device="cuda", generator=g)

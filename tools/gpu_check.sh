@@ -4,6 +4,7 @@
 # tests  the -m gpu suite (per-test timeout, stops at the first failure)
 # smoke  __graft_entry__.smoke()
 # bench  the default bench.py line (in-step roofline probe + CPU baseline) -> gpurun_out/TAG_bench.json
+# bench32  the same at 32 crops per GPU (the multi-GPU per-rank shape, configs[3]) -> gpurun_out/TAG_bench32.json
 # prof   rocprofv3 --kernel-trace --stats of bench.py, cut to the timed steps (tools/kstats.py --window)
 # ddp    the 2-rank DDP + SyncBN bench path with both ranks on cuda:0 over gloo (a rehearsal, not a scaling number)
 # t:EXPR only the -m gpu tests whose names match EXPR (pytest -k)
@@ -30,6 +31,11 @@ for what in "$@"; do
     bench)
       timeout -k 10 600 python -u bench.py > $O/${TAG}_bench.log 2>&1 || { tail -30 $O/${TAG}_bench.log; exit 1; }
       tail -1 $O/${TAG}_bench.log > $O/${TAG}_bench.json; cut -c1-400 $O/${TAG}_bench.json ;;
+    bench32)
+      # the multi-GPU runs' per-rank shape (configs[3]: 32 crops per GPU) on this one GPU
+      timeout -k 10 600 python -u bench.py --crops-per-gpu 32 --steps 30 --warmup 8 --no-cpu-baseline > $O/${TAG}_bench32.log 2>&1 \
+        || { tail -30 $O/${TAG}_bench32.log; exit 1; }
+      tail -1 $O/${TAG}_bench32.log > $O/${TAG}_bench32.json; cut -c1-400 $O/${TAG}_bench32.json ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o run -- \
         python3 $R/bench.py --steps 20 --warmup 10 --no-cpu-baseline --no-probe > $O/${TAG}_prof.log 2>&1) \

@@ -2,6 +2,7 @@
 //   mode 1  the implicit-GEMM conv (M = 12544, N = 768, K = 9 x 768) by tile: 256x192 (196 tiles = 77 % of the 256
 //           CUs), 224x192 (224 tiles, 88 %), 160x256 (237 tiles, 93 %); store and BN-statistics epilogues
 //   mode 2  the weight gradient over the interior pixels (K = 16 x 784 = 12544) by tile and split
+//   sk      stream-K: 256 workgroups share all tiles' k-tiles (gemm.hip sk_plan)
 // Interleaved rounds in one process; every variant compared with the first one of its mode.
 //   build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 -DEBC_GEMM_LAB \
 //          tools/lab/conv_lab.hip -o tools/lab/bin/conv_lab
@@ -42,7 +43,7 @@ struct V { std::string name; int mode; size_t outn; std::function<void(void*)> f
 int main(int argc, char** argv)
 {
     const int rounds = argc > 1 ? atoi(argv[1]) : 3, reps = argc > 2 ? atoi(argv[2]) : 10;
-    const int B = 16, H = 28, W = 28, C = 768, N = 768;
+    const int B = argc > 3 ? atoi(argv[3]) : 16, H = 28, W = 28, C = 768, N = 768;      // crops (16 or 32)
     const int Hp = H + 2, Wp = 32, HWp = H * W, M1 = B * H * W;
     const long Q = (long)B * Hp * Wp, Kq = (long)B * HWp, Pimg = (long)(H + 2) * W;
     const long Qs = ((std::max(Kq, (long)(B + 2) * Pimg + HWp + 2L * W + 64) + 63) / 64) * 64;
@@ -55,7 +56,7 @@ int main(int argc, char** argv)
     CK(hipMalloc(&xT3, (size_t)3 * C * Qs * 2));
     CK(hipMalloc(&dw, (size_t)2 * N * 9 * C * 4));
     char* ws;
-    const size_t wsb = GEMM_CNT_BYTES + (size_t)8 * N * 9 * C * 4;
+    const size_t wsb = GEMM_CNT_BYTES + std::max((size_t)8 * N * 9 * C * 4, (size_t)2 * 256 * 256 * 192 * 4);
     CK(hipMalloc(&ws, wsb));
     CK(hipMemset(ws, 0, wsb));
     CK(hipMalloc(&stats, (size_t)128 * 2 * N * 4));
@@ -65,13 +66,33 @@ int main(int argc, char** argv)
     hipLaunchKernelGGL(fill_f16, dim3(1024), dim3(256), 0, 0, xT3, (size_t)3 * C * Qs, 14u, 1.0f);
     CK(hipDeviceSynchronize());
 
-    auto conv = [&](auto tl, int epi) {
+    auto sk_args = [&](GemmArgs& g, int tiles, int nk) {
+        g.sk_total = (long)tiles * nk; g.sk_nk = nk; g.sk_grid = 256;
+        g.cnt = reinterpret_cast<int*>(ws);
+        g.part = reinterpret_cast<float*>(ws + GEMM_CNT_BYTES);
+    };
+    auto conv = [&](auto tl, int epi, bool sk = false) {
         using TT = decltype(tl);
-        return [&, epi](void* out) {
+        return [&, epi, sk](void* out) {
             GemmArgs g{xpad, wk, out, nullptr, nullptr, nullptr, M1, N, 9 * C};
             g.cH = H; g.cW = W; g.cC = C; g.cHp = Hp; g.cWp = Wp;
             g.splits = 1; g.kslice = 9 * C; g.stats = stats;
-            const int rc = epi == EPI_STATS
+            const int T = ((M1 + TT::BM - 1) / TT::BM) * (N / TT::BN), dp = T / 256 * 256;
+            if (sk && dp) {           // whole waves as a plain launch first (gemm.hip sk_plan)
+                GemmArgs d = g;
+                d.ntile = dp;
+                const int rc = epi == EPI_STATS
+                    ? launch_gemm_k<EF16, _Float16, EPI_STATS, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 1, false>(d, 0)
+                    : launch_gemm_k<EF16, _Float16, EPI_STORE, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 1, false>(d, 0);
+                if (rc) { printf("launch rc %d\n", rc); exit(1); }
+                g.tile0 = dp;
+            }
+            if (sk) sk_args(g, T - dp, 9 * C / 64);
+            const int rc = sk
+                ? (epi == EPI_STATS
+                   ? launch_gemm_k<EF16, _Float16, EPI_STATS, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 1, true>(g, 0)
+                   : launch_gemm_k<EF16, _Float16, EPI_STORE, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 1, true>(g, 0))
+                : epi == EPI_STATS
                 ? launch_gemm_k<EF16, _Float16, EPI_STATS, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 1, false>(g, 0)
                 : launch_gemm_k<EF16, _Float16, EPI_STORE, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 1, false>(g, 0);
             if (rc) { printf("launch rc %d\n", rc); exit(1); }
@@ -83,10 +104,11 @@ int main(int argc, char** argv)
             GemmArgs g{dzT, xT3, out, nullptr, nullptr, nullptr, N, 9 * C, (int)Kq};
             g.cH = H; g.cW = W; g.cC = C; g.cHp = Hp; g.cWp = Wp;
             g.cHWp = HWp; g.cQs = Qs; g.cPimg = Pimg;
-            g.splits = splits; g.kslice = (int)Kq / splits;
+            g.splits = splits > 0 ? splits : 1; g.kslice = (int)Kq / g.splits;
             g.cnt = splits > 1 ? reinterpret_cast<int*>(ws) : nullptr;
             g.part = splits > 1 ? reinterpret_cast<float*>(ws + GEMM_CNT_BYTES) : nullptr;
-            const int rc = splits > 1
+            if (splits == 0) sk_args(g, (N / TT::BM) * (9 * C / TT::BN), (int)Kq / 64);     // stream-K
+            const int rc = splits != 1
                 ? launch_gemm_k<EF16, float, EPI_STORE, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 2, true>(g, 0)
                 : launch_gemm_k<EF16, float, EPI_STORE, TT::BM, TT::BN, TT::S, TT::WGM, TT::WGN, 128, 2, false>(g, 0);
             if (rc) { printf("launch rc %d\n", rc); exit(1); }
@@ -96,13 +118,12 @@ int main(int argc, char** argv)
     const size_t n1 = (size_t)M1 * N, n2 = (size_t)N * 9 * C;
     std::vector<V> vars = {
         {"conv 256x192 store", 1, n1, conv(Tl<256, 192, 2, 4, 2>{}, EPI_STORE), f1},
+        {"conv 256x192 store sk", 1, n1, conv(Tl<256, 192, 2, 4, 2>{}, EPI_STORE, true), f1},
         {"conv 224x192 store", 1, n1, conv(Tl<224, 192, 2, 2, 4>{}, EPI_STORE), f1},
-        {"conv 160x256 store", 1, n1, conv(Tl<160, 256, 2, 2, 4>{}, EPI_STORE), f1},
         {"conv 256x192 stats", 1, n1, conv(Tl<256, 192, 2, 4, 2>{}, EPI_STATS), f1},
-        {"conv 224x192 stats", 1, n1, conv(Tl<224, 192, 2, 2, 4>{}, EPI_STATS), f1},
+        {"conv 256x192 stats sk", 1, n1, conv(Tl<256, 192, 2, 4, 2>{}, EPI_STATS, true), f1},
         {"wgrad 256x192 s2", 2, n2, wgrad(Tl<256, 192, 2, 4, 2>{}, 2), f2},
-        {"wgrad 256x192 s1", 2, n2, wgrad(Tl<256, 192, 2, 4, 2>{}, 1), f2},
-        {"wgrad 256x192 s4", 2, n2, wgrad(Tl<256, 192, 2, 4, 2>{}, 4), f2},
+        {"wgrad 256x192 sk", 2, n2, wgrad(Tl<256, 192, 2, 4, 2>{}, 0), f2},
     };
     std::vector<float> ref, got;
     std::vector<_Float16> refh, goth;
