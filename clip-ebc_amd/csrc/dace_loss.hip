@@ -517,6 +517,34 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
     // so up to NT / 2 points take one pass instead of two
     constexpr int LPT = LPB == 16 ? 2 : 4;
     const int q = t & (LPT - 1);
+    // K v's loop-invariant operands in registers when every point fits one pass (n <= NT / LPT, the bench's crops):
+    // the point's 12-cell Ex chunk, its Ey values and v offsets of the lane's window rows -- per iteration the lane
+    // then reads only the v rows (r03 re-read the window word, the Ex chunk and Ey through LDS every iteration,
+    // one more dependent LDS round trip).  Same products in the same order: the bits do not change.
+    constexpr int KW = G < 12 ? G : 12, MR = (9 + LPT - 1) / LPT;   // window rows <= 9
+    const bool kv_regs = n <= NT / LPT;
+    float4 kv_e[KW / 4];
+    float kv_ey[MR];
+    int kv_off[MR], kv_rows = 0;
+    if (kv_regs && t / LPT < n) {
+        const int i = t / LPT;
+        const int w = win[i];
+        const int ylo = w & 255, ylen = (w >> 8) & 255, xlo = (w >> 16) & 255, xlen = (w >> 24) & 255;
+        if (xlen) {
+            const int x4 = min(xlo & ~3, G - KW);
+            const float* exr = Ex + i * CW + x4 - row_base<G, CW>(xlo, xlen);
+            const float* eyr = Ey + i * CW + ylo - row_base<G, CW>(ylo, ylen);
+#pragma unroll
+            for (int c = 0; c < KW / 4; ++c) kv_e[c] = *reinterpret_cast<const float4*>(exr + 4 * c);
+#pragma unroll
+            for (int k = 0; k < MR; ++k) {
+                const int r = q + k * LPT;
+                kv_ey[k] = r < ylen ? eyr[r] : 0.f;
+                kv_off[k] = (ylo + (r < ylen ? r : 0)) * G + x4;
+                kv_rows += r < ylen;
+            }
+        }
+    }
     int to_eval = eval_freq;
     while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
         int* fl = flag + (it & 1);
@@ -543,7 +571,32 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
         __syncthreads();
         if (t == 0) flag[(it + 1) & 1] = 0;
         // phase B: u = a / (K v + eps)
-        for (int i0 = 0; i0 < n; i0 += NT / LPT) {
+        if (kv_regs) {
+            const int i = t / LPT;
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < MR; ++k) {
+                if (k < kv_rows) {
+                    const float* vr = vn + kv_off[k];
+                    float sum = 0.f;
+#pragma unroll
+                    for (int c = 0; c < KW / 4; ++c) {
+                        const float4 a4 = *reinterpret_cast<const float4*>(vr + 4 * c);
+                        sum = fmaf(kv_e[c].x, a4.x, sum); sum = fmaf(kv_e[c].y, a4.y, sum);
+                        sum = fmaf(kv_e[c].z, a4.z, sum); sum = fmaf(kv_e[c].w, a4.w, sum);
+                    }
+                    acc = fmaf(kv_ey[k], sum, acc);
+                }
+            }
+            if constexpr (LPT == 4) acc = sum4_dpp(acc);
+            else acc += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, acc), 0xB1, 0xF, 0xF, true));
+            if (i < n && q == 0) {
+                const float val = a / (acc + M_EPS);
+                un[i] = val;
+                if (!isfinite(val)) *fl = 1;
+            }
+        }
+        for (int i0 = 0; i0 < (kv_regs ? 0 : n); i0 += NT / LPT) {
             const int i = i0 + t / LPT;
             float acc = 0.f;
             if (i < n) {

@@ -924,7 +924,7 @@ namespace {
 // output has too few tiles to fill the 256 CUs.
 struct TileCfg { int id, bm, bn; };
 constexpr TileCfg CFGS[] = {{1, 128, 128}, {2, 128, 64}, {3, 256, 192}, {4, 192, 192}, {5, 128, 96}, {7, 256, 256},
-                            {13, 128, 96}, {15, 128, 96}, {16, 128, 96}};
+                            {13, 128, 96}, {15, 128, 96}, {16, 128, 96}, {17, 224, 192}};
 const TileCfg* find_cfg(int id) {
     for (const TileCfg& c : CFGS) if (c.id == id) return &c;
     return nullptr;
@@ -1045,6 +1045,9 @@ int launch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st)
         if (cfg == 3) return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2, 128, MODE>(g, st);
         if (cfg == 7) return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2, 128, MODE>(g, st);
         if (cfg == 13) return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, MODE>(g, st);
+        if constexpr (MODE == 1) {
+            if (cfg == 17) return launch_gemm<E, TO, EPI, 224, 192, 2, 2, 4, 128, MODE>(g, st);
+        }
     }
     return EBC_E_UNSUPPORTED;
 }
@@ -1121,6 +1124,11 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
     if (mode == 1 && N % 256 == 0 && N % 192 != 0 && ntiles(M, N, 256, 256) >= 256) return 7;
     // r01: 160x256 tiles (237 instead of 196 tiles at M = 16*784, N = 768) measured only 2-3 % faster on the
     // forward convs (their 80x64 wave tiles lose per-CU throughput), not kept
+    // fewer 256x192 tiles than CUs (16 crops: 196): 224x192 tiles fill more of them (224), 131.8-136.6 vs 138.1-138.6 us
+    // (store epilogue, interleaved, profiles/r04d_conv_lab_16crops.txt); more tiles than CUs keep 256x192 (stream-K)
+    if (mode == 1 && N % 192 == 0 && ntiles(M, N, 256, 192) >= 160 && ntiles(M, N, 256, 192) < NUM_CU &&
+        ntiles(M, N, 224, 192) <= NUM_CU)
+        return 17;
     if (N % 192 == 0 && (mode == 2 || ntiles(M, N, 256, 192) >= 160)) return 3;
     return N % 96 == 0 ? 13 : 2;
 }

@@ -164,7 +164,7 @@ def test_conv3x3_abi_matches_torch():
 
 
 @pytest.mark.parametrize("B,H,C,N,plan", [
-    (16, 28, 256, 768, (256, 192, 1)),       # 196 tiles of 256x192 < 256 CUs: one plain launch (measured no gain)
+    (16, 28, 256, 768, (224, 192, 1)),       # 196 tiles of 256x192 < 256 CUs: 224 tiles of 224x192, one launch
     (8, 56, 512, 2048, (256, 256, -64)),     # 784 tiles of 256x256: 768 whole, then 16 tiles on 64 workgroups
     (8, 56, 256, 1024, (256, 256, -256)),    # 392 tiles: 256 whole, then 136 tiles on 256 workgroups
     (8, 56, 128, 1024, (256, 256, 1))])      # 18 k-tiles a tile: too short to share, plain launch

@@ -149,8 +149,9 @@ def test_decoder_at_bench_batch(dname, B):
     dt = DT[dname]
     C, h = 768, 14
     M = B * 784
-    # 196 tiles of 256x192: one plain launch; 32 crops, 392: 256 whole tiles, then 136 shared by 256 (stream-K)
-    assert conv_cfg(dt, 1, M, C, 9 * C) == (3, (256, 192, 1 if B == 16 else -256))
+    # 16 crops: 224 tiles of 224x192 (196 of 256x192 would leave 60 CUs idle); 32 crops: 392 of 256x192, 256 whole
+    # tiles then 136 shared by 256 workgroups (stream-K)
+    assert conv_cfg(dt, 1, M, C, 9 * C) == ((17, (224, 192, 1)) if B == 16 else (3, (256, 192, -256)))
     geo = (ctypes.c_long * 6)()                         # {Hp, Wp, HWp, Kq, Q, Qs}: K of the wgrad = Kq
     _lib.check(_lib.lib().ebc_dec_geometry(_lib.dtype_code(dt), B, 2 * h, 2 * h, C, geo), "ebc_dec_geometry")
     assert geo[3] == B * 784                            # the interior pixels only (r03: B * 14 * 64 padded)
