@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-crops", type=int, default=16, help="crops per CPU-baseline step (BASELINE.md: 16)")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps after 3 warm-up (BASELINE.md)")
     ap.add_argument("--no-probe", action="store_true", help="skip the instrumented in-step kernel timing pass")
+    ap.add_argument("--no-ln-fold", action="store_true",
+                    help="A/B: ln_1 / ln_2 as LayerNorm launches instead of folded into the QKV / c_fc products")
     ap.add_argument("--optim", default="hip", choices=["hip", "torch"],
                     help="optimizer step: ebc_amd.optim Adam + GradScaler (HIP, 2 launches) or torch's fused Adam + "
                          "torch.amp.GradScaler (same arithmetic; for A/B)")
@@ -242,6 +244,7 @@ def setup(args, rank, world, local, device):
     else:
         model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
                           vpt_drop=0.0, deep_vpt=True, weights_seed=0).to(device)
+        model.vit_ln_fold = not getattr(args, "no_ln_fold", False)
     model.train()
     if world > 1:
         from ebc_amd.distributed import wrap_ddp       # SyncBatchNorm + DDP, as trainer.py:147

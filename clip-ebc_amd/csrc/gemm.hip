@@ -25,7 +25,9 @@ using namespace ebc;
 
 namespace {
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4, EPI_ADD_RELU_GRAD = 5 };
+constexpr int LN_PMAX = ebc::GEMM_LN_PMAX;   // EPI_LN: at most 16 row partials (N / BN * 2 of the producing product)
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4, EPI_ADD_RELU_GRAD = 5, EPI_LN = 6,
+       EPI_LN_GELU = 7 };
 
 struct GemmArgs {
     const void* A; const void* B; void* C;
@@ -61,6 +63,25 @@ struct GemmArgs {
     // partial slots (2 per workgroup) in `part`, the per-tile arrival counters in `cnt`
     long sk_total = 0;
     int sk_nk = 0, sk_grid = 0;
+    // LayerNorm folded into the encoder GEMMs (vit.hip, 16-bit; r04): a RESID product may also write a compute-dtype
+    // copy of its output rows (xh) and per-row partial sums / sums of squares of them (rpart [M][N / BN * WGN][2], one
+    // pair per tile column and wave column); an EPI_LN / EPI_LN_GELU product normalises its rows from such partials
+    // (lnp, lnparts) in the epilogue: out = rstd * (acc - mean * lnw[col]) + bias[col], its B operand being the weight
+    // pre-scaled by gamma (W' = W diag(gamma)), lnw = W'.1 and bias = b + W beta; tile column 0 writes the row mean /
+    // rstd (ln_mean, ln_rstd) for the LayerNorm backward
+    void* xh = nullptr;
+    float* rpart = nullptr;
+    const float* lnp = nullptr;
+    const float* lnw = nullptr;
+    float* ln_mean = nullptr;
+    float* ln_rstd = nullptr;
+    int lnparts = 0;
+    // ... and such a RESID product may replace the deep-VPT prompt rows of its output (rows r with 1 <= r % vrep_L <=
+    // vrep_nv) by the next block's prompts: row r of crop b = r / vrep_L becomes vrep[b * vrep_bs + (r % vrep_L - 1) *
+    // N ...] (copy, row partials and all), the next block's input exactly as the deep-VPT insertion defines it
+    const float* vrep = nullptr;
+    long vrep_bs = 0;
+    int vrep_L = 1, vrep_nv = 0;
     // algorithmic K the probe records (0: K).  MODE 2's K loop runs over padded image rows; its algorithmic K is
     // the interior pixel count B*H*W (bench.py counts 2*M*N*kalg FLOP)
     int kalg = 0;
@@ -271,7 +292,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         // MODE 2: each piece's 16-B chunk index inside its row (the lane's K offset in the tile / (16 / EB)), 4 bits a
         // piece in one register (r04: a K offset per piece made the 256x192 weight-gradient tiles spill)
         unsigned cpk = 0;
-    #pragma unroll
+#pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const bool tail = TAIL && i >= NLDF;
             // full pieces: rows (wave*NLDF + i)*RPI + lane/CPR; tail piece j: 4-B lanes, rows
@@ -342,12 +363,12 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 }
             };
             char* dst = smem + buf * STAGE;
-    #pragma unroll
+#pragma unroll
             for (int i = 0; i < NLDF; ++i) {
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(i),
                                                  EBC_LDS(dst + (lw * NLDF + i) * 1024), 16, 0, 0);
             }
-    #pragma unroll
+#pragma unroll
             for (int j = 0; j < NT4; ++j) {
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)piece(NLDF + j),
                                                  EBC_LDS(dst + NLDF * NLDR * 1024 + (lw * NT4 + j) * 256), 4, 0, 0);
@@ -357,11 +378,25 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         auto stage = [&](int buf, int kt) {
             if constexpr (NLW == 0) stage_pieces(buf, kt);
         };
+        constexpr bool LNP = MODE == 0 && (EPI == EPI_LN || EPI == EPI_LN_GELU);
+        auto stage_stats = [&]() {
+            // 1 KiB a wave-instruction (16 B a lane), the last rows' bytes clamped inside the buffer (rows >= M).
+            // (Issued with the k-tiles 1..4 of the 2-stage rings instead, r04 measured no difference.)
+            const char* base = reinterpret_cast<const char*>(g.lnp);
+            const unsigned rowb = (unsigned)g.lnparts * 8u, total = (unsigned)g.M * rowb, b0 = (unsigned)m0 * rowb;
+            const int chunks = (int)((BM * rowb) >> 10);
+            for (int c = lw; c < chunks; c += NLDR) {
+                unsigned o = b0 + (unsigned)c * 1024u + (unsigned)lane * 16u;
+                o = o + 16u <= total ? o : total - 16u;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + o),
+                                                 EBC_LDS(smem + S * STAGE + c * 1024), 16, 0, 0);
+            }
+        };
 
         f32x4 acc[TM][TN];
-    #pragma unroll
+#pragma unroll
         for (int a = 0; a < TM; ++a)
-    #pragma unroll
+#pragma unroll
             for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
         // S-deep LDS ring + register double-buffered fragments.  Tiles kt+1 .. kt+S-1 are in flight
@@ -381,9 +416,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         // 16-B half); the wave's row block, the sub-tile and the stage buffer are immediates.
         const int xs = swz_row<ROWB>(fr);
         int loff[KS][EB == 2 ? 1 : 2];
-    #pragma unroll
+#pragma unroll
         for (int kk = 0; kk < KS; ++kk)
-    #pragma unroll
+#pragma unroll
             for (int c = 0; c < (EB == 2 ? 1 : 2); ++c) {
                 const int ch = ((kk * 32 + 8 * fg) * EB >> 4) + c;
                 loff[kk][c] = fr * ROWB + ((ch ^ xs) << 4);
@@ -392,7 +427,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         const char* bbase = smem + (BM + wn * WN) * ROWB;
         auto load_frags = [&](auto bufc, int kk, typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
             constexpr int buf = decltype(bufc)::value;
-    #pragma unroll
+#pragma unroll
             for (int a = 0; a < TM; ++a) {
                 const char* rp = abase + buf * STAGE + a * 16 * ROWB;
                 if constexpr (EB == 2) {
@@ -403,7 +438,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     af[a] = typename E::Frag{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
                 }
             }
-    #pragma unroll
+#pragma unroll
             for (int b = 0; b < TN; ++b) {
                 const char* rp = bbase + buf * STAGE + b * 16 * ROWB;
                 if constexpr (EB == 2) {
@@ -436,6 +471,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             if (wave >= NW) {
                 // loader wave: the compute waves' ring schedule (one barrier per k-tile, the buffer of tile kt
                 // refilled with tile kt + S right after the barrier that retires its reads), then exit
+                if constexpr (LNP) stage_stats();
                 for (int s = 0; s < S - 1; ++s)
                     if (s < nk) stage_pieces(s, s);
                 wait_tile(0, std::true_type{});
@@ -454,6 +490,20 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         // loaded before the ring fills, so its latency hides under the first tiles' instead of being paid after the
         // K loop (vmcnt retires loads in order: issued any later, a counted ring wait would block on it mid-loop)
         constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && NW + NLW <= 8;
+        // RESID: the residual row r, or (vrep) the prompt row replacing output row r -- an address select, no branch
+        constexpr bool VREP = MODE == 0 && EPI == EPI_RESID && EB == 2;    // (gemm_nt_ln: 16-bit only)
+        auto vrep_row = [&](int r) -> bool {
+            if (!VREP || !g.vrep) return false;
+            const int j = r % g.vrep_L - 1;
+            return (unsigned)j < (unsigned)g.vrep_nv;
+        };
+        auto resid_row = [&](int r) -> const float* {
+            if constexpr (!VREP) return g.resid + (size_t)r * g.N;
+            const int b = r / g.vrep_L, j = r - b * g.vrep_L - 1;         // (vrep_L >= 1 when vrep is set)
+            const float* pv = g.vrep + b * g.vrep_bs + (size_t)j * g.N;
+            const float* pr = g.resid + (size_t)r * g.N;
+            return g.vrep && (unsigned)j < (unsigned)g.vrep_nv ? pv : pr;
+        };
         typedef float rp8_t __attribute__((ext_vector_type(8)));
         typedef float rp4_t __attribute__((ext_vector_type(4)));
         rp8_t rp8[PREF ? TM : 1][TN / 2 > 0 ? TN / 2 : 1];
@@ -465,24 +515,30 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         if constexpr (PREF_G) {
             const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
             const T* aux = reinterpret_cast<const T*>(g.aux);
-    #pragma unroll
+#pragma unroll
             for (int a = 0; a < TM / 2; ++a) {
                 const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
-    #pragma unroll
+#pragma unroll
                 for (int q = 0; q < TN / 2; ++q) gp8[a][q] = *reinterpret_cast<const gp8_t*>(aux + ro + q * 32 + fq * 8);
             }
         }
         if constexpr (PREF) {
             const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
-    #pragma unroll
+#pragma unroll
             for (int a = 0; a < TM; ++a) {
-                const size_t ro = (size_t)min(mb + a * 16, g.M - 1) * g.N + nb;
-    #pragma unroll
-                for (int q = 0; q < TN / 2; ++q) rp8[a][q] = *reinterpret_cast<const rp8_t*>(g.resid + ro + q * 32 + fq * 8);
-                if constexpr (TN & 1) rp4[a] = *reinterpret_cast<const rp4_t*>(g.resid + ro + (TN / 2) * 32 + fq * 4);
+                const float* src = resid_row(min(mb + a * 16, g.M - 1)) + nb;
+#pragma unroll
+                for (int q = 0; q < TN / 2; ++q) rp8[a][q] = *reinterpret_cast<const rp8_t*>(src + q * 32 + fq * 8);
+                if constexpr (TN & 1) rp4[a] = *reinterpret_cast<const rp4_t*>(src + (TN / 2) * 32 + fq * 4);
             }
         }
-    #pragma unroll
+        // EPI_LN: the workgroup's rows' partials (gemm_nt_ln; lnparts float2 a row, rows m0 .. m0 + BM contiguous) are
+        // copied by LDS-DMA into LDS past the ring ahead of tile 0 -- counted loads of the issuing waves, older than
+        // every ring piece, so landed once tile 0 has -- and reduced in the epilogue.  (Register loads of them, 2-4 per
+        // row and lane, duplicated across the wave columns, cost the products 2.5-4 us a launch in the start-up burst:
+        // profiles/r04t_lnfold_lab_*.txt.)
+        if constexpr (LNP && NLW == 0) stage_stats();
+#pragma unroll
         for (int s = 0; s < S - 1; ++s)
             if (s < nk) stage(s, s);
         sync_tile(0, std::true_type{});
@@ -490,9 +546,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
         load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
         auto mma_all = [&](typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
-    #pragma unroll
+#pragma unroll
             for (int a = 0; a < TM; ++a)
-    #pragma unroll
+#pragma unroll
                 for (int b = 0; b < TN; ++b) acc[a][b] = mma(bf[b], af[a], acc[a][b]);   // swapped: C^T tile
         };
         // step body: prefetch the fragments of the step after (kt, kk) into (an, bn), then MMA (ac, bc);
@@ -558,11 +614,11 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             // the whole GPU instead of re-read through one CU
             float* P = g.part + (size_t)split * g.M * g.N;
             const int mb = m0 + wm * WM + fr;
-    #pragma unroll
+#pragma unroll
             for (int a = 0; a < TM; ++a) {
                 const int m = mb + a * 16;
                 if (m >= g.M) break;
-    #pragma unroll
+#pragma unroll
                 for (int b = 0; b < TN; ++b) {
                     int n;
                     if constexpr (MODE == 0) {
@@ -607,9 +663,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 reinterpret_cast<f32x4*>(g.part) + (skr ? 0 : (size_t)ltile * g.splits * PT), 0, 0x7fffffff, 0x00020000);
             typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    #pragma unroll
+#pragma unroll
             for (int a = 0; a < TM; ++a)
-    #pragma unroll
+#pragma unroll
                 for (int b = 0; b < TN; ++b)
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rs,
                                                            ((mine * PT) + ((wave * TM + a) * TN + b) * 64 + lane) * 16, 0, 16);
@@ -629,15 +685,15 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     static_for<0, TM / PCH>([&](auto cc) {
                         constexpr int a0 = decltype(cc)::value * PCH;
                         f32x4 t[PCH][TN];
-    #pragma unroll
+#pragma unroll
                         for (int a = 0; a < PCH; ++a)
-    #pragma unroll
+#pragma unroll
                             for (int b = 0; b < TN; ++b)
                                 t[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                     rs, ((sp * PT) + ((wave * TM + a0 + a) * TN + b) * 64 + lane) * 16, 0, 16));
-    #pragma unroll
+#pragma unroll
                         for (int a = 0; a < PCH; ++a)
-    #pragma unroll
+#pragma unroll
                             for (int b = 0; b < TN; ++b) acc[a0 + a][b] += t[a][b];
                         // keep the next chunk's loads below this one's adds (a sched_barrier alone did not: the DAG
                         // scheduler hoisted all 32 loads of a 256x256 partial)
@@ -648,9 +704,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 if (np == 2) {
                     add_partial(slot(1 - mypiece));
                 } else {
-    #pragma unroll
+#pragma unroll
                     for (int a = 0; a < TM; ++a)
-    #pragma unroll
+#pragma unroll
                         for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
                     for (int p = 0; p < np; ++p) add_partial(slot(p));
                 }
@@ -664,7 +720,8 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 // group q, 8 (a sub-tile pair) or 4 (odd last sub-tile) consecutive columns.  Operands
                 // (resid / aux) are loaded for the whole wave tile first (row-clamped, unconditional), then each
                 // group is finished and stored; rows >= M are never stored.
-                static_assert(EPI <= EPI_GELU_BWD, "MODE 0 epilogues");
+                static_assert(EPI <= EPI_GELU_BWD || EPI == EPI_LN || EPI == EPI_LN_GELU, "MODE 0 epilogues");
+                constexpr bool LN = EPI == EPI_LN || EPI == EPI_LN_GELU, GE = EPI == EPI_GELU || EPI == EPI_LN_GELU;
                 TO* C = reinterpret_cast<TO*>(g.C);
                 constexpr int NP = TN / 2, ODD = TN & 1;
                 constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID;
@@ -680,7 +737,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 constexpr int PH = (NW >= 8 && PREG > 24 && TM % 2 == 0) ? 2 : 1;
                 constexpr int TMP = TM / PH;
                 float bv[NP > 0 ? NP : 1][8], bo[4];
-        #pragma unroll
+#pragma unroll
                 for (int q = 0; q < NP; ++q) {
                     if (g.bias) load8f<float>(g.bias + nb + q * 32 + fg * 8, bv[q]);
                     else for (int i = 0; i < 8; ++i) bv[q][i] = 0.f;
@@ -689,9 +746,56 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     if (g.bias) load4<float>(g.bias + nb + NP * 32 + fg * 4, bo);
                     else for (int i = 0; i < 4; ++i) bo[i] = 0.f;
                 }
-                auto finish = [&](float* v, int w, const float* bias, const auto& pre, size_t off) {
+                // the row's 4 lanes (lanes fr + 16 fg) meet by lane swaps (same bits on all four)
+                auto pair_sum = [](float x) {
+                    const auto a1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+                    x = __uint_as_float(a1[0]) + __uint_as_float(a1[1]);
+                    const auto a2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+                    return __uint_as_float(a2[0]) + __uint_as_float(a2[1]);
+                };
+                // LN: W'.1 of the lane's columns; each row's rstd and rstd * mean from its partials in LDS (stage_stats):
+                // the row's 4 lanes read 16-B pairs q = fg, fg + 4 and meet by lane swaps, so every tile of a row sums in
+                // the same order (same bits).  var = E[x^2] - mean^2 in f32 (|mean| / std <= 0.15 on the encoder's rows;
+                // tests/test_gpu_model.py holds the error to the LayerNorm-launch path's)
+                float lw[LN && NP > 0 ? NP : 1][8], lwo[4];
+                float rsv[LN ? TM : 1], rsmuv[LN ? TM : 1];
+                if constexpr (LN) {
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) load8f<float>(g.lnw + nb + q * 32 + fg * 8, lw[q]);
+                    if constexpr (ODD) load4<float>(g.lnw + nb + NP * 32 + fg * 4, lwo);
+                    const char* st = smem + S * STAGE;
+#pragma unroll
+                    for (int a = 0; a < TM; ++a) {
+                        const float4* pp = reinterpret_cast<const float4*>(st + (wm * WM + a * 16 + fr) * g.lnparts * 8);
+                        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                        for (int j = 0; j < LN_PMAX / 8; ++j) {
+                            const int q = fg + 4 * j;
+                            const bool in = 2 * q < g.lnparts;
+                            const float4 t = pp[in ? q : 0];
+                            s1 += in ? t.x + t.z : 0.f;
+                            s2 += in ? t.y + t.w : 0.f;
+                        }
+                        s1 = pair_sum(s1);
+                        s2 = pair_sum(s2);
+                        const float mean = s1 / (float)g.K;
+                        const float var = fmaxf(s2 / (float)g.K - mean * mean, 0.f);
+                        rsv[a] = 1.0f / sqrtf(var + 1e-5f);
+                        rsmuv[a] = rsv[a] * mean;
+                        const int m = mb + a * 16;
+                        if (g.ln_mean && tn == 0 && wn == 0 && fg == 0 && m < g.M) { g.ln_mean[m] = mean; g.ln_rstd[m] = rsv[a]; }
+                    }
+                }
+                float rs = 1.f, rsmu = 0.f;
+                bool vr = false;                     // RESID: the row is a replaced prompt row
+                // RESID with rpart: the lane's partial sum / sum of squares of its row's output values
+                float rsum = 0.f, rsq = 0.f;
+                auto finish = [&](float* v, int w, const float* bias, const float* lwv, const auto& pre, size_t off) {
+                    if constexpr (LN) {
+                        for (int i = 0; i < w; ++i) v[i] = fmaf(rs, v[i], -rsmu * lwv[i]);
+                    }
                     for (int i = 0; i < w; ++i) v[i] += bias[i];
-                    if constexpr (EPI == EPI_GELU) {
+                    if constexpr (GE) {
                         if (g.aux) {
                             if (w == 8) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
                             else store4<T>(reinterpret_cast<T*>(g.aux) + off, v);
@@ -700,7 +804,12 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     } else if constexpr (EPI == EPI_GELU_BWD) {
                         for (int i = 0; i < w; ++i) v[i] *= quick_gelu_grad((float)pre[i]);
                     } else if constexpr (EPI == EPI_RESID) {
-                        for (int i = 0; i < w; ++i) v[i] += pre[i];
+                        for (int i = 0; i < w; ++i) v[i] = vr ? (float)pre[i] : v[i] + pre[i];
+                        if (VREP && g.rpart) {
+                            for (int i = 0; i < w; ++i) { rsum += v[i]; rsq = fmaf(v[i], v[i], rsq); }
+                            if (w == 8) store8<T>(reinterpret_cast<T*>(g.xh) + off, v);
+                            else store4<T>(reinterpret_cast<T*>(g.xh) + off, v);
+                        }
                     }
                     if (w == 8) store8<TO>(C + off, v);
                     else store4<TO>(C + off, v);
@@ -710,44 +819,62 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     pa8 p8[PRE ? TMP : 1][NP > 0 ? NP : 1];
                     pa4 p4[PRE && ODD ? TMP : 1];
                     if constexpr (PREF) {
-        #pragma unroll
+#pragma unroll
                         for (int a = 0; a < TMP; ++a) {
-        #pragma unroll
+#pragma unroll
                             for (int q = 0; q < NP; ++q) p8[a][q] = rp8[a0 + a][q];
                             if constexpr (ODD) p4[a] = rp4[a0 + a];
                         }
                     } else if constexpr (PREF_G && a0 == 0 && TMP == TM / 2) {
-        #pragma unroll
+#pragma unroll
                         for (int a = 0; a < TMP; ++a)
-        #pragma unroll
+#pragma unroll
                             for (int q = 0; q < NP; ++q) p8[a][q] = __builtin_convertvector(gp8[a][q], pa8);
                     } else if constexpr (PRE) {
                         const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
-        #pragma unroll
+#pragma unroll
                         for (int a = 0; a < TMP; ++a) {
-                            const size_t ro = (size_t)min(mb + (a0 + a) * 16, g.M - 1) * g.N + nb;
-        #pragma unroll
-                            for (int q = 0; q < NP; ++q) p8[a][q] = *reinterpret_cast<const pa8*>(src + ro + q * 32 + fg * 8);
-                            if constexpr (ODD) p4[a] = *reinterpret_cast<const pa4*>(src + ro + NP * 32 + fg * 4);
+                            const int r = min(mb + (a0 + a) * 16, g.M - 1);
+                            const PA* sr = src + (size_t)r * g.N + nb;
+                            if constexpr (EPI == EPI_RESID) sr = reinterpret_cast<const PA*>(resid_row(r)) + nb;
+#pragma unroll
+                            for (int q = 0; q < NP; ++q) p8[a][q] = *reinterpret_cast<const pa8*>(sr + q * 32 + fg * 8);
+                            if constexpr (ODD) p4[a] = *reinterpret_cast<const pa4*>(sr + NP * 32 + fg * 4);
                         }
                     }
-        #pragma unroll
+#pragma unroll
                     for (int a = 0; a < TMP; ++a) {
                         const int m = mb + (a0 + a) * 16;
-                        if (m >= g.M) break;                 // rows ascend with a
+                        if (m >= g.M) break;                 // rows ascend with a (the 4 lanes of a row together)
                         const size_t ro = (size_t)m * g.N + nb;
-        #pragma unroll
+                        if constexpr (LN) {
+                            rs = rsv[a0 + a];
+                            rsmu = rsmuv[a0 + a];
+                        }
+                        if constexpr (EPI == EPI_RESID) vr = vrep_row(m);
+#pragma unroll
                         for (int q = 0; q < NP; ++q) {
                             float v[8] = {acc[a0 + a][2 * q][0], acc[a0 + a][2 * q][1], acc[a0 + a][2 * q][2], acc[a0 + a][2 * q][3],
                                           acc[a0 + a][2 * q + 1][0], acc[a0 + a][2 * q + 1][1], acc[a0 + a][2 * q + 1][2],
                                           acc[a0 + a][2 * q + 1][3]};
-                            if constexpr (PRE) finish(v, 8, bv[q], p8[a][q], ro + q * 32 + fg * 8);
-                            else finish(v, 8, bv[q], 0, ro + q * 32 + fg * 8);
+                            const float* lwq = LN ? lw[q] : nullptr;
+                            if constexpr (PRE) finish(v, 8, bv[q], lwq, p8[a][q], ro + q * 32 + fg * 8);
+                            else finish(v, 8, bv[q], lwq, 0, ro + q * 32 + fg * 8);
                         }
                         if constexpr (ODD) {
                             float v[4] = {acc[a0 + a][TN - 1][0], acc[a0 + a][TN - 1][1], acc[a0 + a][TN - 1][2], acc[a0 + a][TN - 1][3]};
-                            if constexpr (PRE) finish(v, 4, bo, p4[a], ro + NP * 32 + fg * 4);
-                            else finish(v, 4, bo, 0, ro + NP * 32 + fg * 4);
+                            if constexpr (PRE) finish(v, 4, bo, lwo, p4[a], ro + NP * 32 + fg * 4);
+                            else finish(v, 4, bo, lwo, 0, ro + NP * 32 + fg * 4);
+                        }
+                        if constexpr (EPI == EPI_RESID) {
+                            if (VREP && g.rpart) {
+                                // one partial per (tile column, wave column)
+                                const float ts = pair_sum(rsum), tq = pair_sum(rsq);
+                                if (fg == 0)
+                                    reinterpret_cast<float2*>(g.rpart)[(size_t)m * (g.N / BN * WGN) + tn * WGN + wn] = float2{ts, tq};
+                                rsum = 0.f;
+                                rsq = 0.f;
+                            }
                         }
                         if constexpr (NW >= 8) __builtin_amdgcn_sched_barrier(0);
                     }
@@ -775,13 +902,13 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             typedef PA pa8 __attribute__((ext_vector_type(8)));
             typedef T t8v __attribute__((ext_vector_type(8)));
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        #pragma unroll 1
+#pragma unroll 1
             for (int pass = 0; pass < BM / EPR; ++pass) {
                 pa8 pre[PRE ? NIT : 1];
                 t8v pre2[EPI == EPI_ADD_RELU_GRAD ? NIT : 1];
                 if constexpr (PRE) {
                     const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
-        #pragma unroll
+#pragma unroll
                     for (int k = 0; k < NIT; ++k) {
                         const int c = min(tid + k * NT, NCH - 1), r = c / C8, col = (c % C8) * 8;
                         const int m = min(m0 + pass * EPR + r, g.M - 1);
@@ -793,15 +920,15 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 }
                 __syncthreads();
                 if ((wm * WM) / EPR == pass) {
-        #pragma unroll
+#pragma unroll
                     for (int a = 0; a < TM; ++a)
-        #pragma unroll
+#pragma unroll
                         for (int b = 0; b < TN; ++b)
                             *reinterpret_cast<float4*>(ep + (wm * WM - pass * EPR + a * 16 + fr) * EPL + wn * WN + b * 16 + 4 * fg) =
                                 make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
                 }
                 __syncthreads();
-        #pragma unroll
+#pragma unroll
                 for (int k = 0; k < NIT; ++k) {
                     const int c = tid + k * NT;
                     if (NCH % NT != 0 && c >= NCH) break;
@@ -821,17 +948,17 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     }
                     if constexpr (EPI == EPI_GELU) {
                         if (g.aux) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
-        #pragma unroll
+#pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] = quick_gelu(v[i]);
                     } else if constexpr (EPI == EPI_GELU_BWD) {
-        #pragma unroll
+#pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] *= quick_gelu_grad((float)pre[k][i]);
                     } else if constexpr (EPI == EPI_ADD_RELU_GRAD) {
                         // decoder: conv1's input gradient plus the residual branch's (models/utils.py:300-302)
-        #pragma unroll
+#pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] += (float)pre2[k][i] > 0.f ? (float)pre[k][i] : 0.f;
                     } else if constexpr (EPI == EPI_RESID) {
-        #pragma unroll
+#pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] += pre[k][i];
                     }
                     store8<TO>(C + off, v);
@@ -842,7 +969,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     const int rows = min(EPR, g.M - (m0 + pass * EPR));
                     if (tid < BN) {
                         const float bc = g.bias ? g.bias[n0 + tid] : 0.f;
-        #pragma unroll 4
+#pragma unroll 4
                         for (int r = 0; r < rows; ++r) {
                             const float x = ep[r * EPL + tid] + bc;
                             col_s += x;
@@ -874,7 +1001,10 @@ template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, i
 int launch_gemm_k(const GemmArgs& g, hipStream_t st)
 {
     constexpr int WM = BM / WGM;
-    constexpr int LDS = gemm_lds_bytes<BM, BN, S, ROWB, WM>();
+    // EPI_LN: the workgroup's row partials (BM rows of at most LN_PMAX float2) past the ring
+    constexpr bool LNE = MODE == 0 && (EPI == EPI_LN || EPI == EPI_LN_GELU);
+    constexpr int RING = S * (BM + BN) * ROWB, LNB = LNE ? RING + BM * LN_PMAX * 8 : 0;
+    constexpr int LDS = gemm_lds_bytes<BM, BN, S, ROWB, WM>() > LNB ? gemm_lds_bytes<BM, BN, S, ROWB, WM>() : LNB;
     static_assert(LDS <= 160 * 1024, "LDS");
     constexpr int BK = ROWB / E::BYTES;
     if (!ensure_lds<gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL, NLW>>(LDS, st)) return EBC_E_LAUNCH;
@@ -1031,6 +1161,12 @@ int dispatch_epi(const GemmArgs& g, int epi, int out_f32, void* ws, size_t wsb, 
         case EPI_RESID: return out_f32 ? dispatch_tile<E, float, EPI_RESID>(g, ws, wsb, st)
                                        : dispatch_tile<E, typename E::T, EPI_RESID>(g, ws, wsb, st);
         case EPI_GELU_BWD: return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_GELU_BWD>(g, ws, wsb, st);
+        case EPI_LN:
+            if constexpr (E::BYTES == 2) return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_LN>(g, ws, wsb, st);
+            return EBC_E_UNSUPPORTED;
+        case EPI_LN_GELU:
+            if constexpr (E::BYTES == 2) return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_LN_GELU>(g, ws, wsb, st);
+            return EBC_E_UNSUPPORTED;
     }
     return EBC_E_ARG;
 }
@@ -1319,6 +1455,44 @@ int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void*
     g.a_rpg = a_rpg; g.a_gstride = a_gstride; g.a_goff = a_goff;
     switch (dtype) {
         case EBC_F32: return dispatch_epi<EF32>(g, epi, 0, nullptr, 0, st);   // element type is already f32
+        case EBC_F16: return dispatch_epi<EF16>(g, epi, out_f32, ws, ws_bytes, st);
+        case EBC_BF16: return dispatch_epi<EBF16>(g, epi, out_f32, ws, ws_bytes, st);
+    }
+    return EBC_E_ARG;
+}
+
+int gemm_rowstat_parts(int dtype, int M, int N, int K)
+{
+    const TileCfg* c = find_cfg(select_cfg(dtype != EBC_F32, M, N, K));
+    return N / c->bn * 2;                       // every MODE 0 tile configuration has 2 wave columns
+}
+
+int gemm_nt_ln(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
+               const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws, size_t ws_bytes,
+               const GemmLn& ln)
+{
+    const int bk = dtype == EBC_F32 ? 32 : 64;
+    if (dtype == EBC_F32 || M <= 0 || N <= 0 || K <= 0 || K % bk != 0 || N % 64 != 0 || !A || !B || !C) return EBC_E_ARG;
+    GemmArgs g{A, B, C, bias, resid, aux, M, N, K};
+    if (epi == EPI_RESID) {
+        if (!resid || !out_f32 || !ln.xh || !ln.rpart) return EBC_E_ARG;
+        g.xh = ln.xh;
+        g.rpart = ln.rpart;
+        if (ln.vrep) {
+            if (ln.vrep_L <= 0 || ln.vrep_nv <= 0 || ln.vrep_nv >= ln.vrep_L || ln.vrep_bs < 0) return EBC_E_ARG;
+            g.vrep = ln.vrep; g.vrep_bs = ln.vrep_bs; g.vrep_L = ln.vrep_L; g.vrep_nv = ln.vrep_nv;
+        }
+    } else if (epi == EPI_LN || epi == EPI_LN_GELU) {
+        if (out_f32 || !ln.lnp || !ln.lnw || ln.lnparts <= 0 || ln.lnparts > LN_PMAX || ln.lnparts % 2 || !ln.mean != !ln.rstd) return EBC_E_ARG;
+        g.lnp = ln.lnp;
+        g.lnparts = ln.lnparts;
+        g.lnw = ln.lnw;
+        g.ln_mean = ln.mean;
+        g.ln_rstd = ln.rstd;
+    } else {
+        return EBC_E_ARG;
+    }
+    switch (dtype) {
         case EBC_F16: return dispatch_epi<EF16>(g, epi, out_f32, ws, ws_bytes, st);
         case EBC_BF16: return dispatch_epi<EBF16>(g, epi, out_f32, ws, ws_bytes, st);
     }

@@ -20,6 +20,28 @@ void probe_stop(int idx, hipStream_t st);
 int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
             const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws = nullptr,
             size_t ws_bytes = 0, int a_rpg = 0, int a_gstride = 0, int a_goff = 0);
+// LayerNorm folded into the encoder GEMMs (gemm.hip GemmArgs, vit.hip; 16-bit): a RESID product that also writes a
+// compute-dtype copy of its rows (xh) and per-row partial sums / sums of squares (rpart [M][parts][2],
+// parts = gemm_rowstat_parts), and GEMM_EPI_LN / GEMM_EPI_LN_GELU products normalising their A rows from them
+struct GemmLn {
+    void* xh = nullptr;
+    float* rpart = nullptr;
+    const float* lnp = nullptr;
+    int lnparts = 0;
+    const float* lnw = nullptr;
+    float* mean = nullptr;
+    float* rstd = nullptr;
+    // RESID: replace the deep-VPT prompt rows (1 <= r % vrep_L <= vrep_nv) of the output by vrep (crop stride vrep_bs)
+    const float* vrep = nullptr;
+    long vrep_bs = 0;
+    int vrep_L = 0, vrep_nv = 0;
+};
+constexpr int GEMM_EPI_LN = 6, GEMM_EPI_LN_GELU = 7;
+constexpr int GEMM_LN_PMAX = 16;   // most row partials an EPI_LN product reads (gemm_rowstat_parts of its producer)
+int gemm_nt_ln(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
+               const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws, size_t ws_bytes,
+               const GemmLn& ln);
+int gemm_rowstat_parts(int dtype, int M, int N, int K);
 // split-K workspace the heuristic wants for this shape (0: no split); zero-filled counter block first
 size_t gemm_workspace_bytes(int dtype, int M, int N, int K);
 // implicit-GEMM 3x3 convolution geometry (gemm.hip MODE 1 / MODE 2)

@@ -50,6 +50,8 @@ struct Layout {
     float *dXa, *dXb, *delta;
     float* vpt_rows;                // [layers][B][NV][768] per-crop prompt gradients (summed over crops at the end)
     void *dXt, *dH, *dA, *dO, *dQKV;
+    float* rpart;                   // LayerNorm folding: [M][parts][2] row partials (sum, sum of squares) of X1 / X_l+1
+    int parts_out, parts_proj;      //   written by the out-proj / c_proj residual products (gemm_rowstat_parts)
     void* gws;                      // split-K GEMM workspace (leading counter block zeroed per call)
     size_t gws_bytes;
     size_t bytes;
@@ -103,6 +105,14 @@ Layout carve(void* ws, int B, int L, int G, int layers, int dtype, int training)
         lay.dXa = lay.dXb = lay.delta = nullptr;
         lay.dXt = lay.dH = lay.dA = lay.dO = lay.dQKV = nullptr;
     }
+    if (dtype != EBC_F32) {
+        lay.parts_out = ebc::gemm_rowstat_parts(dtype, (int)M, WIDTH, WIDTH);
+        lay.parts_proj = ebc::gemm_rowstat_parts(dtype, (int)M, WIDTH, MLP);
+        lay.rpart = c.take<float>(M * std::max(lay.parts_out, lay.parts_proj) * 2 * 4);
+    } else {
+        lay.parts_out = lay.parts_proj = 0;
+        lay.rpart = nullptr;
+    }
     // the largest split-K workspace any of the encoder GEMMs asks for
     size_t g = ebc::gemm_workspace_bytes(dtype, B * G, WIDTH, WIDTH);          // patch embedding
     const int Mi = (int)M;
@@ -155,13 +165,24 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
     // The frozen weights were last read a step ago (HBM).  Block l's attention reads onto the die (Infinity Cache) the
     // weights of the GEMMs after it -- its out-proj, c_fc and c_proj, and block l+1's QKV -- while it computes
     // (attention.hip touch_issue): those GEMMs then start with their B operand on-die.  16-bit path only.
+    // LayerNorm folding (16-bit, every layer carrying the folded weights): ln_2 of every block and ln_1 of blocks
+    // 1.. run inside the QKV / c_fc products' epilogues.  The residual products before them (out-proj; c_proj of the
+    // block below) also write a compute-dtype copy of their output rows into H and per-row partial sums / sums of
+    // squares into rpart; the product reads H as its A operand, the folded weight W diag(gamma) as B, and finishes
+    // rstd * (acc - mean * W'.1) + b + W beta (gemm.hip EPI_LN), writing the row's mean / rstd for the backward.
+    // Saves the two LayerNorm launches' read of X and write of H per block; the backward is unchanged.
+    bool fold = dtype != EBC_F32 && lay.rpart && std::max(lay.parts_out, lay.parts_proj) <= ebc::GEMM_LN_PMAX;
+    for (int l = 0; l < layers && fold; ++l) {
+        const EbcVitLayer& p = w->layer[l];
+        fold = p.w_qkv_ln && p.b_qkv_ln && p.s_qkv_ln && p.w_fc_ln && p.b_fc_ln && p.s_fc_ln;
+    }
     auto touch_fwd = [&](int l) {
         ebc::TouchList t{};
         const EbcVitLayer& p = w->layer[l];
         t.add(p.w_out, (size_t)WIDTH * WIDTH * es);
-        t.add(p.w_fc, (size_t)MLP * WIDTH * es);
+        t.add(fold ? p.w_fc_ln : p.w_fc, (size_t)MLP * WIDTH * es);
         t.add(p.w_proj, (size_t)WIDTH * MLP * es);
-        if (l + 1 < layers) t.add(w->layer[l + 1].w_qkv, (size_t)QKVW * WIDTH * es);
+        if (l + 1 < layers) t.add(fold ? w->layer[l + 1].w_qkv_ln : w->layer[l + 1].w_qkv, (size_t)QKVW * WIDTH * es);
         return t;
     };
     auto block = [&](int l, int b0, int nb, hipStream_t sx) -> int {
@@ -182,20 +203,55 @@ extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B
                         const float* resid, void* aux, int n, int k) {
             return ebc::gemm_nt(dtype, epi, out_f32, Am, Bm, C, bias, resid, aux, m, n, k, sx, lay.gws, lay.gws_bytes);
         };
-        // x = x + out_proj(attn(ln_1(x))); deep VPT: ln_1 reads the prompt rows from vpt_l and writes them into X
-        if (l > 0 && NV > 0 && vpt[l])
-            EBC_TRY(ebc::layernorm_fwd_vpt(dtype, X, vpt[l] + (size_t)b0 * vpt_bstride, vpt_bstride, L, NV, p.ln1_g,
-                                           p.ln1_b, Hn, s.m1 + r0, s.r1 + r0, m, WIDTH, sx));
-        else
-            EBC_TRY(ebc::layernorm_fwd(dtype, X, 0, 0, 0, p.ln1_g, p.ln1_b, Hn, nullptr, s.m1 + r0, s.r1 + r0, m, WIDTH, sx));
-        EBC_TRY(gemm(EBC_EPI_STORE, 0, Hn, p.w_qkv, QKV, p.b_qkv, nullptr, nullptr, QKVW, WIDTH));
+        auto gemm_ln = [&](int epi, int out_f32, const void* Am, const void* Bm, void* C, const float* bias,
+                           const float* resid, void* aux, int n, int k, const ebc::GemmLn& ln) {
+            return ebc::gemm_nt_ln(dtype, epi, out_f32, Am, Bm, C, bias, resid, aux, m, n, k, sx, lay.gws, lay.gws_bytes, ln);
+        };
+        // x = x + out_proj(attn(ln_1(x))); deep VPT: the prompt rows come from vpt_l (written into X)
+        const bool vrows = l > 0 && NV > 0 && vpt[l];
+        if (fold && l > 0) {
+            // X_l's rows (the prompt rows already replaced by vpt_l), their H copy and partials came from block
+            // l-1's c_proj
+            ebc::GemmLn ln;
+            ln.lnp = lay.rpart + r0 * lay.parts_proj * 2; ln.lnparts = lay.parts_proj; ln.lnw = p.s_qkv_ln;
+            ln.mean = s.m1 + r0; ln.rstd = s.r1 + r0;
+            EBC_TRY(gemm_ln(ebc::GEMM_EPI_LN, 0, Hn, p.w_qkv_ln, QKV, p.b_qkv_ln, nullptr, nullptr, QKVW, WIDTH, ln));
+        } else {
+            if (vrows)
+                EBC_TRY(ebc::layernorm_fwd_vpt(dtype, X, vpt[l] + (size_t)b0 * vpt_bstride, vpt_bstride, L, NV, p.ln1_g,
+                                               p.ln1_b, Hn, s.m1 + r0, s.r1 + r0, m, WIDTH, sx));
+            else
+                EBC_TRY(ebc::layernorm_fwd(dtype, X, 0, 0, 0, p.ln1_g, p.ln1_b, Hn, nullptr, s.m1 + r0, s.r1 + r0, m, WIDTH, sx));
+            EBC_TRY(gemm(EBC_EPI_STORE, 0, Hn, p.w_qkv, QKV, p.b_qkv, nullptr, nullptr, QKVW, WIDTH));
+        }
         const ebc::TouchList tl = touch_fwd(l);
         EBC_TRY(ebc::attention_fwd(dtype, QKV, O, lse, nb, L, HEADS, sx, &tl));
-        EBC_TRY(gemm(EBC_EPI_RESID, 1, O, p.w_out, X1, p.b_out, X, nullptr, WIDTH, WIDTH));
         // x = x + c_proj(QuickGELU(c_fc(ln_2(x))))
-        EBC_TRY(ebc::layernorm_fwd(dtype, X1, 0, 0, 0, p.ln2_g, p.ln2_b, Hn, nullptr, s.m2 + r0, s.r2 + r0, m, WIDTH, sx));
-        EBC_TRY(gemm(EBC_EPI_GELU, 0, Hn, p.w_fc, Gm, p.b_fc, nullptr, A, MLP, WIDTH));
-        EBC_TRY(gemm(EBC_EPI_RESID, 1, Gm, p.w_proj, Xn, p.b_proj, X1, nullptr, WIDTH, MLP));
+        if (fold) {
+            ebc::GemmLn res;
+            res.xh = Hn; res.rpart = lay.rpart + r0 * lay.parts_out * 2;
+            EBC_TRY(gemm_ln(EBC_EPI_RESID, 1, O, p.w_out, X1, p.b_out, X, nullptr, WIDTH, WIDTH, res));
+            ebc::GemmLn ln;
+            ln.lnp = res.rpart; ln.lnparts = lay.parts_out; ln.lnw = p.s_fc_ln;
+            ln.mean = s.m2 + r0; ln.rstd = s.r2 + r0;
+            EBC_TRY(gemm_ln(ebc::GEMM_EPI_LN_GELU, 0, Hn, p.w_fc_ln, Gm, p.b_fc_ln, nullptr, A, MLP, WIDTH, ln));
+        } else {
+            EBC_TRY(gemm(EBC_EPI_RESID, 1, O, p.w_out, X1, p.b_out, X, nullptr, WIDTH, WIDTH));
+            EBC_TRY(ebc::layernorm_fwd(dtype, X1, 0, 0, 0, p.ln2_g, p.ln2_b, Hn, nullptr, s.m2 + r0, s.r2 + r0, m, WIDTH, sx));
+            EBC_TRY(gemm(EBC_EPI_GELU, 0, Hn, p.w_fc, Gm, p.b_fc, nullptr, A, MLP, WIDTH));
+        }
+        if (fold && l + 1 < layers) {
+            ebc::GemmLn res;
+            res.xh = Hn; res.rpart = lay.rpart + r0 * lay.parts_proj * 2;
+            if (NV > 0 && vpt[l + 1]) {
+                // deep VPT: block l+1's prompt rows written in place of this product's (copy, H rows and partials)
+                res.vrep = vpt[l + 1] + (size_t)b0 * vpt_bstride; res.vrep_bs = vpt_bstride;
+                res.vrep_L = L; res.vrep_nv = NV;
+            }
+            EBC_TRY(gemm_ln(EBC_EPI_RESID, 1, Gm, p.w_proj, Xn, p.b_proj, X1, nullptr, WIDTH, MLP, res));
+        } else {
+            EBC_TRY(gemm(EBC_EPI_RESID, 1, Gm, p.w_proj, Xn, p.b_proj, X1, nullptr, WIDTH, MLP));
+        }
         return EBC_OK;
     };
     // (the two crop halves on two streams, overlapping one half's GEMM store phases with the other's main loops,

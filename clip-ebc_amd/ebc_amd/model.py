@@ -108,7 +108,8 @@ _VP = ctypes.c_void_p
 
 class EbcVitLayer(ctypes.Structure):
     _fields_ = [(n, _VP) for n in ("w_qkv", "b_qkv", "w_out", "b_out", "w_fc", "b_fc", "w_proj", "b_proj",
-                                   "ln1_g", "ln1_b", "ln2_g", "ln2_b", "wt_qkv", "wt_out", "wt_fc", "wt_proj")]
+                                   "ln1_g", "ln1_b", "ln2_g", "ln2_b", "wt_qkv", "wt_out", "wt_fc", "wt_proj",
+                                   "w_qkv_ln", "b_qkv_ln", "s_qkv_ln", "w_fc_ln", "b_fc_ln", "s_fc_ln")]
 
 
 class EbcVitWeights(ctypes.Structure):
@@ -124,7 +125,8 @@ def _p(t: Tensor) -> int:
 class _EncoderCache:
     """Frozen encoder weights in the compute dtype (+ transposes for the dX backward), kept resident."""
 
-    def __init__(self, enc: VisionTransformer, num_vpt: int, dtype: torch.dtype, device: torch.device):
+    def __init__(self, enc: VisionTransformer, num_vpt: int, dtype: torch.dtype, device: torch.device,
+                 ln_fold: bool = True):
         self.dtype, self.device = dtype, device
         keep: List[Tensor] = []
 
@@ -134,6 +136,8 @@ class _EncoderCache:
             return r
 
         layers = len(enc.transformer.resblocks)
+        # ln_fold False keeps ln_1 / ln_2 as LayerNorm launches (tests, A/B measurements); f32 never folds
+        fold_ln = dtype != torch.float32 and ln_fold
         self.layer_arr = (EbcVitLayer * layers)()
         for i, blk in enumerate(enc.transformer.resblocks):
             L = self.layer_arr[i]
@@ -148,6 +152,18 @@ class _EncoderCache:
             L.b_proj = _p(cvt(blk.mlp.c_proj.bias, torch.float32))
             L.ln1_g, L.ln1_b = _p(cvt(blk.ln_1.weight, torch.float32)), _p(cvt(blk.ln_1.bias, torch.float32))
             L.ln2_g, L.ln2_b = _p(cvt(blk.ln_2.weight, torch.float32)), _p(cvt(blk.ln_2.bias, torch.float32))
+            if fold_ln:
+                # ln_1 / ln_2 folded into the QKV / c_fc products (vit.hip): W' = W diag(gamma) in the compute dtype,
+                # its row sums from the rounded W' (so the epilogue's mean term cancels what the MFMA sums), and
+                # b' = b + W beta, in f64
+                for pre, w, bias, ln in (("qkv", blk.attn.in_proj_weight, blk.attn.in_proj_bias, blk.ln_1),
+                                         ("fc", blk.mlp.c_fc.weight, blk.mlp.c_fc.bias, blk.ln_2)):
+                    w64 = w.detach().to(device, torch.float64)
+                    wf = cvt(w64 * ln.weight.detach().to(device, torch.float64)[None, :])
+                    setattr(L, f"w_{pre}_ln", _p(wf))
+                    setattr(L, f"s_{pre}_ln", _p(cvt(wf.double().sum(1), torch.float32)))
+                    setattr(L, f"b_{pre}_ln", _p(cvt(bias.detach().to(device, torch.float64)
+                                                     + w64 @ ln.bias.detach().to(device, torch.float64), torch.float32)))
         self.w_patch = cvt(enc.conv1.weight.reshape(WIDTH, -1))
         self.cls = cvt(enc.class_embedding, torch.float32)
         self.ln = [cvt(t, torch.float32) for t in (enc.ln_pre.weight, enc.ln_pre.bias, enc.ln_post.weight, enc.ln_post.bias)]
@@ -590,6 +606,7 @@ class CLIP_EBC(nn.Module):
         self._cache: Optional[_EncoderCache] = None
         self._cache_key = None
         self.vit_bwd_flags = 0          # ebc_vit_backward flags (include/ebc_hip.h), for parity tests only
+        self.vit_ln_fold = True         # 16-bit: ln_1 / ln_2 folded into the QKV / c_fc products (vit.hip)
 
     # -- weights ---------------------------------------------------------------------------
     def _load_synthetic(self, seed, vit_layers, text_layers, input_size):
@@ -622,9 +639,9 @@ class CLIP_EBC(nn.Module):
 
     def _encoder_cache(self, dtype: torch.dtype, device: torch.device) -> _EncoderCache:
         ver = sum(p._version for p in self.image_encoder.parameters())
-        key = (dtype, device, ver)
+        key = (dtype, device, ver, bool(self.vit_ln_fold))
         if self._cache is None or self._cache_key != key:
-            self._cache = _EncoderCache(self.image_encoder, self.num_vpt, dtype, device)
+            self._cache = _EncoderCache(self.image_encoder, self.num_vpt, dtype, device, bool(self.vit_ln_fold))
             self._cache_key = key
         self._cache.bwd_flags = int(self.vit_bwd_flags)
         return self._cache

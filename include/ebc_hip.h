@@ -136,6 +136,12 @@ typedef struct {
     const void* w_proj; const float* b_proj;   /* mlp.c_proj [768,3072] */
     const float* ln1_g; const float* ln1_b; const float* ln2_g; const float* ln2_b;
     const void* wt_qkv; const void* wt_out; const void* wt_fc; const void* wt_proj;   /* transposes */
+    /* optional (16-bit; all null: ln_1 / ln_2 run as LayerNorm launches): ln_1 / ln_2 folded into the QKV / c_fc
+     * products -- the weight rows pre-scaled by gamma (W' = W diag(gamma), [out, 768] in dtype), the folded bias
+     * b + W beta and the row sums W'.1 (f32 [out]); the layer's input rows are then normalised in those products'
+     * epilogues from row statistics the previous residual product writes */
+    const void* w_qkv_ln; const float* b_qkv_ln; const float* s_qkv_ln;
+    const void* w_fc_ln;  const float* b_fc_ln;  const float* s_fc_ln;
 } EbcVitLayer;
 
 typedef struct {

@@ -1,9 +1,9 @@
 // LayerNorm-fold lab (experiment harness, not product code): the encoder's c_fc (+QuickGELU) and QKV products at
 // 16 crops (M = 16 x 229) timed as plain products (EPI_GELU / EPI_STORE) and as LayerNorm-folded ones (EPI_LN_GELU /
 // EPI_LN reading 16 row partials per row), on a normalised-like A and on a raw-residual-like A, interleaved rounds in
-// one process.  Separates the epilogue / prologue cost of the fold from operand effects.  The fold was measured and
-// not kept: the kernels it times exist only with tools/lab/ln_fold.diff applied to the tree (that
-// diff also carries the LNX_* isolation switches used for profiles/r04t_lnfold_lab_*.txt).
+// one process.  Separates the cost of the fold from operand effects (profiles/r04t_lnfold_lab_*.txt were taken on the
+// first form, register loads of the partials, with isolation switches since removed; the tree's form stages them
+// into LDS by DMA).
 //   build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 -DEBC_GEMM_LAB \
 //          tools/lab/lnfold_lab.hip -o tools/lab/bin/lnfold_lab
 //   run:   lnfold_lab [rounds] [reps]
