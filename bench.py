@@ -366,7 +366,7 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
         kind = _lib.PROBE_KINDS.get(r.kind, str(r.kind))
         if kind == "gemm":
             mode = {0: "", 1: " conv3x3", 2: " conv3x3-wgrad"}[r.mode]
-            epi = {0: "store", 1: "gelu", 2: "resid", 3: "gelu_bwd", 4: "bn_stats", 5: "add_relu_grad"}.get(r.epi, r.epi)
+            epi = {0: "store", 1: "gelu", 2: "resid", 3: "gelu_bwd", 4: "bn_stats", 5: "add_relu_grad", 6: "ln", 7: "ln_gelu"}.get(r.epi, r.epi)
             key = f"gemm_nt {r.bm}x{r.bn}{mode} {epi} M={r.m} N={r.n} K={r.k}"
             flops = 2.0 * r.m * r.n * r.k
         elif kind == "dace_loss":
