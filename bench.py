@@ -413,7 +413,7 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
     return out, dace_us
 
 
-PMC_FILE = os.path.join("profiles", "r04m_pmc_step.json")
+PMC_FILE = os.path.join("profiles", "r04y_pmc_step.json")
 
 
 def committed_pmc(kernel_key):
