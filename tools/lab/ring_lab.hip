@@ -77,18 +77,23 @@ int main(int argc, char** argv)
     hipLaunchKernelGGL(fill_f32, dim3(64), dim3(256), 0, 0, bias, (size_t)3072, 4u);
     CK(hipDeviceSynchronize());
 
-    struct V { std::string name; int N, epi; Fn fn; };
+    struct V { std::string name; int N, epi; Fn fn; int gm = 0; };
     std::vector<V> vs = {
         {"c_fc 256x192 R128 S2", 3072, EPI_GELU, var<EPI_GELU, 256, 192, 2, 4, 2, 128>()},
         {"c_fc 256x192 R64 S4", 3072, EPI_GELU, var<EPI_GELU, 256, 192, 4, 4, 2, 64>()},
+        {"c_fc 256x256 R128 S2", 3072, EPI_GELU, var<EPI_GELU, 256, 256, 2, 4, 2, 128>()},
         {"QKV 192x192 R128 S2", 2304, EPI_STORE, var<EPI_STORE, 192, 192, 2, 4, 2, 128>()},
         {"QKV 192x192 R128 S3", 2304, EPI_STORE, var<EPI_STORE, 192, 192, 3, 4, 2, 128>()},
         {"QKV 192x192 R64 S4", 2304, EPI_STORE, var<EPI_STORE, 192, 192, 4, 4, 2, 64>()},
+        {"QKV 256x192 R128 S2", 2304, EPI_STORE, var<EPI_STORE, 256, 192, 2, 4, 2, 128>()},
     };
+    // tile order as gemm.hip's group_rows for each variant's tile
+    const int tiles_bm[] = {256, 256, 256, 192, 192, 192, 256}, tiles_bn[] = {192, 192, 256, 192, 192, 192, 192};
+    for (size_t i = 0; i < vs.size(); ++i) vs[i].gm = lab_group_rows(M, vs[i].N, tiles_bm[i], tiles_bn[i]);
     auto args = [&](const V& v, _Float16* C) {
         GemmArgs g{A, W, C, bias, nullptr, v.epi == EPI_GELU ? Aux : nullptr, M, v.N, K};
         g.kslice = K;
-        g.group_m = lab_group_rows(M, v.N, v.N == 3072 ? 256 : 192, 192);
+        g.group_m = v.gm;
         return g;
     };
     // bitwise check against the first variant of the same N
