@@ -327,10 +327,15 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
     from ebc_amd import _lib
     L = _lib.lib()
     cap = 8192
+    stats_by_step = {}                            # the loss's per-crop stats of every step run here (device tensors)
+
+    def run(i):
+        step(i)
+        stats_by_step[i] = getattr(getattr(step, "loss_fn", None), "last_stats", None)
     torch.cuda.synchronize()
     _lib.check(L.ebc_probe_begin(cap), "ebc_probe_begin")
     for i in range(n):
-        step(first + i)
+        run(first + i)
     torch.cuda.synchronize()
     recs = (_lib.EbcProbeRecord * cap)()
     got = L.ebc_probe_end(recs, cap)
@@ -340,7 +345,7 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
     # the same launch sequence again, traced: per family, the k-th kernel of the family is the k-th probe record
     if trace:
         try:
-            trace = trace_steps(step, first + n, n)
+            trace = trace_steps(run, first + n, n)
         except Exception as exc:                   # profiler unavailable: event durations only
             print(f"bench.py: kernel trace unavailable ({exc}); in-step durations from HIP events", file=sys.stderr)
             trace = None
@@ -371,7 +376,10 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
             flops = 2.0 * r.m * r.n * r.k
         elif kind == "dace_loss":
             key, flops = f"dace_loss_kernel B={r.m} g={r.k}", 0.0
-            dace.append(traced[ri] * 1e-3 if traced[ri] is not None else r.ms)
+            # one loss launch a step: the k-th record is probe step first + k, its traced twin step first + n + k
+            k = len(dace)
+            dace.append((traced[ri] * 1e-3 if traced[ri] is not None else r.ms,
+                         stats_by_step.get(first + n + k if traced[ri] is not None else first + k)))
         elif kind.startswith("attn"):
             # algorithmic products (FA2 counting): forward 2 (QK^T, PV), the whole backward 5 (S, dP, dV, dK, dQ) = 2.5x;
             # the 16-bit backward is ONE launch (probe epi 1, recorded as attn_bwd_dq), the f32 one a dQ (S, dP, dQ)
@@ -409,8 +417,9 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
             rec["flop_per_launch"] = c["flop_per_launch"]
         out.append(rec)
     out.sort(key=lambda r: -r["per_step_us"])
-    dace_us = sum(dace) / len(dace) * 1e3 if dace else None
-    return out, dace_us
+    # the loss launch: (duration us, Sinkhorn iterations of THAT step's launch, max over its crops) per step
+    dace_steps = [(ms * 1e3, int(st[:, 5].max()) if st is not None else None) for ms, st in dace]
+    return out, dace_steps
 
 
 PMC_FILE = os.path.join("profiles", "r04y_pmc_step.json")
@@ -439,7 +448,7 @@ def committed_pmc(kernel_key):
     return None
 
 
-def sinkhorn_entry(dace_us, iters, cells):
+def sinkhorn_entry(dace_steps, cells):
     """The loss launch as what bounds it: one 1024-thread workgroup per crop (B of the 256 CUs), 100 dependent
     Sinkhorn iterations of two LDS-resident products, a division pass and two barriers each -- latency, not bytes.
     HBM bytes per launch from the committed PMC pass over the bench command (same key as the kernels list)."""
@@ -452,9 +461,13 @@ def sinkhorn_entry(dace_us, iters, cells):
                     pmc = r
     except (OSError, ValueError):
         pass
+    dace_us = sum(d for d, _ in dace_steps) / len(dace_steps)
+    its = [i for _, i in dace_steps]
+    per_it = [d / i for d, i in dace_steps if i]
+    # us_per_iteration pairs each launch's duration with its own step's iteration count
     out = {"bound": "latency", "kernel": f"dace_loss_kernel<{g}> (fused DACE + DMCount + Sinkhorn)",
-           "avg_us": round(dace_us, 1), "iterations": iters,
-           "us_per_iteration": round(dace_us / iters, 3) if iters else None}
+           "avg_us": round(dace_us, 1), "launches": len(dace_steps), "iterations": its,
+           "us_per_iteration": round(sum(per_it) / len(per_it), 3) if per_it and len(per_it) == len(its) else None}
     if pmc and "traffic_bytes_per_launch" in pmc:
         b = pmc["traffic_bytes_per_launch"]
         out.update({"hbm_bytes_per_launch": round(b), "hbm_gbs": round(b / (pmc["avg_duration_us"] * 1e-6) / 1e9, 1),
@@ -628,11 +641,9 @@ def main():
     kernels, sink = None, None
     if not args.no_probe:
         first = args.warmup + args.steps
-        kernels, dace_us = probe_steps(step, first, 3, device, trace=not args.no_trace,
-                                       classes_out=args.classes_out if rank == 0 else None)
-        st_l = getattr(step.loss_fn, "last_stats", None)
-        iters = int(st_l[:, 5].max()) if st_l is not None else None      # Sinkhorn iterations run (max over crops)
-        sink = sinkhorn_entry(dace_us, iters, (args.size // 8) ** 2) if dace_us else None
+        kernels, dace_steps = probe_steps(step, first, 3, device, trace=not args.no_trace,
+                                          classes_out=args.classes_out if rank == 0 else None)
+        sink = sinkhorn_entry(dace_steps, (args.size // 8) ** 2) if dace_steps else None
     if rank == 0:
         peak = MFMA_PEAK_TF[args.dtype]
         rn = args.model == "clip_resnet50"

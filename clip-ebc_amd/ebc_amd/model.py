@@ -367,6 +367,16 @@ def _bn_momentum(bn: nn.Module) -> float:
     return 1.0 / float(bn.num_batches_tracked.item())
 
 
+class DecoderMaskTap:
+    """Test hook on the decoder's two ReLU decisions (tests/test_gpu_ddp.py): while ``capture`` is a list, every
+    _DecoderFn forward appends (m1, m2, pre1, pre2): its masks (relu(bn1) > 0 as [P, N], the block output > 0 as
+    [B, H, W, N], bool) and the two pre-activations they were decided on (bn1(z1), bn2(z2) + x; f32, recomputed
+    here by torch); while ``replay`` is a non-empty list, every backward pops one entry and uses its masks in place
+    of its own (the backward kernels then take the given decisions).  Both None in normal use."""
+    capture: Optional[list] = None
+    replay: Optional[list] = None
+
+
 class _DecoderFn(torch.autograd.Function):
     """BasicBlock(768, 768) (models/utils.py:254-303) after the x`up` bilinear reduction adapt
     (models/clip/model.py:195-196), on libebc_hip.so: implicit-GEMM 3x3 convs, BatchNorm statistics in
@@ -444,6 +454,13 @@ class _DecoderFn(torch.autograd.Function):
         y = torch.empty(B, H, W, N, device=dev, dtype=cdtype)
         _lib.check(L.ebc_bn_add_relu(dt, _lib.ptr(z2), _lib.ptr(scale2), _lib.ptr(shift2), _lib.ptr(feat), up,
                                      _lib.ptr(y), B, H, W, N, st), "ebc_bn_add_relu")
+        if DecoderMaskTap.capture is not None:
+            Hp, Wp = geo[0], geo[1]
+            h1 = hpad.view(B, Hp, Wp, N)[:, 1:H + 1, 1:W + 1]
+            (z1, _, _, sc1, sh1), (z2, _, _, sc2, sh2) = (o[:5] for o in outs)
+            xu = xpad.view(B, Hp, Wp, C)[:, 1:H + 1, 1:W + 1].float().reshape(P, N)
+            DecoderMaskTap.capture.append(((h1 > 0).reshape(P, N), y > 0, z1.float() * sc1 + sh1,
+                                           (z2.float() * sc2 + sh2 + xu).view(B, H, W, N)))
         ctx.save_for_backward(xpad, hpad, y, wflip[0], g1, wflip[1], g2)
         from .resnet import flush_bn_counters
         flush_bn_counters()                        # both BatchNorms' num_batches_tracked in one launch
@@ -470,6 +487,11 @@ class _DecoderFn(torch.autograd.Function):
         grads = []
         dnext = gy                                    # gradient at the current BN output's ReLU
         mask = y                                      # ReLU mask source (None: recompute from z)
+        ymask, mask1 = y, None
+        if DecoderMaskTap.replay:
+            m1, m2 = DecoderMaskTap.replay.pop(0)[:2]
+            mask1 = m1.to(cdtype).reshape(P, N).contiguous()
+            mask = ymask = m2.to(cdtype).reshape(B, H, W, N).contiguous()
         for i in (1, 0):
             z, mean, rstd, scale, shift, count, pg, colsum = ctx.outs[i]
             gm = (g1, g2)[i]
@@ -516,11 +538,11 @@ class _DecoderFn(torch.autograd.Function):
             wf = (wf1, wf2)[i]                                                    # [C][3][3][N]
             dx = torch.empty(P, C, device=dev, dtype=cdtype)
             # conv1's data gradient also takes the residual branch's gradient (gy through the final ReLU)
-            add = (_lib.ptr(gy), _lib.ptr(y)) if i == 0 else (None, None)
+            add = (_lib.ptr(gy), _lib.ptr(ymask)) if i == 0 else (None, None)
             _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(dzpad), _lib.ptr(wf), _lib.ptr(dx), None, *add, _lib.ptr(ws),
                                          ws.numel(), B, H, W, N, C, st), "ebc_conv3x3_fwd(dgrad)")
             grads.append((dw, dg, db))
-            dnext, mask = dx, None
+            dnext, mask = dx, mask1
         dfeat = torch.empty(B, h, w, C, **f32)
         _lib.check(L.ebc_dec_upsample_bwd(dt, _lib.ptr(dnext), _lib.ptr(dfeat), B, h, w, C, up, st),
                    "ebc_dec_upsample_bwd")

@@ -245,7 +245,8 @@ class GradScaler:
     def state_dict(self):
         if not self._enabled:
             return {}
-        tr = float(self._buf[self._parity, 1]) if self._buf is not None else 0.0
+        # before the first step: the loaded (or initial) tracker, as torch returns _init_growth_tracker
+        tr = float(self._buf[self._parity, 1]) if self._buf is not None else float(self._init_tracker)
         return {"scale": self.get_scale(), "growth_factor": self._growth_factor, "backoff_factor": self._backoff_factor,
                 "growth_interval": self._growth_interval, "_growth_tracker": int(tr)}
 

@@ -48,7 +48,11 @@ def rank_main(rank: int, world: int, port: int, out_dir: str) -> None:
     b0 = sum(SPLIT[:rank])
     sl = slice(b0, b0 + SPLIT[rank])
     x = torch.from_numpy(img[sl]).to(dev)
+    from ebc_amd.model import DecoderMaskTap
+    DecoderMaskTap.capture = []                # this rank's decoder ReLU decisions (the parent replays them)
     logits, exp = model(x)
+    (m1, m2, _, _), = DecoderMaskTap.capture
+    DecoderMaskTap.capture = None
     loss, info = DACELoss(BINS, 8, count_loss="dmcount", input_size=224)(
         logits, exp, torch.from_numpy(dens[sl]).to(dev), [torch.from_numpy(p).to(dev) for p in pts[sl]])
     loss.backward()
@@ -60,6 +64,7 @@ def rank_main(rank: int, world: int, port: int, out_dir: str) -> None:
         if "running" in k or "num_batches" in k:
             res["buf:" + k] = b.detach().cpu()
     res.update({"info:" + k: v.detach().cpu() for k, v in info.items()})
+    res["mask1"], res["mask2"] = m1.cpu(), m2.cpu()
     torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

@@ -50,10 +50,33 @@ def test_ddp_syncbn_step_matches_single_process(tmp_path):
     # single process: one forward over all crops (BN batch statistics over all of them), the mean of the
     # ranks' losses
     from ebc_amd.losses import DACELoss
+    from ebc_amd.model import DecoderMaskTap
     dev = torch.device("cuda:0")
     m = W.build(dev)
     img, pts, dens = W.batch()
-    logits, exp = m(torch.from_numpy(img).to(dev))
+    DecoderMaskTap.capture = []
+    try:
+        logits, exp = m(torch.from_numpy(img).to(dev))
+        (m1, m2, pre1, pre2), = DecoderMaskTap.capture
+    finally:
+        DecoderMaskTap.capture = None
+    # The two decompositions sum the decoder's BatchNorm statistics over different row tiles (each rank's last conv
+    # tile is partial), so the f32 mean / rstd can differ in the last bit, and a ReLU pre-activation within that of
+    # zero takes the other decision.  Count those decisions: few, and each at a pre-activation within f32
+    # resolution of zero (values ~O(1)).  The single process's backward then replays the ranks' decisions
+    # (DecoderMaskTap.replay), so the gradients compare the arithmetic, not one pixel's coin flip (r04 had to loosen
+    # this bar 15x to 3e-3 for one such flip).
+    rm1 = torch.cat([r0["mask1"], r1["mask1"]]).to(dev)
+    rm2 = torch.cat([r0["mask2"], r1["mask2"]]).to(dev)
+    flips = []
+    for own, ranks, pre in ((m1, rm1, pre1), (m2, rm2, pre2)):
+        sel = own != ranks
+        flips.append(int(sel.sum()))
+        if flips[-1]:
+            assert float(pre[sel].abs().max()) < 1e-4, float(pre[sel].abs().max())
+    print("ReLU decisions that differ between the decompositions:", flips, "of", m1.numel(), "per mask")
+    assert sum(flips) <= 8, flips
+    DecoderMaskTap.replay = [(rm1, rm2)]
     fn = DACELoss(W.BINS, 8, count_loss="dmcount", input_size=224)
     total, infos, b0 = 0.0, [], 0
     for n in W.SPLIT:
@@ -62,14 +85,12 @@ def test_ddp_syncbn_step_matches_single_process(tmp_path):
         total = total + loss / len(W.SPLIT)
         infos.append(info)
         b0 += n
-    total.backward()
-    # Bar: rel-L2 3e-3.  The two decompositions sum the decoder's BatchNorm statistics over different row tiles (each
-    # rank's last conv tile is partial), so the f32 mean / rstd can differ in the last bit, and a ReLU pre-activation
-    # within that of zero then takes the other mask value: the gradient moves by O(gy) at one pixel and channel and
-    # carries into every parameter upstream.  r04: the attention forward's new summation order (packed f32 row sums)
-    # moved this test from 1.6e-6 to 1.1e-3 on bn1.bias; bisected by swapping that one source file between builds
-    # (tools/dbg/ddp_bisect.sh), and the attention itself is bitwise repeatable and batch-invariant per (crop, head)
-    # (tools/dbg/attn_inv.py), so the ranks and the single process see the same encoder outputs.
+    try:
+        total.backward()
+        assert not DecoderMaskTap.replay
+    finally:
+        DecoderMaskTap.replay = None
+    # Bar: rel-L2 2e-4 on every trainable parameter (the decisions matched; what is left is f32 summation order).
     # A wrong SyncBatchNorm exchange (count weighting, a missing all-reduce) is off by 1e-1 or more.
     bad, worst = [], (None, 0.0)
     for k, p in m.named_parameters():
@@ -79,7 +100,7 @@ def test_ddp_syncbn_step_matches_single_process(tmp_path):
         for rank, r in enumerate((r0, r1)):
             err = rel_l2(r[k].numpy(), g)
             worst = max(worst, (k, err), key=lambda e: e[1])
-            if err >= 3e-3:
+            if err >= 2e-4:
                 bad.append((k, rank, err))
     print("worst gradient rel-L2", worst)
     assert not bad, bad

@@ -90,6 +90,40 @@ def test_attention_fwd_bwd(dname, B, L):
         assert _rel(d3[:, i], r3[:, i]) < tol, i
 
 
+@pytest.mark.parametrize("dname", ["f32", "f16"])
+def test_attention_batch_invariance(dname):
+    """One crop's attention output / lse / gradient must not depend on the batch it is in: alone (the 16-wave
+    forward: 12 units <= 256 CUs) and as crop 21 of 22 (264 units: the 8-wave forward of 128-query workgroups,
+    attn_fwd_waves), and bitwise repeatable.  The DDP / SyncBN test compares ranks of 2 and 1 crops with one
+    process on 3, and the 32-crop ranks of the multi-GPU bench with 16-crop single-GPU runs."""
+    dt = DT[dname]
+    H, Lq, B = 12, 229, 22
+    Lb = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    qkv = (torch.randn(B * Lq, 3 * H * 64, device="cuda", generator=g) * 1.5).to(dt)
+    dout = torch.randn(B * Lq, H * 64, device="cuda", generator=g).to(dt)
+
+    def run(x, do, n):
+        out = torch.empty(n * Lq, H * 64, device="cuda", dtype=dt)
+        lse = torch.empty(n, H, Lq, device="cuda")
+        _lib.check(Lb.ebc_attention_fwd(_lib.dtype_code(dt), _lib.ptr(x), _lib.ptr(out), _lib.ptr(lse), n, Lq, H,
+                                        _lib.stream()), "fwd")
+        delta = torch.empty(n, H, Lq, device="cuda")
+        d = torch.empty_like(x)
+        _lib.check(Lb.ebc_attention_bwd(_lib.dtype_code(dt), _lib.ptr(x), _lib.ptr(do), _lib.ptr(out), _lib.ptr(lse),
+                                        _lib.ptr(delta), _lib.ptr(d), n, Lq, H, _lib.stream()), "bwd")
+        return out, lse, d
+    ob, lb, db = run(qkv, dout, B)
+    ob2, lb2, db2 = run(qkv, dout, B)
+    assert torch.equal(ob, ob2) and torch.equal(lb, lb2) and torch.equal(db, db2)
+    c = B - 1
+    sl = slice(c * Lq, (c + 1) * Lq)
+    o1, l1, d1 = run(qkv[sl].contiguous(), dout[sl].contiguous(), 1)
+    assert torch.equal(ob[sl], o1), float((ob[sl].float() - o1.float()).abs().max())
+    assert torch.equal(lb[c], l1[0])
+    assert torch.equal(db[sl], d1)
+
+
 @pytest.mark.parametrize("embed,NB", [(512, 5), (512, 16), (1024, 5), (1024, 12), (1024, 16)])
 @pytest.mark.parametrize("dname", ["f32", "f16", "bf16"])
 def test_head_bwd_dz_dtypes(dname, embed, NB):

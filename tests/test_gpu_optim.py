@@ -175,8 +175,11 @@ def test_grad_scaler_resume_before_first_step_keeps_tracker():
             opt, sc = eo.Adam([p], lr=1e-3), eo.GradScaler(growth_interval=4)
         else:
             opt, sc = torch.optim.Adam([p], lr=1e-3, fused=True), torch.amp.GradScaler("cuda", growth_interval=4)
-        sc.load_state_dict({"scale": 1024.0, "growth_factor": 2.0, "backoff_factor": 0.5, "growth_interval": 4,
-                            "_growth_tracker": 3})
+        loaded = {"scale": 1024.0, "growth_factor": 2.0, "backoff_factor": 0.5, "growth_interval": 4,
+                  "_growth_tracker": 3}
+        sc.load_state_dict(loaded)
+        # a checkpoint saved right after resuming (before any step) keeps what was loaded
+        assert sc.state_dict() == loaded, (kind, sc.state_dict())
         out = []
         for i in range(3):
             sc.scale(torch.ones((), device=dev))
