@@ -79,6 +79,36 @@ def vit_state(seed: int = 0, layers: int = 12, input_size: int = 224) -> Dict[st
     return sd
 
 
+def outlier_stats(sd: Dict[str, np.ndarray], seed: int = 0, n_channels: int = 6, dc: float = 3.0) -> Dict[str, np.ndarray]:
+    """A copy of a ViT state dict (vit_state / full_state) with residual-stream statistics closer to a pretrained
+    CLIP tower's than the benign init above: a handful of 'massive activation' channels (ln_pre gamma at 30..100x,
+    random sign, and every block's out-proj / c_proj bias pushing them further by 2..8 per block), a common offset
+    `dc` on every channel (ln_pre beta: the rows' mean, which the fold's one-pass variance E[x^2] - mean^2 must
+    survive) and the LayerNorm gammas spread log-uniformly over 0.1..10.  Rows then carry per-channel ranges of ~100x and a mean offset from
+    the outliers: the stress case of the folded LayerNorm (gemm.hip EPI_LN normalises f16 rows after the product;
+    VERDICT r04 item 6)."""
+    out = dict(sd)
+    g = _rng(seed, "outlier_stats")
+    ch = g.choice(WIDTH, n_channels, replace=False)
+    sign = np.where(g.random(n_channels) < 0.5, -1.0, 1.0).astype(np.float32)
+    p = "image_encoder."
+    w = out[p + "ln_pre.weight"].copy()
+    w[ch] = sign * g.uniform(30.0, 100.0, n_channels).astype(np.float32)
+    out[p + "ln_pre.weight"] = w
+    out[p + "ln_pre.bias"] = out[p + "ln_pre.bias"] + np.float32(dc)
+    i = 0
+    while f"{p}transformer.resblocks.{i}.ln_1.weight" in out:
+        q = f"{p}transformer.resblocks.{i}."
+        for ln in ("ln_1", "ln_2"):
+            out[q + ln + ".weight"] = np.exp(g.uniform(math.log(0.1), math.log(10.0), WIDTH)).astype(np.float32)
+        for b in ("attn.out_proj.bias", "mlp.c_proj.bias"):
+            v = out[q + b].copy()
+            v[ch] += sign * g.uniform(2.0, 8.0, n_channels).astype(np.float32)
+            out[q + b] = v
+        i += 1
+    return out
+
+
 def text_state(seed: int = 0, layers: int = 12, embed: int = EMBED) -> Dict[str, np.ndarray]:
     """Frozen CLIP text tower (`text_encoder.py:7-53`)."""
     sd: Dict[str, np.ndarray] = {}

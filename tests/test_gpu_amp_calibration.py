@@ -40,11 +40,14 @@ def _oracle(p_cpu, img, txt, dens, pts, device, amp, size=224):
     return out
 
 
-def _hip(img, txt, dens, pts, amp, size=224):
+def _hip(img, txt, dens, pts, amp, size=224, stats="benign"):
     from ebc_amd.losses import DACELoss
     from ebc_amd.model import get_model
     m = get_model("clip_vit_b_16", size, 8, BINS, ANCHORS_NWPU, prompt_type="word", text_features=txt,
                   weights_seed=0).cuda().train()
+    if stats == "outlier":
+        from test_gpu_model import load_outlier_stats
+        load_outlier_stats(m)
     with torch.autocast("cuda", dtype=amp):
         lg, ex = m(torch.from_numpy(img).cuda())
         loss, _ = DACELoss(BINS, 8, count_loss="dmcount", input_size=size)(
@@ -60,15 +63,21 @@ def _hip(img, txt, dens, pts, amp, size=224):
     return out
 
 
-@pytest.mark.parametrize("B,amp,size", [(16, torch.float16, 224), (32, torch.float16, 224), (16, torch.bfloat16, 224),
-                                        (4, torch.float16, 448)])
-def test_step_error_within_pytorch_amp_error(B, amp, size):
+@pytest.mark.parametrize("B,amp,size,stats", [(16, torch.float16, 224, "benign"), (32, torch.float16, 224, "benign"),
+                                              (16, torch.bfloat16, 224, "benign"), (4, torch.float16, 448, "benign"),
+                                              # massive-activation channels, a row offset, gammas over 0.1..10
+                                              # (synthetic.outlier_stats)
+                                              (16, torch.float16, 224, "outlier"), (16, torch.bfloat16, 224, "outlier")])
+def test_step_error_within_pytorch_amp_error(B, amp, size, stats):
     txt = torch.from_numpy(golden("f6_text.npz")["text_features_word"])
     img, pts, dens = syn.synthetic_crops(B, size, seed=900 + B + (size if size != 224 else 0))
-    p = ref.params_from_state(syn.full_state(0, layers=LAYERS, include_text=False, input_size=size))
+    sd = syn.full_state(0, layers=LAYERS, include_text=False, input_size=size)
+    if stats == "outlier":
+        sd = syn.outlier_stats(sd)
+    p = ref.params_from_state(sd)
     truth = _oracle(p, img, txt, dens, pts, torch.device("cpu"), None, size)
     torch_amp = _oracle(p, img, txt, dens, pts, torch.device("cuda"), amp, size)
-    hip = _hip(img, txt, dens, pts, amp, size)
+    hip = _hip(img, txt, dens, pts, amp, size, stats)
     worst, bad = 0.0, []
     for k in truth:
         e_amp, e_hip = rel_l2(torch_amp[k], truth[k]), rel_l2(hip[k], truth[k])
@@ -77,5 +86,5 @@ def test_step_error_within_pytorch_amp_error(B, amp, size):
         print(f"{k:32s} hip {e_hip:.3e}  torch-amp {e_amp:.3e}  ratio {ratio:.2f}")
         if e_hip > 1.5 * e_amp:
             bad.append((k, e_hip, e_amp))
-    print(f"B={B} {amp} {size}x{size}: worst hip / torch-amp error ratio {worst:.2f}")
+    print(f"B={B} {amp} {size}x{size} {stats}: worst hip / torch-amp error ratio {worst:.2f}")
     assert not bad, bad
