@@ -63,6 +63,10 @@ struct GemmArgs {
     // partial slots (2 per workgroup) in `part`, the per-tile arrival counters in `cnt`
     long sk_total = 0;
     int sk_nk = 0, sk_grid = 0;
+    // > 0: every workgroup's share is exactly sk_share k-tiles (R(w) = w * sk_share, the last one shorter), a multiple
+    // chosen so that the shares start at few distinct k offsets inside their tiles: the workgroups on one XCD that start
+    // at the same offset walk k together over tiles of one tile row (sk_plan)
+    int sk_share = 0;
     // LayerNorm folded into the encoder GEMMs (vit.hip, 16-bit; r04): a RESID product may also write a compute-dtype
     // copy of its output rows (xh) and per-row partial sums / sums of squares of them (rpart [M][N / BN * WGN][2], one
     // pair per tile column and wave column); an EPI_LN / EPI_LN_GELU product normalises its rows from such partials
@@ -256,8 +260,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
     constexpr bool SKM = SPL && MODE != 0;
     const bool skr = SKM && g.sk_total > 0;
     // (32-bit: (sk_total + 1) * grid < 2^31, launch_gemm_k)
-    const unsigned G = gridDim.x, skt = (unsigned)g.sk_total, sknk = (unsigned)g.sk_nk;
-    const unsigned it_beg = skr ? (unsigned)wg * skt / G : 0u, it_end = skr ? (unsigned)(wg + 1) * skt / G : 0u;
+    const unsigned G = gridDim.x, skt = (unsigned)g.sk_total, sknk = (unsigned)g.sk_nk, shr = (unsigned)g.sk_share;
+    const unsigned it_beg = !skr ? 0u : shr ? (unsigned)wg * shr : (unsigned)wg * skt / G;
+    const unsigned it_end = !skr ? 0u : shr ? min((unsigned)(wg + 1) * shr, skt) : (unsigned)(wg + 1) * skt / G;
     if (skr && it_beg >= it_end) return;
     // a segment: k-tiles [it, it + nk) of one tile (always inlined: a loop over the segments, or a call per segment,
     // made the 8-wave tiles spill 60-230 registers)
@@ -647,8 +652,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             int mine, mypiece, wf = 0, np = g.splits;
             const unsigned i0 = (unsigned)ltile * sknk;
             if (skr) {
-                wf = (int)(((i0 + 1) * G - 1) / skt);
-                np = (int)(((i0 + sknk) * G - 1) / skt) - wf + 1;
+                // the workgroups whose shares touch this tile: the last w with R(w) <= i0 .. the last with R(w) < i0 + nk
+                wf = shr ? (int)(i0 / shr) : (int)(((i0 + 1) * G - 1) / skt);
+                np = (shr ? (int)((i0 + sknk - 1) / shr) : (int)(((i0 + sknk) * G - 1) / skt)) - wf + 1;
                 mine = it == it_beg ? 2 * wg : 2 * wg + 1;
                 mypiece = wg - wf;
             } else {
@@ -657,7 +663,8 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             auto slot = [&](int piece) -> int {
                 if (!skr) return piece;
                 const int w = wf + piece;
-                return piece == 0 && (unsigned)w * skt / G < i0 ? 2 * w + 1 : 2 * w;
+                const unsigned rw = shr ? (unsigned)w * shr : (unsigned)w * skt / G;
+                return piece == 0 && rw < i0 ? 2 * w + 1 : 2 * w;
             };
             // one buffer resource over the partials; aux 16 = sc1
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1014,7 +1021,8 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
     if (g.sk_total) {
         if (!SPL || MODE == 0 || g.splits != 1 || g.sk_nk * BK != g.K || (long)tiles * g.sk_nk != g.sk_total ||
             g.sk_grid < tiles || g.sk_grid > g.sk_total || (g.sk_total + 1) * g.sk_grid >= (1L << 31) || !g.cnt ||
-            !g.part || tiles > 4096)
+            !g.part || tiles > 4096 ||
+            (g.sk_share && (g.sk_share > g.sk_nk || (long)g.sk_grid != (g.sk_total + g.sk_share - 1) / g.sk_share)))
             return EBC_E_ARG;
     }
     const int nwg = g.sk_total ? g.sk_grid : tiles * g.splits;
@@ -1279,18 +1287,36 @@ int conv_cfg(bool sixteen, int mode, int M, int N)
 //     (fewer tiles than CUs, 16 crops' 196: 140-143 us vs 138-142 plain -- no gain, not taken)
 //   MODE 2 up to 256 k-tiles a tile: the 16-crop weight gradient (108 tiles x 196 k-tiles): 140-143 us vs 144-152
 //     on 2 splits (216 workgroups); 32 crops (392 k-tiles): 269-272 us vs 247-253 on 2 splits, not taken
-struct SkPlan { int dp; long total; int nk, grid; };
+//   MODE 2 shares aligned to few k offsets (r05, `share`): with R(w) = w * total / grid every workgroup starts at its own
+//     offset inside its tile, so no two walk the same k-slice of a shared panel at the same time (r04 PMC: 968.7 MB per
+//     launch beyond L2, hit rate 0.32).  A share of exactly `share` k-tiles, the multiple of nk / F (F distinct offsets)
+//     nearest above total / NUM_CU: 108 tiles x 196 k-tiles -> 84 (F = 7, 252 workgroups); the workgroups w, w + 7,
+//     w + 14, .. of one XCD then start at one offset, on tiles 3 apart in one tile row (one A panel).
+struct SkPlan { int dp; long total; int nk, grid, share; };
+int sk_share_for(long total, long nk) {
+    const long lo = (total + NUM_CU - 1) / NUM_CU;
+    int best = 0;
+    long bestF = nk + 1;
+    for (long s = lo; s <= lo + lo / 32 && s <= nk; ++s) {              // at most ~3 % over the even share
+        long a = s, b = nk;
+        while (b) { const long t = a % b; a = b; b = t; }                 // gcd(s, nk)
+        if (nk / a < bestF) { bestF = nk / a; best = (int)s; }
+    }
+    return bestF <= 16 ? best : 0;
+}
 SkPlan sk_plan(int mode, int cfg, int M, int N, int K, int bk, long wgs) {
-    if (cfg != 3 && cfg != 7) return SkPlan{0, 0, 0, 0};
+    if (cfg != 3 && cfg != 7) return SkPlan{0, 0, 0, 0, 0};
     const TileCfg* c = find_cfg(cfg);
     const long T = ntiles(M, N, c->bm, c->bn), nk = K / bk;
     const long waves = (wgs + NUM_CU - 1) / NUM_CU;
     const double fill = (double)wgs / (double)(waves * NUM_CU);
     const long dp = T / NUM_CU * NUM_CU, rest = T - dp;
-    if (mode == 1 ? dp == 0 : nk > 256) return SkPlan{0, 0, 0, 0};
-    const int grid = (int)std::min<long>(NUM_CU, rest * 4);
-    if (fill >= 0.92 || rest == 0 || rest * nk < 16L * grid) return SkPlan{0, 0, 0, 0};
-    return SkPlan{(int)dp, rest * nk, (int)nk, grid};
+    if (mode == 1 ? dp == 0 : nk > 256) return SkPlan{0, 0, 0, 0, 0};
+    int grid = (int)std::min<long>(NUM_CU, rest * 4);
+    if (fill >= 0.92 || rest == 0 || rest * nk < 16L * grid) return SkPlan{0, 0, 0, 0, 0};
+    const int share = mode == 2 ? sk_share_for(rest * nk, nk) : 0;
+    if (share) grid = (int)((rest * nk + share - 1) / share);
+    return SkPlan{(int)dp, rest * nk, (int)nk, grid, share};
 }
 size_t sk_ws_bytes(int cfg, const SkPlan& p) {
     const TileCfg* c = find_cfg(cfg);
@@ -1348,6 +1374,7 @@ int dispatch_conv(GemmArgs g, int mode, int epi, void* ws, size_t wsb, hipStream
             g.sk_total = sk.total;
             g.sk_nk = sk.nk;
             g.sk_grid = sk.grid;
+            g.sk_share = sk.share;
             g.cnt = reinterpret_cast<int*>(ws);
             g.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + off);
             if (mode == 1 && epi == EPI_STORE) return launch_conv_tile<E, T, EPI_STORE, 1>(g, cfg, st);

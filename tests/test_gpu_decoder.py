@@ -295,3 +295,49 @@ def test_conv3x3_stream_k(B, H, C, N, plan):
             torch.testing.assert_close(colsum[0], ref.sum(0), rtol=1e-2, atol=2.0)
             torch.testing.assert_close(colsum[1], (ref ** 2).sum(0), rtol=3e-3, atol=1.0)
     assert int(ws[:16384].view(torch.int32).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("B,plan", [(16, (256, 192, -252)),     # stream-K: 252 shares of 84 k-tiles (7 start offsets)
+                                    (32, (256, 192, 2)),        # 392 k-tiles a tile: 2-way split-K
+                                    (3, None)])                 # 3 crops: 2352 pixels, a K tail
+def test_conv3x3_wgrad_abi_matches_torch(B, plan):
+    """ebc_conv3x3_wgrad (MODE 2 implicit GEMM over the interior pixels) on f16 operands vs torch's conv2d weight
+    gradient of the same f16 values in f64: only the f32 accumulation order differs (rel-L2 < 1e-5); bitwise equal
+    across launches (the stream-K pieces / split partials are summed in a fixed order)."""
+    from ebc_amd import _lib
+    import ctypes
+    L = _lib.lib()
+    dt, H, W, C = torch.float16, 28, 28, 768
+    N = C
+    dev = torch.device("cuda")
+    geo = (ctypes.c_long * 6)()
+    _lib.check(L.ebc_dec_geometry(_lib.EBC_F16, B, H, W, C, geo), "geo")
+    Hp, Wp, HWp, Kq, Q, Qs = (int(v) for v in geo)
+    if plan is not None:
+        out = (ctypes.c_int * 3)()
+        L.ebc_conv_tile_config(_lib.EBC_F16, 2, N, 9 * C, Kq, out)
+        assert tuple(out) == plan
+    g = torch.Generator(device=dev).manual_seed(50 + B)
+    x = torch.randn(B, H, W, C, generator=g, device=dev).to(dt)
+    dz = (torch.randn(B, H, W, N, generator=g, device=dev) / 8).to(dt)
+    xpad = torch.zeros(B, Hp, Wp, C, device=dev, dtype=dt)
+    xpad[:, 1:H + 1, 1:W + 1] = x
+    xT3 = torch.empty(3, C, Qs, device=dev, dtype=dt)
+    _lib.check(L.ebc_dec_transpose3(_lib.EBC_F16, _lib.ptr(xpad), _lib.ptr(xT3), B, H, W, C, _lib.stream()), "t3")
+    dzT = torch.zeros(N, Qs, device=dev, dtype=dt)
+    dzT[:, :B * HWp].view(N, B, HWp)[:, :, :H * W] = dz.reshape(B, H * W, N).permute(2, 0, 1)
+    ws = torch.zeros(L.ebc_dec_workspace_bytes(_lib.EBC_F16, B, H, W, C, N), dtype=torch.uint8, device=dev)
+    outs = []
+    for _ in range(2):
+        dw = torch.empty(N, C, 3, 3, device=dev)
+        _lib.check(L.ebc_conv3x3_wgrad(_lib.EBC_F16, _lib.ptr(dzT), _lib.ptr(xT3), _lib.ptr(dw), _lib.ptr(ws), ws.numel(),
+                                       B, H, W, C, N, _lib.stream()), "wgrad")
+        outs.append(dw)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).cpu().double(), (N, C, 3, 3),
+                                      dz.permute(0, 3, 1, 2).cpu().double(), padding=1)
+    err = rel_l2(outs[1].cpu().double(), ref)
+    print(f"B={B}: wgrad rel-L2 vs f64 {err:.2e}")
+    assert err < 1e-5
+    assert int(ws[:16384].view(torch.int32).abs().sum()) == 0          # arrival counters re-armed

@@ -156,8 +156,9 @@ def test_decoder_at_bench_batch(dname, B):
     _lib.check(_lib.lib().ebc_dec_geometry(_lib.dtype_code(dt), B, 2 * h, 2 * h, C, geo), "ebc_dec_geometry")
     assert geo[3] == B * 784                            # the interior pixels only (r03: B * 14 * 64 padded)
     cfg2, (_, _, splits) = conv_cfg(dt, 2, C, 9 * C, geo[3])
-    # 108 tiles x 196 k-tiles: stream-K over 256; x 392 k-tiles (32 crops): 2-way split-K (gemm.hip sk_plan)
-    assert cfg2 == 3 and splits == (-256 if B == 16 else 2), (cfg2, splits)
+    # 108 tiles x 196 k-tiles: stream-K, shares of 84 k-tiles (7 start offsets) on 252 workgroups; x 392 k-tiles
+    # (32 crops): 2-way split-K (gemm.hip sk_plan)
+    assert cfg2 == 3 and splits == (-252 if B == 16 else 2), (cfg2, splits)
     blk = _block(C)
     g = torch.Generator(device="cuda").manual_seed(B)
     feat = torch.randn(B, h, h, C, device="cuda", generator=g)
