@@ -67,6 +67,10 @@ def parse(argv=None):
     ap.add_argument("--no-probe", action="store_true", help="skip the instrumented in-step kernel timing pass")
     ap.add_argument("--no-ln-fold", action="store_true",
                     help="A/B: ln_1 / ln_2 as LayerNorm launches instead of folded into the QKV / c_fc products")
+    ap.add_argument("--touch", type=int, default=None, choices=[0, 1],
+                    help="A/B: the attention launches' weight touch off / on (ebc_set_weight_touch)")
+    ap.add_argument("--no-ln-fold-bwd", action="store_true",
+                    help="A/B: ln_2's backward as a LayerNorm launch instead of in the c_fc dX product's epilogue")
     ap.add_argument("--optim", default="hip", choices=["hip", "torch"],
                     help="optimizer step: ebc_amd.optim Adam + GradScaler (HIP, 2 launches) or torch's fused Adam + "
                          "torch.amp.GradScaler (same arithmetic; for A/B)")
@@ -245,6 +249,11 @@ def setup(args, rank, world, local, device):
         model = get_model("clip_vit_b_16", 224, 8, BINS, ANCHORS_NWPU, prompt_type="word", num_vpt=32,
                           vpt_drop=0.0, deep_vpt=True, weights_seed=0).to(device)
         model.vit_ln_fold = not getattr(args, "no_ln_fold", False)
+        if getattr(args, "no_ln_fold_bwd", False):
+            model.vit_bwd_flags = 2                      # EBC_VIT_BWD_NO_LN_FOLD
+    if getattr(args, "touch", None) is not None:
+        from ebc_amd import _lib as _l
+        _l.check(_l.lib().ebc_set_weight_touch(args.touch), "ebc_set_weight_touch")
     model.train()
     if world > 1:
         from ebc_amd.distributed import wrap_ddp       # SyncBatchNorm + DDP, as trainer.py:147
@@ -371,7 +380,7 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
         kind = _lib.PROBE_KINDS.get(r.kind, str(r.kind))
         if kind == "gemm":
             mode = {0: "", 1: " conv3x3", 2: " conv3x3-wgrad"}[r.mode]
-            epi = {0: "store", 1: "gelu", 2: "resid", 3: "gelu_bwd", 4: "bn_stats", 5: "add_relu_grad", 6: "ln", 7: "ln_gelu"}.get(r.epi, r.epi)
+            epi = {0: "store", 1: "gelu", 2: "resid", 3: "gelu_bwd", 4: "bn_stats", 5: "add_relu_grad", 6: "ln", 7: "ln_gelu", 8: "ln_bwd"}.get(r.epi, r.epi)
             key = f"gemm_nt {r.bm}x{r.bn}{mode} {epi} M={r.m} N={r.n} K={r.k}"
             flops = 2.0 * r.m * r.n * r.k
         elif kind == "dace_loss":

@@ -1224,6 +1224,12 @@ template <class E> int attn_bwd_long(const void* qkv, const void* dout, const vo
 // 128 queries, two a CU (768 halves: 1.5 passes of the 512 slots, each half half the work)
 constexpr int ATTN_CUS = 256;
 int attn_waves(int L) { return L > 128 ? 16 : 8; }
+
+// Weight touch mode (ebc_set_weight_touch): 1 (default) in the attention kernels, 0 off.  (r05 measured a third mode, a
+// touch kernel on a side stream whose workgroups reserve enough LDS to land only on the 64 CUs a 16-crop attention
+// launch leaves idle: 4.58 ms a step against 4.39 in-kernel and 4.55 with no touch, same box -- the fork / join events
+// around 24 launches a step cost more than the touch; removed.)
+int g_touch_mode = 1;
 int attn_fwd_waves(int B, int L, int H) { return attn_waves(L) == 16 && B * H <= ATTN_CUS ? 16 : 8; }
 
 // the CLIP ViT-B/16 + 32-prompt sequence (1 + 32 + 196 tokens) gets kernels compiled for it
@@ -1233,10 +1239,10 @@ template <class E, int NW, int LFIX, int QT = 1> int attn_fwd_nw(const void* qkv
                                                                 hipStream_t st, const TouchList* touch = nullptr)
 {
     using C = AttnCfg<E>;
-    const TouchList t = touch ? *touch : TouchList{};
     const size_t lds = 2 * C::TILE_BYTES;
     if (!ensure_lds<attn_fwd_kernel<E, NW, LFIX, QT>>((int)lds, st)) return EBC_E_LAUNCH;
     const int grid = B * H * ((L + 16 * NW * QT - 1) / (16 * NW * QT));
+    const TouchList t = touch && g_touch_mode == 1 ? *touch : TouchList{};
     const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_FWD, 0, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_fwd_kernel<E, NW, LFIX, QT>), dim3(grid), dim3(64 * NW), lds, st, (const typename E::T*)qkv,
                        (typename E::T*)out, lse, B, L, H, 0.125f, t);
@@ -1279,9 +1285,9 @@ template <class E, int LFIX> int attn_bwd_one(const void* qkv, const void* dout,
                                               void* dqkv, int B, int L, int H, hipStream_t st, int rows, const TouchList* touch)
 {
     using C = AttnCfg<E>;
-    const TouchList t = touch ? *touch : TouchList{};
     const size_t lds = 4 * C::TILE_BYTES + 2 * LP * sizeof(float);
     if (!ensure_lds<attn_bwd_one_kernel<E, LFIX>>((int)lds, st)) return EBC_E_LAUNCH;
+    const TouchList t = touch && g_touch_mode == 1 ? *touch : TouchList{};
     const int pi = probe_on() ? probe_start(EBC_PROBE_ATTN_BWD_DQ, 1, 0, 0, 0, B, L, H, st) : -1;
     hipLaunchKernelGGL((attn_bwd_one_kernel<E, LFIX>), dim3(B * H), dim3(1024), lds, st, (const typename E::T*)qkv,
                        (const typename E::T*)dout, (const typename E::T*)out, lse, (typename E::T*)dqkv, B, L, H, 0.125f,
@@ -1308,6 +1314,13 @@ template <class E> int attn_bwd_t(const void* qkv, const void* dout, const void*
 }
 
 }  // namespace
+
+extern "C" int ebc_set_weight_touch(int mode)
+{
+    if (mode < 0 || mode > 1) return EBC_E_ARG;
+    g_touch_mode = mode;
+    return EBC_OK;
+}
 
 namespace ebc {
 int attention_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, hipStream_t st,

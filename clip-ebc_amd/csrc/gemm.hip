@@ -26,8 +26,13 @@ using namespace ebc;
 namespace {
 
 constexpr int LN_PMAX = ebc::GEMM_LN_PMAX;   // EPI_LN: at most 16 row partials (N / BN * 2 of the producing product)
+constexpr int LN_PMAX_B = ebc::GEMM_LN_PMAX_B;   // EPI_LN_BWD: at most 32
 enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_STATS = 4, EPI_ADD_RELU_GRAD = 5, EPI_LN = 6,
-       EPI_LN_GELU = 7 };
+       EPI_LN_GELU = 7, EPI_LN_BWD = 8 };
+// row partials an LN-normalising epilogue reads (its LDS staging past the ring: BM rows of ln_pmax float2)
+template <int EPI> constexpr int ln_pmax() {
+    return EPI == EPI_LN_BWD ? LN_PMAX_B : (EPI == EPI_LN || EPI == EPI_LN_GELU) ? LN_PMAX : 0;
+}
 
 struct GemmArgs {
     const void* A; const void* B; void* C;
@@ -86,6 +91,13 @@ struct GemmArgs {
     const float* vrep = nullptr;
     long vrep_bs = 0;
     int vrep_L = 1, vrep_nv = 0;
+    // LayerNorm backward fold (kernels.h GemmLn, r05): GELU_BWD writes the row partials bpart [M][N / BN * WGN][2] of
+    // sum dA s and sum dA (A - c) (s = lnb_s, c = lnb_c, staged per tile in LDS); EPI_LN_BWD reads them (lnp, lnparts),
+    // the LayerNorm input rows lnx (f32) and the row mean / rstd (ln_mean / ln_rstd as inputs)
+    const float* lnb_s = nullptr;
+    const float* lnb_c = nullptr;
+    float* bpart = nullptr;
+    const float* lnx = nullptr;
     // algorithmic K the probe records (0: K).  MODE 2's K loop runs over padded image rows; its algorithmic K is
     // the interior pixel count B*H*W (bench.py counts 2*M*N*kalg FLOP)
     int kalg = 0;
@@ -383,7 +395,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         auto stage = [&](int buf, int kt) {
             if constexpr (NLW == 0) stage_pieces(buf, kt);
         };
-        constexpr bool LNP = MODE == 0 && (EPI == EPI_LN || EPI == EPI_LN_GELU);
+        constexpr bool LNP = MODE == 0 && ln_pmax<EPI>() > 0;
         auto stage_stats = [&]() {
             // 1 KiB a wave-instruction (16 B a lane), the last rows' bytes clamped inside the buffer (rows >= M).
             // (Issued with the k-tiles 1..4 of the 2-stage rings instead, r04 measured no difference.)
@@ -395,6 +407,20 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 o = o + 16u <= total ? o : total - 16u;
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + o),
                                                  EBC_LDS(smem + S * STAGE + c * 1024), 16, 0, 0);
+            }
+        };
+        // GELU_BWD writing the LayerNorm-backward partials (g.bpart): s and c of the tile's BN columns into LDS past the
+        // ring as stage_stats does (counted loads older than every ring piece), SCP 1-KiB pieces a vector, lanes past
+        // the tile's columns clamped (they land in the padding)
+        constexpr bool BPT = MODE == 0 && EPI == EPI_GELU_BWD;
+        constexpr int SCP = (BN * 4 + 1023) / 1024;
+        auto stage_sc = [&]() {
+            for (int pc = lw; pc < 2 * SCP; pc += NLDR) {
+                const float* vsrc = pc < SCP ? g.lnb_s : g.lnb_c;
+                int o = (pc < SCP ? pc : pc - SCP) * 256 + lane * 4;       // float offset in the tile's columns
+                o = o + 4 <= BN ? o : BN - 4;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(vsrc + n0 + o),
+                                                 EBC_LDS(smem + S * STAGE + pc * 1024), 16, 0, 0);
             }
         };
 
@@ -477,6 +503,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 // loader wave: the compute waves' ring schedule (one barrier per k-tile, the buffer of tile kt
                 // refilled with tile kt + S right after the barrier that retires its reads), then exit
                 if constexpr (LNP) stage_stats();
+                if constexpr (BPT) { if (g.bpart) stage_sc(); }
                 for (int s = 0; s < S - 1; ++s)
                     if (s < nk) stage_pieces(s, s);
                 wait_tile(0, std::true_type{});
@@ -494,7 +521,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         // 4-wave RESID tiles (one wave per SIMD: registers to spare): the f32 residual operand of the epilogue is
         // loaded before the ring fills, so its latency hides under the first tiles' instead of being paid after the
         // K loop (vmcnt retires loads in order: issued any later, a counted ring wait would block on it mid-loop)
-        constexpr bool PREF = MODE == 0 && EPI == EPI_RESID && NW == 4 && NW + NLW <= 8;
+        constexpr bool PREF = MODE == 0 && (EPI == EPI_RESID || EPI == EPI_LN_BWD) && NW == 4 && NW + NLW <= 8;
         // RESID: the residual row r, or (vrep) the prompt row replacing output row r -- an address select, no branch
         constexpr bool VREP = MODE == 0 && EPI == EPI_RESID && EB == 2;    // (gemm_nt_ln: 16-bit only)
         auto vrep_row = [&](int r) -> bool {
@@ -543,6 +570,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         // row and lane, duplicated across the wave columns, cost the products 2.5-4 us a launch in the start-up burst:
         // profiles/r04t_lnfold_lab_*.txt.)
         if constexpr (LNP && NLW == 0) stage_stats();
+        if constexpr (BPT && NLW == 0) { if (g.bpart) stage_sc(); }
 #pragma unroll
         for (int s = 0; s < S - 1; ++s)
             if (s < nk) stage(s, s);
@@ -727,12 +755,14 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 // group q, 8 (a sub-tile pair) or 4 (odd last sub-tile) consecutive columns.  Operands
                 // (resid / aux) are loaded for the whole wave tile first (row-clamped, unconditional), then each
                 // group is finished and stored; rows >= M are never stored.
-                static_assert(EPI <= EPI_GELU_BWD || EPI == EPI_LN || EPI == EPI_LN_GELU, "MODE 0 epilogues");
+                static_assert(EPI <= EPI_GELU_BWD || EPI == EPI_LN || EPI == EPI_LN_GELU || EPI == EPI_LN_BWD,
+                              "MODE 0 epilogues");
                 constexpr bool LN = EPI == EPI_LN || EPI == EPI_LN_GELU, GE = EPI == EPI_GELU || EPI == EPI_LN_GELU;
+                constexpr bool LNB = EPI == EPI_LN_BWD;
                 TO* C = reinterpret_cast<TO*>(g.C);
                 constexpr int NP = TN / 2, ODD = TN & 1;
-                constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID;
-                using PA = typename std::conditional<EPI == EPI_RESID, float, T>::type;
+                constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_RESID || LNB;
+                using PA = typename std::conditional<EPI == EPI_RESID || LNB, float, T>::type;
                 typedef PA pa8 __attribute__((ext_vector_type(8)));
                 typedef PA pa4 __attribute__((ext_vector_type(4)));
                 const int mb = m0 + wm * WM + fr;
@@ -776,7 +806,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                         const float4* pp = reinterpret_cast<const float4*>(st + (wm * WM + a * 16 + fr) * g.lnparts * 8);
                         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-                        for (int j = 0; j < LN_PMAX / 8; ++j) {
+                        for (int j = 0; j < ln_pmax<EPI>() / 8; ++j) {
                             const int q = fg + 4 * j;
                             const bool in = 2 * q < g.lnparts;
                             const float4 t = pp[in ? q : 0];
@@ -793,11 +823,51 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                         if (g.ln_mean && tn == 0 && wn == 0 && fg == 0 && m < g.M) { g.ln_mean[m] = mean; g.ln_rstd[m] = rsv[a]; }
                     }
                 }
+                // LN_BWD: per row rstd, mean(g) = sum g / N and mean(g xhat) = sum g xhat / N from the GELU' product's
+                // partials in LDS (the row's 4 lanes read the pairs fg, fg + 4, .. and meet by lane swaps, as above),
+                // the LayerNorm's mean / rstd from ln_mean / ln_rstd:  out = rstd (g - mean(g) - (x - mu) rstd mean(g
+                // xhat)) + resid
+                float kr[LNB ? TM : 1], ka[LNB ? TM : 1], km[LNB ? TM : 1], kb[LNB ? TM : 1];
+                if constexpr (LNB) {
+                    const char* st = smem + S * STAGE;
+#pragma unroll
+                    for (int a = 0; a < TM; ++a) {
+                        const float4* pp = reinterpret_cast<const float4*>(st + (wm * WM + a * 16 + fr) * g.lnparts * 8);
+                        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                        for (int j = 0; j < ln_pmax<EPI>() / 8; ++j) {
+                            const int q = fg + 4 * j;
+                            const bool in = 2 * q < g.lnparts;
+                            const float4 t = pp[in ? q : 0];
+                            s1 += in ? t.x + t.z : 0.f;
+                            s2 += in ? t.y + t.w : 0.f;
+                        }
+                        s1 = pair_sum(s1);
+                        s2 = pair_sum(s2);
+                        const int m = min(mb + a * 16, g.M - 1);
+                        kr[a] = g.ln_rstd[m];
+                        km[a] = g.ln_mean[m];
+                        ka[a] = s1 / (float)g.N;
+                        kb[a] = kr[a] * (s2 / (float)g.N);
+                    }
+                }
+                // GELU_BWD with bpart: the lane's partial sums dA s and dA (A - c) of its row over its columns
+                float bs1 = 0.f, bs2 = 0.f;
+                auto bpt_add = [&](const float* v, int w, const auto& pre, int cl) {
+                    const float* sl = reinterpret_cast<const float*>(smem + S * STAGE) + cl;
+                    const float* cv = reinterpret_cast<const float*>(smem + S * STAGE + SCP * 1024) + cl;
+                    for (int i = 0; i < w; ++i) {
+                        bs1 = fmaf(v[i], sl[i], bs1);
+                        bs2 = fmaf(v[i], (float)pre[i] - cv[i], bs2);
+                    }
+                };
                 float rs = 1.f, rsmu = 0.f;
+                float lr = 1.f, la = 0.f, lm = 0.f, lb = 0.f;    // LN_BWD: the row's constants
                 bool vr = false;                     // RESID: the row is a replaced prompt row
                 // RESID with rpart: the lane's partial sum / sum of squares of its row's output values
                 float rsum = 0.f, rsq = 0.f;
-                auto finish = [&](float* v, int w, const float* bias, const float* lwv, const auto& pre, size_t off) {
+                auto finish = [&](float* v, int w, const float* bias, const float* lwv, const auto& pre, size_t off,
+                                  const auto& xs) {
                     if constexpr (LN) {
                         for (int i = 0; i < w; ++i) v[i] = fmaf(rs, v[i], -rsmu * lwv[i]);
                     }
@@ -810,6 +880,10 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                         for (int i = 0; i < w; ++i) v[i] = quick_gelu(v[i]);
                     } else if constexpr (EPI == EPI_GELU_BWD) {
                         for (int i = 0; i < w; ++i) v[i] *= quick_gelu_grad((float)pre[i]);
+                    } else if constexpr (LNB) {
+                        for (int i = 0; i < w; ++i) v[i] = fmaf(lr, v[i] - la - (xs[i] - lm) * lb, (float)pre[i]);
+                        if (w == 8) store8<T>(reinterpret_cast<T*>(g.xh) + off, v);
+                        else store4<T>(reinterpret_cast<T*>(g.xh) + off, v);
                     } else if constexpr (EPI == EPI_RESID) {
                         for (int i = 0; i < w; ++i) v[i] = vr ? (float)pre[i] : v[i] + pre[i];
                         if (VREP && g.rpart) {
@@ -825,6 +899,19 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     constexpr int a0 = decltype(phc)::value * TMP;
                     pa8 p8[PRE ? TMP : 1][NP > 0 ? NP : 1];
                     pa4 p4[PRE && ODD ? TMP : 1];
+                    typedef float xv8 __attribute__((ext_vector_type(8)));
+                    typedef float xv4 __attribute__((ext_vector_type(4)));
+                    xv8 x8[LNB ? TMP : 1][NP > 0 ? NP : 1];
+                    xv4 x4[LNB && ODD ? TMP : 1];
+                    if constexpr (LNB) {
+#pragma unroll
+                        for (int a = 0; a < TMP; ++a) {
+                            const float* sr = g.lnx + (size_t)min(mb + (a0 + a) * 16, g.M - 1) * g.N + nb;
+#pragma unroll
+                            for (int q = 0; q < NP; ++q) x8[a][q] = *reinterpret_cast<const xv8*>(sr + q * 32 + fg * 8);
+                            if constexpr (ODD) x4[a] = *reinterpret_cast<const xv4*>(sr + NP * 32 + fg * 4);
+                        }
+                    }
                     if constexpr (PREF) {
 #pragma unroll
                         for (int a = 0; a < TMP; ++a) {
@@ -838,7 +925,8 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
 #pragma unroll
                             for (int q = 0; q < NP; ++q) p8[a][q] = __builtin_convertvector(gp8[a][q], pa8);
                     } else if constexpr (PRE) {
-                        const PA* src = EPI == EPI_RESID ? reinterpret_cast<const PA*>(g.resid) : reinterpret_cast<const PA*>(g.aux);
+                        const PA* src = (EPI == EPI_RESID || LNB) ? reinterpret_cast<const PA*>(g.resid)
+                                                                   : reinterpret_cast<const PA*>(g.aux);
 #pragma unroll
                         for (int a = 0; a < TMP; ++a) {
                             const int r = min(mb + (a0 + a) * 16, g.M - 1);
@@ -858,6 +946,9 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                             rs = rsv[a0 + a];
                             rsmu = rsmuv[a0 + a];
                         }
+                        if constexpr (LNB) {
+                            lr = kr[a0 + a]; la = ka[a0 + a]; lm = km[a0 + a]; lb = kb[a0 + a];
+                        }
                         if constexpr (EPI == EPI_RESID) vr = vrep_row(m);
 #pragma unroll
                         for (int q = 0; q < NP; ++q) {
@@ -865,13 +956,25 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                                           acc[a0 + a][2 * q + 1][0], acc[a0 + a][2 * q + 1][1], acc[a0 + a][2 * q + 1][2],
                                           acc[a0 + a][2 * q + 1][3]};
                             const float* lwq = LN ? lw[q] : nullptr;
-                            if constexpr (PRE) finish(v, 8, bv[q], lwq, p8[a][q], ro + q * 32 + fg * 8);
-                            else finish(v, 8, bv[q], lwq, 0, ro + q * 32 + fg * 8);
+                            if constexpr (PRE) finish(v, 8, bv[q], lwq, p8[a][q], ro + q * 32 + fg * 8, x8[LNB ? a : 0][q]);
+                            else finish(v, 8, bv[q], lwq, 0, ro + q * 32 + fg * 8, 0);
+                            if constexpr (BPT) { if (g.bpart) bpt_add(v, 8, p8[a][q], wn * WN + q * 32 + fg * 8); }
                         }
                         if constexpr (ODD) {
                             float v[4] = {acc[a0 + a][TN - 1][0], acc[a0 + a][TN - 1][1], acc[a0 + a][TN - 1][2], acc[a0 + a][TN - 1][3]};
-                            if constexpr (PRE) finish(v, 4, bo, lwo, p4[a], ro + NP * 32 + fg * 4);
-                            else finish(v, 4, bo, lwo, 0, ro + NP * 32 + fg * 4);
+                            if constexpr (PRE) finish(v, 4, bo, lwo, p4[a], ro + NP * 32 + fg * 4, x4[LNB ? a : 0]);
+                            else finish(v, 4, bo, lwo, 0, ro + NP * 32 + fg * 4, 0);
+                            if constexpr (BPT) { if (g.bpart) bpt_add(v, 4, p4[a], wn * WN + NP * 32 + fg * 4); }
+                        }
+                        if constexpr (BPT) {
+                            if (g.bpart) {
+                                // one partial pair per (tile column, wave column), as the RESID row partials
+                                const float t1 = pair_sum(bs1), t2 = pair_sum(bs2);
+                                if (fg == 0)
+                                    reinterpret_cast<float2*>(g.bpart)[(size_t)m * (g.N / BN * WGN) + tn * WGN + wn] = float2{t1, t2};
+                                bs1 = 0.f;
+                                bs2 = 0.f;
+                            }
                         }
                         if constexpr (EPI == EPI_RESID) {
                             if (VREP && g.rpart) {
@@ -1008,11 +1111,18 @@ template <class E, class TO, int EPI, int BM, int BN, int S, int WGM, int WGN, i
 int launch_gemm_k(const GemmArgs& g, hipStream_t st)
 {
     constexpr int WM = BM / WGM;
-    // EPI_LN: the workgroup's row partials (BM rows of at most LN_PMAX float2) past the ring
-    constexpr bool LNE = MODE == 0 && (EPI == EPI_LN || EPI == EPI_LN_GELU);
-    constexpr int RING = S * (BM + BN) * ROWB, LNB = LNE ? RING + BM * LN_PMAX * 8 : 0;
+    // EPI_LN / EPI_LN_BWD: the workgroup's row partials (BM rows of at most ln_pmax float2) past the ring; GELU_BWD:
+    // the LayerNorm-backward fold's s / c column vectors (2 x 1-KiB-rounded)
+    constexpr bool LNE = MODE == 0 && ln_pmax<EPI>() > 0;
+    constexpr int RING = S * (BM + BN) * ROWB, LNB0 = LNE ? RING + BM * ln_pmax<EPI>() * 8 : 0;
+    constexpr int BPB = MODE == 0 && EPI == EPI_GELU_BWD ? RING + 2 * ((BN * 4 + 1023) / 1024) * 1024 : 0;
+    constexpr int LNB = LNB0 > BPB ? LNB0 : BPB;
     constexpr int LDS = gemm_lds_bytes<BM, BN, S, ROWB, WM>() > LNB ? gemm_lds_bytes<BM, BN, S, ROWB, WM>() : LNB;
-    static_assert(LDS <= 160 * 1024, "LDS");
+    // (the LN_BWD instances of the 256-wide tiles would need more: that epilogue runs on the N = 768 tiles only)
+    static_assert(LDS <= 160 * 1024 || EPI == EPI_LN_BWD, "LDS");
+    if constexpr (LDS > 160 * 1024) {
+        return EBC_E_UNSUPPORTED;
+    } else {
     constexpr int BK = ROWB / E::BYTES;
     if (!ensure_lds<gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL, NLW>>(LDS, st)) return EBC_E_LAUNCH;
     if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
@@ -1032,6 +1142,7 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
     probe_stop(pi, st);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
+    }
 }
 
 // Split-K launches exist for the weight gradients (MODE 2, and MODE 0 f32 stores) and the conv GEMMs' tail tiles
@@ -1174,6 +1285,9 @@ int dispatch_epi(const GemmArgs& g, int epi, int out_f32, void* ws, size_t wsb, 
             return EBC_E_UNSUPPORTED;
         case EPI_LN_GELU:
             if constexpr (E::BYTES == 2) return out_f32 ? EBC_E_UNSUPPORTED : dispatch_tile<E, typename E::T, EPI_LN_GELU>(g, ws, wsb, st);
+            return EBC_E_UNSUPPORTED;
+        case EPI_LN_BWD:
+            if constexpr (E::BYTES == 2) return out_f32 ? dispatch_tile<E, float, EPI_LN_BWD>(g, ws, wsb, st) : EBC_E_UNSUPPORTED;
             return EBC_E_UNSUPPORTED;
     }
     return EBC_E_ARG;
@@ -1514,6 +1628,22 @@ int gemm_nt_ln(int dtype, int epi, int out_f32, const void* A, const void* B, vo
         g.lnp = ln.lnp;
         g.lnparts = ln.lnparts;
         g.lnw = ln.lnw;
+        g.ln_mean = ln.mean;
+        g.ln_rstd = ln.rstd;
+    } else if (epi == EPI_GELU_BWD) {
+        // the LayerNorm-backward partials of the next product (bpart [M][gemm_rowstat_parts][2])
+        if (out_f32 || !aux || !ln.bpart || !ln.lnb_s || !ln.lnb_c) return EBC_E_ARG;
+        g.bpart = ln.bpart;
+        g.lnb_s = ln.lnb_s;
+        g.lnb_c = ln.lnb_c;
+    } else if (epi == EPI_LN_BWD) {
+        if (!out_f32 || !resid || !ln.xh || !ln.lnx || !ln.lnp || ln.lnparts <= 0 || ln.lnparts > LN_PMAX_B ||
+            ln.lnparts % 2 || !ln.mean || !ln.rstd || bias)
+            return EBC_E_ARG;
+        g.xh = ln.xh;
+        g.lnx = ln.lnx;
+        g.lnp = ln.lnp;
+        g.lnparts = ln.lnparts;
         g.ln_mean = ln.mean;
         g.ln_rstd = ln.rstd;
     } else {

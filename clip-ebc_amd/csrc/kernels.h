@@ -35,9 +35,20 @@ struct GemmLn {
     const float* vrep = nullptr;
     long vrep_bs = 0;
     int vrep_L = 0, vrep_nv = 0;
+    // LayerNorm backward folded into the encoder's dX products (r05).  GELU_BWD with bpart: per row and (tile column,
+    // wave column) the partial sums  sum_k dA_k s_k  and  sum_k dA_k (A_k - c_k)  over the product's columns, s = W'.1
+    // and c = b + W beta of the folded forward product (lnb_s, lnb_c): with g = dX_ln (.) gamma these are sum_j g_j and
+    // sum_j g_j xhat_j of the LayerNorm the forward folded, read in A's space (A = xhat W'^T + c).  EPI_LN_BWD: the next
+    // dX product, B = (W')^T, so acc = g; out = rstd (g - sum g / N - xhat sum(g xhat) / N) + resid (f32, xhat from lnx
+    // and the row's mean / rstd), also written to xh in the compute dtype -- the LayerNorm backward without its launch.
+    const float* lnb_s = nullptr;
+    const float* lnb_c = nullptr;
+    float* bpart = nullptr;
+    const float* lnx = nullptr;
 };
-constexpr int GEMM_EPI_LN = 6, GEMM_EPI_LN_GELU = 7;
+constexpr int GEMM_EPI_LN = 6, GEMM_EPI_LN_GELU = 7, GEMM_EPI_LN_BWD = 8;
 constexpr int GEMM_LN_PMAX = 16;   // most row partials an EPI_LN product reads (gemm_rowstat_parts of its producer)
+constexpr int GEMM_LN_PMAX_B = 32; // ... and an EPI_LN_BWD product (the GELU' product's: 3072 / 192 x 2)
 int gemm_nt_ln(int dtype, int epi, int out_f32, const void* A, const void* B, void* C, const float* bias,
                const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws, size_t ws_bytes,
                const GemmLn& ln);

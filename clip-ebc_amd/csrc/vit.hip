@@ -52,6 +52,8 @@ struct Layout {
     void *dXt, *dH, *dA, *dO, *dQKV;
     float* rpart;                   // LayerNorm folding: [M][parts][2] row partials (sum, sum of squares) of X1 / X_l+1
     int parts_out, parts_proj;      //   written by the out-proj / c_proj residual products (gemm_rowstat_parts)
+    float* bpart;                   // LayerNorm-backward folding: [M][parts_gelu][2] partials of the GELU' products
+    int parts_gelu;
     void* gws;                      // split-K GEMM workspace (leading counter block zeroed per call)
     size_t gws_bytes;
     size_t bytes;
@@ -104,6 +106,12 @@ Layout carve(void* ws, int B, int L, int G, int layers, int dtype, int training)
         lay.vpt_rows = nullptr;
         lay.dXa = lay.dXb = lay.delta = nullptr;
         lay.dXt = lay.dH = lay.dA = lay.dO = lay.dQKV = nullptr;
+    }
+    lay.bpart = nullptr;
+    lay.parts_gelu = 0;
+    if (dtype != EBC_F32 && training) {
+        lay.parts_gelu = ebc::gemm_rowstat_parts(dtype, (int)M, MLP, WIDTH);
+        if (lay.parts_gelu <= ebc::GEMM_LN_PMAX_B) lay.bpart = c.take<float>(M * lay.parts_gelu * 2 * 4);
     }
     if (dtype != EBC_F32) {
         lay.parts_out = ebc::gemm_rowstat_parts(dtype, (int)M, WIDTH, WIDTH);
@@ -282,6 +290,17 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
     auto gemm = [&](int epi, const void* A, const void* Bm, void* C, void* aux, int m, int n, int k) {
         return ebc::gemm_nt(dtype, epi, 0, A, Bm, C, nullptr, nullptr, aux, m, n, k, st, lay.gws, lay.gws_bytes);
     };
+    // ln_2's backward folded into the c_fc dX product (16-bit, every layer carrying (W_fc')^T): the GELU' product also
+    // writes, per row, the partial sums sum_k dA_k s_k and sum_k dA_k (A_k - c_k) over its columns (s = W_fc'.1, c = the
+    // folded c_fc bias; A = the saved pre-activation = xhat W_fc'^T + c): these are sum_j g_j and sum_j g_j xhat_j of
+    // ln_2's backward, g = dLN2 (.) gamma_2.  The c_fc dX product then multiplies by (W_fc')^T, so its accumulator IS g,
+    // and finishes dX1 = dX + rstd (g - mean(g) - xhat mean(g xhat)) in its epilogue (gemm.hip EPI_LN_BWD): no dH write
+    // and re-read, no LayerNorm launch.
+    bool fold_b = dtype != EBC_F32 && lay.bpart && !(flags & EBC_VIT_BWD_NO_LN_FOLD);
+    for (int l = 0; l < layers && fold_b; ++l) {
+        const EbcVitLayer& p = w->layer[l];
+        fold_b = p.wt_fc_ln && p.s_fc_ln && p.b_fc_ln;
+    }
     // block l's attention backward reads onto the die the transposed weights of the dX products after it: its QKV dX
     // and block l-1's c_proj / c_fc / out-proj ones (see ebc_vit_forward)
     const size_t es = dtype == EBC_F32 ? 4 : 2;
@@ -291,7 +310,7 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         if (l > 0) {
             const EbcVitLayer& q = w->layer[l - 1];
             t.add(q.wt_proj, (size_t)MLP * WIDTH * es);
-            t.add(q.wt_fc, (size_t)WIDTH * MLP * es);
+            t.add(fold_b ? q.wt_fc_ln : q.wt_fc, (size_t)WIDTH * MLP * es);
             t.add(q.wt_out, (size_t)WIDTH * WIDTH * es);
         }
         return t;
@@ -304,9 +323,20 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         LayerSave& s = lay.s[l];
         const ebc::TouchList tl = touch_bwd(l);
         // MLP half: dA = (dX . W_proj) * QuickGELU'(A);  dH2 = dA . W_fc;  dX1 = dX + LN2'(dH2)
-        EBC_TRY(gemm(EBC_EPI_GELU_BWD, lay.dXt, p.wt_proj, lay.dA, s.A, M, MLP, WIDTH));
-        EBC_TRY(gemm(EBC_EPI_STORE, lay.dA, p.wt_fc, lay.dH, nullptr, M, WIDTH, MLP));
-        EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, s.X1, 0, 0, 0, s.m2, s.r2, p.ln2_g, dX, dXo, lay.dXt, M, WIDTH, st));
+        if (fold_b) {
+            ebc::GemmLn gb;
+            gb.bpart = lay.bpart; gb.lnb_s = p.s_fc_ln; gb.lnb_c = p.b_fc_ln;
+            EBC_TRY(ebc::gemm_nt_ln(dtype, EBC_EPI_GELU_BWD, 0, lay.dXt, p.wt_proj, lay.dA, nullptr, nullptr, s.A, M, MLP,
+                                    WIDTH, st, lay.gws, lay.gws_bytes, gb));
+            ebc::GemmLn lb;
+            lb.xh = lay.dXt; lb.lnx = s.X1; lb.lnp = lay.bpart; lb.lnparts = lay.parts_gelu; lb.mean = s.m2; lb.rstd = s.r2;
+            EBC_TRY(ebc::gemm_nt_ln(dtype, ebc::GEMM_EPI_LN_BWD, 1, lay.dA, p.wt_fc_ln, dXo, nullptr, dX, nullptr, M, WIDTH,
+                                    MLP, st, lay.gws, lay.gws_bytes, lb));
+        } else {
+            EBC_TRY(gemm(EBC_EPI_GELU_BWD, lay.dXt, p.wt_proj, lay.dA, s.A, M, MLP, WIDTH));
+            EBC_TRY(gemm(EBC_EPI_STORE, lay.dA, p.wt_fc, lay.dH, nullptr, M, WIDTH, MLP));
+            EBC_TRY(ebc::layernorm_bwd(dtype, 0, lay.dH, s.X1, 0, 0, 0, s.m2, s.r2, p.ln2_g, dX, dXo, lay.dXt, M, WIDTH, st));
+        }
         { float* t = dX; dX = dXo; dXo = t; }
         // attention half: dO = dX1 . W_out;  dQKV = attn'(...);  dH = dQKV . W_qkv;  dX = dX1 + LN1'(dH)
         EBC_TRY(gemm(EBC_EPI_STORE, lay.dXt, p.wt_out, lay.dO, nullptr, M, WIDTH, WIDTH));

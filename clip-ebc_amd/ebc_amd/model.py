@@ -109,7 +109,8 @@ _VP = ctypes.c_void_p
 class EbcVitLayer(ctypes.Structure):
     _fields_ = [(n, _VP) for n in ("w_qkv", "b_qkv", "w_out", "b_out", "w_fc", "b_fc", "w_proj", "b_proj",
                                    "ln1_g", "ln1_b", "ln2_g", "ln2_b", "wt_qkv", "wt_out", "wt_fc", "wt_proj",
-                                   "w_qkv_ln", "b_qkv_ln", "s_qkv_ln", "w_fc_ln", "b_fc_ln", "s_fc_ln")]
+                                   "w_qkv_ln", "b_qkv_ln", "s_qkv_ln", "w_fc_ln", "b_fc_ln", "s_fc_ln",
+                                   "wt_qkv_ln", "wt_fc_ln")]
 
 
 class EbcVitWeights(ctypes.Structure):
@@ -161,6 +162,9 @@ class _EncoderCache:
                     w64 = w.detach().to(device, torch.float64)
                     wf = cvt(w64 * ln.weight.detach().to(device, torch.float64)[None, :])
                     setattr(L, f"w_{pre}_ln", _p(wf))
+                    if pre == "fc":
+                        # (W')^T for the backward's dX product: its epilogue then finishes ln_2's backward (vit.hip)
+                        L.wt_fc_ln = _p(cvt(wf.t()))
                     setattr(L, f"s_{pre}_ln", _p(cvt(wf.double().sum(1), torch.float32)))
                     setattr(L, f"b_{pre}_ln", _p(cvt(bias.detach().to(device, torch.float64)
                                                      + w64 @ ln.bias.detach().to(device, torch.float64), torch.float32)))

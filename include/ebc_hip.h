@@ -142,6 +142,10 @@ typedef struct {
      * epilogues from row statistics the previous residual product writes */
     const void* w_qkv_ln; const float* b_qkv_ln; const float* s_qkv_ln;
     const void* w_fc_ln;  const float* b_fc_ln;  const float* s_fc_ln;
+    /* optional (16-bit, with the fold above; null: LayerNorm-backward launches): the transposes of the folded weights,
+     * (W')^T [768, out], so the dX products after the GELU' / attention backward produce g = dX_ln (.) gamma and finish
+     * the LayerNorm backward in their epilogues (row sums from the GELU' product's partials, vit.hip) */
+    const void* wt_qkv_ln; const void* wt_fc_ln;
 } EbcVitLayer;
 
 typedef struct {
@@ -165,8 +169,9 @@ int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B, int H, in
 /* dfeat [B, G, 768] f32 -> dvpt[l] ([num_vpt,768] f32, summed over crops; per crop if vpt_bstride).
  * Layer 0's backward stops at its prompt rows (the frozen embedding below takes no gradient: dQ/dK/dV of the first
  * query/key block, dH and ln_1' of the prompt rows only); flags & EBC_VIT_BWD_FULL_LAYER0 runs it over every row
- * instead, which must give bit-identical prompt gradients (a parity hook for tests/test_gpu_model.py). */
-enum { EBC_VIT_BWD_FULL_LAYER0 = 1 };
+ * instead, which must give bit-identical prompt gradients (a parity hook for tests/test_gpu_model.py).
+ * flags & EBC_VIT_BWD_NO_LN_FOLD runs ln_2's backward as a LayerNorm launch even when wt_fc_ln is set (A/B, tests). */
+enum { EBC_VIT_BWD_FULL_LAYER0 = 1, EBC_VIT_BWD_NO_LN_FOLD = 2 };
 int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int dtype, void* workspace,
                      size_t workspace_bytes, const float* dfeat, float* const* dvpt, long vpt_bstride, int flags,
                      ebc_stream_t stream);
@@ -398,6 +403,10 @@ int ebc_amp_check(const EbcAdamTensor* tensors, int n, float* scaler, int scaler
 int ebc_adam_update(const EbcAdamTensor* tensors, int n, float* step, int step_parity, float* scaler, int scaler_parity,
                     double lr, double beta1, double beta2, double eps, double weight_decay, double growth_factor,
                     double backoff_factor, int growth_interval, int write_unscaled_grad, ebc_stream_t stream);
+
+/* Weight touch (performance only; the results do not change): the encoder's attention launches read onto the die the
+ * frozen weights of the GEMMs after them (attention.hip touch_issue).  mode 1 (default): on; 0: off (A/B, tests). */
+int ebc_set_weight_touch(int mode);
 
 /* ------------------------------------------------------------------------------------------
  * Measurement (bench.py): in-step kernel durations and profile windows.  Not on the reference's
