@@ -611,6 +611,25 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             // (all of them within the first half of the MFMAs, two per MFMA)
             constexpr int NRD = (TM + TN) * (EB == 2 ? 1 : 2), NG = (NRD + 1) / 2;
             static_assert(NG <= TM * TN, "read/MFMA interleave");
+            // (r05: 256x192 MODE 0 step 3692 -> 3710 crops/s same box, profiles/r05g_glds_interleave_ab.txt)
+            constexpr int NV = NLW == 0 && NLD + NG <= TM * TN ? NLD : 0;
+            if (!tail && kk + 1 == KS && NV > 0) {
+                // tile boundary: the next tile's LDS-DMA pieces (stage above) spread over this step's MFMAs instead of
+                // issued as one burst right after the barrier (both waves of a SIMD then stop issuing MFMAs at once)
+                // (the fragment reads of the next buffer stay behind every piece: the compiler orders LDS-DMA writes
+                // before later LDS reads)
+                static_for<0, NV>([&](auto) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);             // VMEM (LDS-DMA piece)
+                });
+                static_for<0, NG>([&](auto) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);             // DS reads
+                });
+                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - NG - NV, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                return;
+            }
             static_for<0, NG>([&](auto) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);                 // DS reads
