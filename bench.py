@@ -115,8 +115,13 @@ def make_batch(B, rank, step, device, size=224):
     """BASELINE.md synthetic crops: seed 1000 + rank*100003 + step, lognormal(ln 20, 1.2) points."""
     from ebc_amd import synthetic as syn
     img, pts, dens = syn.synthetic_crops(B, size, seed=1000 + rank * 100003 + step)
-    return (torch.from_numpy(img).to(device), [torch.from_numpy(p).to(device) for p in pts],
-            torch.from_numpy(dens).to(device), [len(p) for p in pts])
+    # the crops' labels uploaded in one copy, as views of one [sum n, 2] buffer (the loss then needs no concatenation)
+    packed = torch.from_numpy(np.concatenate([p.reshape(-1, 2) for p in pts], 0).astype(np.float32)).to(device)
+    views, o = [], 0
+    for p in pts:
+        views.append(packed[o:o + len(p)])
+        o += len(p)
+    return (torch.from_numpy(img).to(device), views, torch.from_numpy(dens).to(device), [len(p) for p in pts])
 
 
 def host_cores():

@@ -21,6 +21,7 @@
 //    (bregman_pytorch.py:117-126), stop when err <= stopThr or it > maxIter, NaN/Inf rollback
 //    to the previous (u, v) and break (:111-115), the 1e-16 epsilons, denormals kept (the build
 //    never flushes f32 denormals).  The err pass's K^T u is reused by the next iteration.
+#include <algorithm>
 #include <type_traits>
 
 #include "ebc_common.h"
@@ -72,6 +73,7 @@ __device__ __forceinline__ int row_base(int lo, int len) {
     else return len ? min(lo & ~3, G - CW) : 0;
 }
 
+constexpr int HMETA_MAX = 64;
 struct Params {
     const float* pred_class; const float* pred_density; const float* target_density;
     int target_is_reduced;
@@ -87,6 +89,9 @@ struct Params {
     int lds_cap_s;         // max points kept in LDS with full factor rows (bucketed path)
     int lds_cap_c;         // max points kept in LDS with compact factor rows (bucketed path)
     int total_points;      // sum of n over the crops (probe records only)
+    // ebc_dace_loss_h: the crop offsets / order as kernel arguments (B <= HMETA_MAX): no host-to-device copy
+    int hmeta;
+    int hoff[HMETA_MAX + 1], hord[HMETA_MAX];
 };
 
 // ---------------------------------------------------------------------------------------
@@ -719,7 +724,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     float* fac = part + C::KSPLIT * GG;                       // LDS factors, full rows (if they fit)
     float* facc = part + GG;                                  // LDS factors, compact rows (bucketed path)
 
-    const int p0 = P.offsets[b], n = P.offsets[b + 1] - p0;
+    const int p0 = P.hmeta ? P.hoff[b] : P.offsets[b], n = (P.hmeta ? P.hoff[b + 1] : P.offsets[b + 1]) - p0;
 
     // 1. pred density, target block sums (losses/utils.py:4-9)
     for (int j = t; j < GG; j += NT) { pd[j] = live(j) ? P.pred_density[(size_t)b * gg + gidx(j)] : 0.f; td[j] = 0.f; }
@@ -885,7 +890,7 @@ template <int G>
 __global__ __launch_bounds__(NT) void dace_loss_kernel(Params P)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = P.order ? P.order[blockIdx.x] : (int)blockIdx.x;
+    const int b = P.hmeta ? P.hord[blockIdx.x] : P.order ? P.order[blockIdx.x] : (int)blockIdx.x;
     crop_body<G>(P, b, lds);
 }
 
@@ -949,14 +954,15 @@ extern "C" size_t ebc_dace_workspace_bytes(int B, int total_points, int size, in
     return sizeof(float) * ((size_t)(2 * (G ? G : 64) + 6) * (size_t)(total_points > 0 ? total_points : 1)) + 256;
 }
 
-extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,
-                             int target_is_reduced, const float* points, const int* offsets, const int* order,
-                             const float* bins_lo, const float* bins_hi, int B, int N, int size, int reduction,
-                             int count_mode, int norm_cood, float weight_count_loss, float weight_ot, float weight_tv,
-                             float reg, int max_iter, float stop_thr, int eval_freq,
-                             float* grad_class, float* grad_density, float* losses, float* crop_stats,
-                             float* beta_out, int* status, void* workspace, size_t workspace_bytes,
-                             ebc_stream_t stream)
+namespace {
+int dace_loss_impl(const float* pred_class, const float* pred_density, const float* target_density,
+                   int target_is_reduced, const float* points, const int* offsets, const int* order, bool host_meta,
+                   const float* bins_lo, const float* bins_hi, int B, int N, int size, int reduction,
+                   int count_mode, int norm_cood, float weight_count_loss, float weight_ot, float weight_tv,
+                   float reg, int max_iter, float stop_thr, int eval_freq,
+                   float* grad_class, float* grad_density, float* losses, float* crop_stats,
+                   float* beta_out, int* status, void* workspace, size_t workspace_bytes,
+                   ebc_stream_t stream)
 {
     if (B <= 0 || N <= 0 || reduction <= 0 || size % reduction != 0 || eval_freq <= 0 || reg <= 0.f)
         return EBC_E_ARG;
@@ -970,7 +976,18 @@ extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density,
     hipStream_t st = (hipStream_t)stream;
     Params P{};
     P.pred_class = pred_class; P.pred_density = pred_density; P.target_density = target_density;
-    P.target_is_reduced = target_is_reduced; P.points = points; P.offsets = offsets; P.order = order;
+    P.target_is_reduced = target_is_reduced; P.points = points;
+    if (host_meta) {
+        if (B > HMETA_MAX) return EBC_E_UNSUPPORTED;
+        P.hmeta = 1;
+        for (int i = 0; i <= B; ++i) P.hoff[i] = offsets[i];
+        for (int i = 0; i < B; ++i) {
+            if (order && (order[i] < 0 || order[i] >= B)) return EBC_E_ARG;
+            P.hord[i] = order ? order[i] : i;
+        }
+    } else {
+        P.offsets = offsets; P.order = order;
+    }
     P.bins_lo = bins_lo; P.bins_hi = bins_hi; P.B = B; P.N = N; P.size = size; P.red = reduction;
     P.count_mode = count_mode; P.norm_cood = norm_cood; P.w_count = weight_count_loss; P.w_ot = weight_ot; P.w_tv = weight_tv;
     P.reg = reg; P.stop_thr = stop_thr; P.max_iter = max_iter; P.eval_freq = eval_freq;
@@ -995,6 +1012,58 @@ extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density,
     if (rc) return rc;
     hipLaunchKernelGGL(dace_finalize_kernel, dim3(1), dim3(256), 0, st, crop_stats, B, count_mode,
                        weight_count_loss, weight_ot, weight_tv, losses);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+}  // namespace
+
+extern "C" int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,
+                             int target_is_reduced, const float* points, const int* offsets, const int* order,
+                             const float* bins_lo, const float* bins_hi, int B, int N, int size, int reduction,
+                             int count_mode, int norm_cood, float weight_count_loss, float weight_ot, float weight_tv,
+                             float reg, int max_iter, float stop_thr, int eval_freq,
+                             float* grad_class, float* grad_density, float* losses, float* crop_stats,
+                             float* beta_out, int* status, void* workspace, size_t workspace_bytes,
+                             ebc_stream_t stream)
+{
+    return dace_loss_impl(pred_class, pred_density, target_density, target_is_reduced, points, offsets, order, false,
+                          bins_lo, bins_hi, B, N, size, reduction, count_mode, norm_cood, weight_count_loss, weight_ot,
+                          weight_tv, reg, max_iter, stop_thr, eval_freq, grad_class, grad_density, losses, crop_stats,
+                          beta_out, status, workspace, workspace_bytes, stream);
+}
+extern "C" int ebc_dace_loss_h(const float* pred_class, const float* pred_density, const float* target_density,
+                               int target_is_reduced, const float* points, const int* offsets_host,
+                               const int* order_host, const float* bins_lo, const float* bins_hi, int B, int N, int size,
+                               int reduction, int count_mode, int norm_cood, float weight_count_loss, float weight_ot,
+                               float weight_tv, float reg, int max_iter, float stop_thr, int eval_freq,
+                               float* grad_class, float* grad_density, float* losses, float* crop_stats,
+                               float* beta_out, int* status, void* workspace, size_t workspace_bytes,
+                               ebc_stream_t stream)
+{
+    return dace_loss_impl(pred_class, pred_density, target_density, target_is_reduced, points, offsets_host,
+                          order_host, true, bins_lo, bins_hi, B, N, size, reduction, count_mode, norm_cood,
+                          weight_count_loss, weight_ot, weight_tv, reg, max_iter, stop_thr, eval_freq, grad_class,
+                          grad_density, losses, crop_stats, beta_out, status, workspace, workspace_bytes, stream);
+}
+
+// The loss's backward (_DaceFn): both kernel-made gradients times the upstream scalar (GradScaler's scale) in one
+// launch, out of place (a retained graph may run the backward again)
+__global__ __launch_bounds__(256) void scale2_kernel(const float* __restrict__ s, const float* __restrict__ a, float* ao,
+                                                     long na, const float* __restrict__ b, float* bo, long nb)
+{
+    const float f = *s;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < na + nb; i += (long)gridDim.x * 256) {
+        if (i < na) ao[i] = a[i] * f;
+        else bo[i - na] = b[i - na] * f;
+    }
+}
+extern "C" int ebc_scale2(const float* s, const float* a, float* a_out, long na, const float* b, float* b_out, long nb,
+                          ebc_stream_t stream)
+{
+    if (!s || na < 0 || nb < 0 || (na && (!a || !a_out)) || (nb && (!b || !b_out))) return EBC_E_ARG;
+    if (na + nb == 0) return EBC_OK;
+    const long blocks = std::min<long>((na + nb + 255) / 256, 1024);
+    hipLaunchKernelGGL(scale2_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, s, a, a_out, na, b, b_out, nb);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }

@@ -230,10 +230,12 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __re
                                                               const double* __restrict__ count_dev, float eps,
                                                               float momentum, const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* mean, float* rstd,
-                                                              float* scale, float* shift, float* rmean, float* rvar, int C)
+                                                              float* scale, float* shift, float* rmean, float* rvar, int C,
+                                                              long long* nbt)
 {
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= C) return;
+    if (nbt && c == 0) *nbt += 1;                 // BatchNorm2d.num_batches_tracked (no torch launch for it)
     double m, var;
     if (count_dev) count = *count_dev;
     if (sums) {
@@ -286,13 +288,15 @@ __global__ __launch_bounds__(1024) void reduce_fwd_finalize_kernel(const float* 
                                                                    const float* __restrict__ gamma,
                                                                    const float* __restrict__ beta, float* mean,
                                                                    float* rstd, float* scale, float* shift,
-                                                                   float* rmean, float* rvar, double* colsum_out)
+                                                                   float* rmean, float* rvar, double* colsum_out,
+                                                                   long long* nbt)
 {
     __shared__ double red[2][16][64];
     double S, Q;
     reduce_pair(part, nb, C, red, S, Q);
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
     if (threadIdx.x >= 64 || c >= C) return;
+    if (nbt && c == 0) *nbt += 1;                 // BatchNorm2d.num_batches_tracked
     if (colsum_out) { colsum_out[c] = S; colsum_out[C + c] = Q; }
     const double m = S / count;
     double var = Q / count - m * m;
@@ -832,7 +836,7 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 inline int bn_partial_rows(int C) { return 8 * std::max(1, 512 / std::max(1, C / 8)); }
 
 // optional fused finalize (reduce_fwd_finalize_kernel / reduce_bwd_finalize_kernel) instead of reduce_partials
-struct FwdFin { float eps, momentum; const float *gamma, *beta; float *mean, *rstd, *scale, *shift, *rmean, *rvar; };
+struct FwdFin { float eps, momentum; const float *gamma, *beta; float *mean, *rstd, *scale, *shift, *rmean, *rvar; long long* nbt; };
 struct BwdFin { const float* gamma; float *dgamma, *dbeta, *coef; };
 
 template <class T>
@@ -883,7 +887,7 @@ int bn_stats_t(const void* z, double* colsum, void* ws, size_t wsb, long P, int 
     if (fin)
         hipLaunchKernelGGL(reduce_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
                            C, (double)P, fin->eps, fin->momentum, fin->gamma, fin->beta, fin->mean, fin->rstd, fin->scale,
-                           fin->shift, fin->rmean, fin->rvar, colsum);
+                           fin->shift, fin->rmean, fin->rvar, colsum, fin->nbt);
     else
         hipLaunchKernelGGL(reduce_partials_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, (const float*)part, (int)nb,
                            2 * C, colsum);
@@ -955,6 +959,31 @@ extern "C" int ebc_conv3x3_fwd(int dtype, const void* xpad, const void* weight, 
     return EBC_OK;
 }
 
+extern "C" int ebc_conv3x3_fwd_bn(int dtype, const void* xpad, const void* weight, void* out, void* ws, size_t wsb,
+                                  int B, int H, int W, int C, int N, float eps, float momentum, const float* gamma,
+                                  const float* beta, float* mean, float* rstd, float* scale, float* shift,
+                                  float* running_mean, float* running_var, long long* num_batches_tracked,
+                                  double* colsum_out, ebc_stream_t stream)
+{
+    if (!xpad || !weight || !out || C % 64 || N % 64 || !gamma || !beta || !mean || !rstd || !scale || !shift)
+        return EBC_E_ARG;
+    if ((running_mean == nullptr) != (running_var == nullptr) || B * H * W <= 1) return EBC_E_ARG;
+    const Geo g = make_geo(dtype, B, H, W, C);
+    ebc::ConvGeom cg{H, W, C, g.Hp, g.Wp, 0, 0, 0, B};
+    const int M = B * H * W;
+    int tiles = 0;
+    const hipStream_t st = (hipStream_t)stream;
+    EBC_TRY(ebc::conv_gemm(dtype, 1, 4, xpad, weight, out, cg, M, N, 9 * C, ws, wsb, &tiles, st, nullptr, nullptr));
+    // the conv epilogue's per-tile column sums -> f64 in reduce_partials' order -> batch statistics, running stats,
+    // scale / shift: one launch (reduce_fwd_finalize_kernel) where ebc_conv3x3_fwd + ebc_bn_finalize take two
+    const float* part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(ws) + CONV_WS_STATS_OFFSET);
+    hipLaunchKernelGGL(reduce_fwd_finalize_kernel, dim3((N + 63) / 64), dim3(1024), 0, st, part, tiles, N, (double)M,
+                       eps, momentum, gamma, beta, mean, rstd, scale, shift, running_mean, running_var, colsum_out,
+                       num_batches_tracked);
+    EBC_CHECK_LAUNCH();
+    return EBC_OK;
+}
+
 extern "C" int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, float* dw, void* ws, size_t wsb, int B,
                                  int H, int W, int C, int N, ebc_stream_t stream)
 {
@@ -966,14 +995,15 @@ extern "C" int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, fl
 
 extern "C" int ebc_bn_finalize(const double* colsum, double count, float eps, float momentum, const float* gamma,
                                const float* beta, float* mean, float* rstd, float* scale, float* shift,
-                               float* running_mean, float* running_var, int C, ebc_stream_t stream)
+                               float* running_mean, float* running_var, long long* num_batches_tracked, int C,
+                               ebc_stream_t stream)
 {
     if (!gamma || !beta || !mean || !rstd || !scale || !shift) return EBC_E_ARG;
     if (!colsum && (!running_mean || !running_var)) return EBC_E_ARG;
     if (colsum && count >= 0.0 && count <= 1.0) return EBC_E_ARG;
     const double* cdev = colsum && count < 0.0 ? colsum + 2 * C : nullptr;     // device count at colsum[2C]
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nblk(C)), dim3(256), 0, (hipStream_t)stream, colsum, count, cdev, eps,
-                       momentum, gamma, beta, mean, rstd, scale, shift, running_mean, running_var, C);
+                       momentum, gamma, beta, mean, rstd, scale, shift, running_mean, running_var, C, num_batches_tracked);
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -1120,11 +1150,11 @@ extern "C" int ebc_bn_stats(int dtype, const void* z, double* colsum, void* ws, 
 extern "C" int ebc_bn_stats_finalize(int dtype, const void* z, void* ws, size_t wsb, long P, int C, float eps,
                                      float momentum, const float* gamma, const float* beta, float* mean, float* rstd,
                                      float* scale, float* shift, float* running_mean, float* running_var,
-                                     double* colsum_out, ebc_stream_t stream)
+                                     double* colsum_out, long long* num_batches_tracked, ebc_stream_t stream)
 {
     if (!z || P <= 1 || C % 8 || !gamma || !beta || !mean || !rstd || !scale || !shift) return EBC_E_ARG;
     if ((running_mean == nullptr) != (running_var == nullptr)) return EBC_E_ARG;
-    const FwdFin fin{eps, momentum, gamma, beta, mean, rstd, scale, shift, running_mean, running_var};
+    const FwdFin fin{eps, momentum, gamma, beta, mean, rstd, scale, shift, running_mean, running_var, num_batches_tracked};
     const hipStream_t st = (hipStream_t)stream;
     switch (dtype) {
         case EBC_F32: return bn_stats_t<float>(z, colsum_out, ws, wsb, P, C, st, &fin);

@@ -64,6 +64,9 @@ class EbcAdamTensor(ctypes.Structure):
 SIGNATURES = {
     "ebc_version": (_I, []),
     "ebc_dace_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "ebc_scale2": (_I, [_P, _P, _P, _L, _P, _P, _L, _P]),
+    "ebc_dace_loss_h": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _I, _F, _I,
+                             _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "ebc_dace_loss": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _I, _F, _I,
                            _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "ebc_sinkhorn_workspace_bytes": (_Z, [_I, _I]),
@@ -95,7 +98,9 @@ SIGNATURES = {
     "ebc_dec_upsample_pad": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ebc_conv3x3_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _P]),
     "ebc_conv3x3_wgrad": (_I, [_I, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _P]),
-    "ebc_bn_finalize": (_I, [_P, _D, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "ebc_bn_finalize": (_I, [_P, _D, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "ebc_conv3x3_fwd_bn": (_I, [_I, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P,
+                                _P, _P, _P]),
     "ebc_bn_relu_pad": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ebc_bn_add_relu": (_I, [_I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P]),
     "ebc_bn_bwd_reduce": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _L, _I, _P]),
@@ -106,7 +111,7 @@ SIGNATURES = {
     "ebc_dec_upsample_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ebc_dec_upsample": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ebc_bn_stats": (_I, [_I, _P, _P, _P, _Z, _L, _I, _P]),
-    "ebc_bn_stats_finalize": (_I, [_I, _P, _P, _Z, _L, _I, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "ebc_bn_stats_finalize": (_I, [_I, _P, _P, _Z, _L, _I, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "ebc_bn_bwd_reduce_finalize": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _L, _I, _P]),
     "ebc_bn_relu": (_I, [_I, _P, _P, _P, _P, _L, _I, _P]),
     "ebc_bn_bwd_apply_flat": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),

@@ -24,6 +24,8 @@ NotImplementedError at construction.
 """
 from __future__ import annotations
 
+import ctypes
+
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -80,8 +82,12 @@ def _run_dace(pred_class, pred_density, target_density, points, offsets, order, 
     with _lib.on(dev):
         ws_bytes = L.ebc_dace_workspace_bytes(B, total, size, red)
         ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
-        rc = L.ebc_dace_loss(_lib.ptr(pc), _lib.ptr(pd, dev), _lib.ptr(td, dev), int(reduced), _lib.ptr(points, dev),
-                             _lib.ptr(offsets, dev), _lib.ptr(order, dev), _lib.ptr(bins_lo, dev), _lib.ptr(bins_hi, dev),
+        # offsets / order: host ctypes arrays (B <= 64: kernel arguments, ebc_dace_loss_h) or device tensors
+        host = not isinstance(offsets, torch.Tensor)
+        fn = L.ebc_dace_loss_h if host else L.ebc_dace_loss
+        rc = fn(_lib.ptr(pc), _lib.ptr(pd, dev), _lib.ptr(td, dev), int(reduced), _lib.ptr(points, dev),
+                             offsets if host else _lib.ptr(offsets, dev), order if host else _lib.ptr(order, dev),
+                             _lib.ptr(bins_lo, dev), _lib.ptr(bins_hi, dev),
                              B, N, size, red, mode, int(norm), wc, wot, wtv, reg, iters, thr, freq,
                              _lib.ptr(grad_c), _lib.ptr(grad_d), _lib.ptr(losses), _lib.ptr(stats),
                              _lib.ptr(beta), _lib.ptr(status), _lib.ptr(ws), ws_bytes, _lib.stream(dev))
@@ -113,15 +119,48 @@ class _DaceFn(torch.autograd.Function):
         if g_loss is None:
             return (None,) * 10
         grad_c, grad_d = ctx.saved_tensors
-        gc, gd = torch._foreach_mul([grad_c, grad_d], g_loss)
+        if g_loss.dtype == torch.float32 and g_loss.numel() == 1 and g_loss.device == grad_c.device:
+            gc, gd = torch.empty_like(grad_c), torch.empty_like(grad_d)
+            with _lib.on(grad_c.device):
+                _lib.check(_lib.lib().ebc_scale2(_lib.ptr(g_loss), _lib.ptr(grad_c), _lib.ptr(gc), grad_c.numel(),
+                                                 _lib.ptr(grad_d), _lib.ptr(gd), grad_d.numel(), _lib.stream(grad_c.device)),
+                           "ebc_scale2")
+        else:
+            gc, gd = torch._foreach_mul([grad_c, grad_d], g_loss)
         return (gc.to(ctx.dtypes[0]), gd.to(ctx.dtypes[1]), None, None, None, None, None, None, None, None)
 
 
-def _pack_points(target_points: Sequence[Tensor], device) -> Tuple[Tensor, Tensor, Tensor, int]:
-    """The ragged label list -> packed [sum n, 2] f32 + offsets [B+1] + heaviest-first crop order (one H2D)."""
+def _packed_views(target_points: Sequence[Tensor], device) -> bool:
+    """True when the point lists are row-contiguous f32 [n_i, 2] views laid end to end in one device storage."""
+    p0 = target_points[0]
+    if p0.device != torch.device(device):
+        return False
+    store = p0.untyped_storage().data_ptr()
+    nxt = store + p0.storage_offset() * 4                 # (an empty view's data_ptr() is 0: use the offsets)
+    for p in target_points:
+        if (p.dtype != torch.float32 or p.dim() != 2 or p.shape[1] != 2 or p.device != p0.device
+                or (p.shape[0] > 1 and p.stride() != (2, 1)) or (p.shape[0] == 1 and p.stride(1) != 1)
+                or p.untyped_storage().data_ptr() != store or (p.shape[0] and p.data_ptr() != nxt)):
+            return False
+        nxt += p.shape[0] * 8
+    return True
+
+
+HMETA_MAX = 64          # dace_loss.hip: up to this many crops the offsets / order travel as kernel arguments
+
+
+def _pack_points(target_points: Sequence[Tensor], device):
+    """The ragged label list -> packed [sum n, 2] f32 + offsets [B+1] + heaviest-first crop order: host ctypes arrays
+    for up to HMETA_MAX crops (passed as kernel arguments, no copy), else one H2D of both."""
     counts = [int(p.shape[0]) for p in target_points]
     total = sum(counts)
-    if total:
+    if total and _packed_views(target_points, device):
+        # the crops' point lists are consecutive rows of one [sum n, 2] f32 device buffer (a collate that uploads the
+        # batch's labels in one copy): use it as is, no concatenation launch
+        p0 = target_points[0]
+        pts = torch.empty(0, device=device, dtype=torch.float32).set_(p0.untyped_storage(), p0.storage_offset(),
+                                                                      (total, 2), (2, 1))
+    elif total:
         pts = torch.cat([p.reshape(-1, 2).to(device=device, dtype=torch.float32) for p in target_points], 0).contiguous()
     else:
         pts = torch.zeros(1, 2, device=device, dtype=torch.float32)
@@ -129,6 +168,8 @@ def _pack_points(target_points: Sequence[Tensor], device) -> Tuple[Tensor, Tenso
     for c in counts:
         offs.append(offs[-1] + c)
     order = sorted(range(len(counts)), key=lambda i: -counts[i])        # heaviest crops first
+    if len(counts) <= HMETA_MAX:
+        return pts, (ctypes.c_int * len(offs))(*offs), (ctypes.c_int * len(order))(*order), total
     meta = torch.tensor(offs + order, dtype=torch.int32)
     if torch.cuda.is_available():
         meta = meta.pin_memory()

@@ -427,8 +427,10 @@ class _DecoderFn(torch.autograd.Function):
             # count read on device (count = -1), so ranks may hold different batch sizes (torch.nn.SyncBatchNorm
             # gathers the per-rank counts the same way)
             colsum = torch.empty(2 * N + (pg is not None), device=dev, dtype=torch.float64) if use_batch else None
-            _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(inp), _lib.ptr(wk), _lib.ptr(z), _lib.ptr(colsum), None, None,
-                                         _lib.ptr(ws), ws.numel(), B, H, W, C, N, st), "ebc_conv3x3_fwd")
+            fused_bn = use_batch and pg is None and training and bn.track_running_stats and bn.momentum is not None
+            if not fused_bn:
+                _lib.check(L.ebc_conv3x3_fwd(dt, _lib.ptr(inp), _lib.ptr(wk), _lib.ptr(z), _lib.ptr(colsum), None, None,
+                                             _lib.ptr(ws), ws.numel(), B, H, W, C, N, st), "ebc_conv3x3_fwd")
             count = float(P)
             if pg is not None:
                 colsum[2 * N].fill_(float(P))
@@ -436,18 +438,26 @@ class _DecoderFn(torch.autograd.Function):
                 count = -1.0
             mean, rstd, scale, shift = (torch.empty(N, **f32) for _ in range(4))
             upd = use_batch and training and bn.track_running_stats
+            nbt = None                             # num_batches_tracked += 1 inside the finalize launch
             if upd:
                 if bn.momentum is None:            # cumulative average: the factor needs the updated count now
                     bn.num_batches_tracked.add_(1)
                 else:
-                    from .resnet import _PENDING_NBT
-                    _PENDING_NBT.append(bn.num_batches_tracked)
+                    nbt = _lib.ptr(bn.num_batches_tracked)
             mom = _bn_momentum(bn) if upd else 0.0
-            _lib.check(L.ebc_bn_finalize(_lib.ptr(colsum), count, float(bn.eps), mom, _lib.ptr(gm.detach()),
-                                         _lib.ptr(bt.detach()), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale),
-                                         _lib.ptr(shift), _lib.ptr(bn.running_mean) if (upd or not use_batch) else None,
-                                         _lib.ptr(bn.running_var) if (upd or not use_batch) else None, N, st),
-                       "ebc_bn_finalize")
+            if fused_bn:
+                # no SyncBatchNorm exchange: the conv, then its column sums reduced and finalized in one launch
+                _lib.check(L.ebc_conv3x3_fwd_bn(dt, _lib.ptr(inp), _lib.ptr(wk), _lib.ptr(z), _lib.ptr(ws), ws.numel(),
+                                                B, H, W, C, N, float(bn.eps), mom, _lib.ptr(gm.detach()),
+                                                _lib.ptr(bt.detach()), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale),
+                                                _lib.ptr(shift), _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var),
+                                                nbt, _lib.ptr(colsum), st), "ebc_conv3x3_fwd_bn")
+            else:
+                _lib.check(L.ebc_bn_finalize(_lib.ptr(colsum), count, float(bn.eps), mom, _lib.ptr(gm.detach()),
+                                             _lib.ptr(bt.detach()), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(scale),
+                                             _lib.ptr(shift), _lib.ptr(bn.running_mean) if (upd or not use_batch) else None,
+                                             _lib.ptr(bn.running_var) if (upd or not use_batch) else None, nbt, N, st),
+                           "ebc_bn_finalize")
             outs.append((z, mean, rstd, scale, shift, count, pg, colsum))
             if i == 0:
                 hpad = torch.empty(Q, N, device=dev, dtype=cdtype)

@@ -150,11 +150,12 @@ def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, 
         count = -1.0
     mean, rstd, scale, shift = (torch.empty(N, **f32) for _ in range(4))
     upd = use_batch and training and bn.track_running_stats
+    nbt = None                                     # num_batches_tracked += 1 inside the finalize launch
     if upd:
         if bn.momentum is None:                    # cumulative average: the factor needs the updated count now
             bn.num_batches_tracked.add_(1)
         else:
-            _PENDING_NBT.append(bn.num_batches_tracked)
+            nbt = _lib.ptr(bn.num_batches_tracked)
     mom = _bn_momentum(bn) if upd else 0.0
     if fused:
         dt, z, ws = src
@@ -162,13 +163,13 @@ def _batch_norm_fwd(L, bn: nn.Module, colsum: Optional[Tensor], P: int, N: int, 
                                            _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()), _lib.ptr(mean),
                                            _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),
                                            _lib.ptr(bn.running_mean) if upd else None,
-                                           _lib.ptr(bn.running_var) if upd else None, None, st), "ebc_bn_stats_finalize")
+                                           _lib.ptr(bn.running_var) if upd else None, None, nbt, st), "ebc_bn_stats_finalize")
         return mean, rstd, scale, shift, count, pg, colsum
     _lib.check(L.ebc_bn_finalize(_lib.ptr(colsum) if use_batch else None, count, float(bn.eps), mom,
                                  _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()), _lib.ptr(mean),
                                  _lib.ptr(rstd), _lib.ptr(scale), _lib.ptr(shift),
                                  _lib.ptr(bn.running_mean) if (upd or not use_batch) else None,
-                                 _lib.ptr(bn.running_var) if (upd or not use_batch) else None, N, st),
+                                 _lib.ptr(bn.running_var) if (upd or not use_batch) else None, nbt, N, st),
                "ebc_bn_finalize")
     return mean, rstd, scale, shift, count, pg, colsum
 

@@ -62,6 +62,10 @@ int ebc_version(void);
  * workspace: ebc_dace_workspace_bytes(...) bytes of device memory.
  */
 size_t ebc_dace_workspace_bytes(int B, int total_points, int size, int reduction);
+/* a_out[i] = a[i] * *s, b_out[i] = b[i] * *s (s a device scalar): the loss gradients times the upstream gradient of the
+ * loss (GradScaler's scale) in one launch */
+int ebc_scale2(const float* s, const float* a, float* a_out, long na, const float* b, float* b_out, long nb,
+               ebc_stream_t stream);
 int ebc_dace_loss(const float* pred_class, const float* pred_density, const float* target_density,
                   int target_is_reduced, const float* points, const int* offsets, const int* order,
                   const float* bins_lo, const float* bins_hi, int B, int N, int size, int reduction,
@@ -70,6 +74,16 @@ int ebc_dace_loss(const float* pred_class, const float* pred_density, const floa
                   float* grad_class, float* grad_density, float* losses, float* crop_stats,
                   float* beta_out, int* status, void* workspace, size_t workspace_bytes,
                   ebc_stream_t stream);
+/* The same with the crop offsets [B+1] and order [B] in HOST memory (B <= 64): passed to the kernel as launch
+ * arguments, so the label metadata needs no host-to-device copy. */
+int ebc_dace_loss_h(const float* pred_class, const float* pred_density, const float* target_density,
+                    int target_is_reduced, const float* points, const int* offsets_host, const int* order_host,
+                    const float* bins_lo, const float* bins_hi, int B, int N, int size, int reduction,
+                    int count_mode, int norm_cood, float weight_count_loss, float weight_ot, float weight_tv,
+                    float reg, int max_iter, float stop_thr, int eval_freq,
+                    float* grad_class, float* grad_density, float* losses, float* crop_stats,
+                    float* beta_out, int* status, void* workspace, size_t workspace_bytes,
+                    ebc_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * General dense Sinkhorn-Knopp, one problem: replaces sinkhorn(a, b, C, reg, maxIter, stopThr, verbose,
@@ -298,10 +312,17 @@ int ebc_conv3x3_wgrad(int dtype, const void* dzT, const void* xT3, float* dw, vo
  * updated (momentum, unbiased variance) when colsum != NULL, read (eval) when colsum == NULL.
  * count < 0: the element count is the DEVICE value colsum[2*C] (SyncBatchNorm: each rank stores its own
  * count there and all-reduces it with the sums, so ranks may hold different batch sizes, as
- * torch.nn.SyncBatchNorm allows) */
+ * torch.nn.SyncBatchNorm allows); num_batches_tracked (int64, may be NULL) is incremented by the same launch */
 int ebc_bn_finalize(const double* colsum, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* mean, float* rstd, float* scale, float* shift, float* running_mean,
-                    float* running_var, int C, ebc_stream_t stream);
+                    float* running_var, long long* num_batches_tracked, int C, ebc_stream_t stream);
+/* ebc_conv3x3_fwd with the BatchNorm statistics epilogue + ebc_bn_finalize (count = B*H*W, running stats updated,
+ * num_batches_tracked incremented when non-NULL) for BatchNorms with no SyncBatchNorm exchange between the two: the
+ * conv's per-tile column sums are reduced and finalized in one launch; colsum_out (may be NULL) gets the f64 sums */
+int ebc_conv3x3_fwd_bn(int dtype, const void* xpad, const void* weight, void* out, void* ws, size_t wsb, int B, int H,
+                       int W, int C, int N, float eps, float momentum, const float* gamma, const float* beta,
+                       float* mean, float* rstd, float* scale, float* shift, float* running_mean, float* running_var,
+                       long long* num_batches_tracked, double* colsum_out, ebc_stream_t stream);
 /* hpad = zero-padded relu(z*scale + shift) */
 int ebc_bn_relu_pad(int dtype, const void* z, const float* scale, const float* shift, void* hpad, int B, int H,
                     int W, int C, ebc_stream_t stream);
@@ -343,7 +364,8 @@ int ebc_bn_stats(int dtype, const void* z, double* colsum, void* ws, size_t wsb,
  * colsum_out (may be NULL) receives the f64 sums ebc_bn_stats would. */
 int ebc_bn_stats_finalize(int dtype, const void* z, void* ws, size_t wsb, long P, int C, float eps, float momentum,
                           const float* gamma, const float* beta, float* mean, float* rstd, float* scale, float* shift,
-                          float* running_mean, float* running_var, double* colsum_out, ebc_stream_t stream);
+                          float* running_mean, float* running_var, double* colsum_out, long long* num_batches_tracked,
+                          ebc_stream_t stream);
 /* ebc_bn_bwd_reduce + ebc_bn_bwd_finalize (count = P) in two launches instead of three (no SyncBatchNorm exchange) */
 int ebc_bn_bwd_reduce_finalize(int dtype, const void* gy, const void* mask_y, const void* z, const float* mean,
                                const float* rstd, const float* scale, const float* shift, const float* gamma,

@@ -116,3 +116,37 @@ def test_dace_kernel_reduced_target_and_dmloss():
     pd = torch.tensor(pde, device=dev, requires_grad=True)
     loss, info = DMLoss(224, 8)(pd, torch.from_numpy(dens).to(dev), [torch.from_numpy(p).to(dev) for p in pts])
     assert float(loss) == pytest.approx(a[1]["loss"] - a[1]["ce_loss"], rel=1e-5)
+
+
+def test_dace_kernel_host_and_device_label_metadata_agree():
+    """Up to 64 crops the crop offsets / order travel as kernel arguments (ebc_dace_loss_h); 70 crops take the device
+    tensors (ebc_dace_loss).  Each crop runs in its own workgroup on the same arithmetic, so the per-crop statistics
+    (CE, TV, count, OT, Wasserstein distance, iterations) of the 70-crop batch equal those of its two 35-crop halves
+    bit for bit; packed label views (one buffer, the second half) give the same as separate tensors."""
+    from ebc_amd.losses import DACELoss
+    dev = torch.device("cuda:0")
+    B, size = 70, 224
+    img, pts, dens = syn.synthetic_crops(B, size, seed=123)
+    g = torch.Generator().manual_seed(9)
+    pc = torch.randn(B, len(BINS), 28, 28, generator=g).to(dev)
+    pd = torch.rand(B, 1, 28, 28, generator=g).to(dev)
+    td = torch.from_numpy(dens).to(dev)
+    fn = DACELoss(BINS, 8, count_loss="dmcount", input_size=size)
+
+    def run(sl, packed=False):
+        a, b = pc[sl].clone().requires_grad_(), pd[sl].clone().requires_grad_()
+        if packed:
+            buf = torch.from_numpy(np.concatenate([p.reshape(-1, 2) for p in pts[sl]], 0).astype(np.float32)).to(dev)
+            views, o = [], 0
+            for p in pts[sl]:
+                views.append(buf[o:o + len(p)])
+                o += len(p)
+        else:
+            views = [torch.from_numpy(p).to(dev) for p in pts[sl]]
+        loss, _ = fn(a, b, td[sl], views)
+        loss.backward()
+        return fn.last_stats.clone(), a.grad.clone(), b.grad.clone()
+    full = run(slice(0, B))
+    halves = [run(slice(0, 35)), run(slice(35, B), packed=True)]
+    st = torch.cat([h[0] for h in halves])
+    assert torch.equal(full[0][:, :6], st[:, :6])          # per-crop ce, tv*n, count, ot, wd, iterations
