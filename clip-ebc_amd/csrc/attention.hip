@@ -914,19 +914,6 @@ __global__ __launch_bounds__(64 * LNW) void attn_fwd_long_kernel(const typename 
         // (all products first, then the mask and the maximum: the LP kernel's order -- reading each tile's maximum
         // right behind its MFMA pair measured wrong maxima on gfx950 for some query lanes)
         f32x4 s[NKT];
-#ifdef EBC_LONG_MAX_LAB
-        float mc = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt) {
-            s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (kt < nkt) {
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) s[kt] = mma(lds_rowfrag<E>(Ks, 16 * kt + fr, 32 * ks + 8 * fg), qf[ks], s[kt]);
-#if EBC_LONG_MAX_LAB == 2
-                asm volatile("s_nop 7\n s_nop 7" ::: "memory");
-#endif
-                if (kt == nkt - 1) {
-#else
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt) {
             s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -940,7 +927,6 @@ __global__ __launch_bounds__(64 * LNW) void attn_fwd_long_kernel(const typename 
         for (int kt = 0; kt < NKT; ++kt) {
             if (kt < nkt) {
                 if (kt == nkt - 1) {
-#endif
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         if (16 * kt + 4 * fg + i >= Lc) s[kt][i] = -INFINITY;
