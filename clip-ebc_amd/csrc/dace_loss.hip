@@ -39,6 +39,16 @@ constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
 constexpr int SORTED_W16_MIN_POINTS = 257;   // crops from this many points: 16 lanes per block (r02 probe)
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
 
+// Lab-only phase timer (-DEBC_DACE_PROF, tools/dbg/dace_prof.py): thread 0 of each crop's workgroup records core-clock
+// stamps (s_memtime) at the crop body's phase boundaries and per-iteration phase sums; read by ebc_dace_prof_read.
+#ifdef EBC_DACE_PROF
+__device__ unsigned long long g_dace_prof[64][64];
+#define PROF_AT(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_dace_prof[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
+#define PROF_T() (__builtin_amdgcn_s_memtime())
+#else
+#define PROF_AT(k) do {} while (0)
+#endif
+
 // G = the LDS grid (a multiple of 4 >= the crop's density grid g = size / reduction); cells with a row or
 // column >= g are dead: zero density, zero kernel factors, v = 0, never written out.
 template <int G> struct Cfg {
@@ -326,6 +336,14 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
     int* tmpwin = reinterpret_cast<int*>(u1);
     for (int k = t; k < NBK; k += NT) cnt[k] = 0;
     __syncthreads();
+    // The scatter pass (ranks, factor rows) runs LPP lanes a point, as many as one pass of the workgroup takes (up to 32):
+    // each lane counts every LPP-th earlier point and fills every LPP-th factor cell, the rank meets by lane shuffles; the
+    // values are the one-lane form's, cell for cell.  r05 (kernel trace, 16 crops): 172 -> 163 us at 20 points a crop, 221
+    // -> 215 us on a bench-like batch (one lane a point ran the 28-cell expf / division chain serially).  The windows pass
+    // with LPP lanes a point as well measured no further gain on the bench's batches, and made the kernel spill: it stays
+    // one lane a point.
+    const int LG = n <= 32 ? 5 : n <= 64 ? 4 : n <= 128 ? 3 : n <= 256 ? 2 : n <= 512 ? 1 : 0, LPP = 1 << LG;
+    auto grp_sum = [&](int v) { for (int o = LPP >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64); return v; };
     // 1. windows (read off the computed factors, as sinkhorn_crop) and home buckets, original order
     int wide = 0;
     for (int i = t; i < n; i += NT) {
@@ -346,34 +364,41 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
         atomicAdd(&cnt[kk], 1);
     }
     if (block_or(wide, reinterpret_cast<int*>(misc))) return false;
+    PROF_AT(48);
     if (t == 0) {
         int s = 0;
         for (int k = 0; k < NBK; ++k) { start[k] = s; s += cnt[k]; }
         start[NBK] = s;
     }
     __syncthreads();
+    PROF_AT(49);
     // 2. stable scatter: slot = bucket start + rank among the earlier points of the same bucket
-    for (int i = t; i < n; i += NT) {
+    for (int e0 = 0; e0 < n * LPP; e0 += NT) {
+        const int e = e0 + t, i = e >> LG, sub = e & (LPP - 1);
+        if (i >= n) break;                                   // whole groups (n * LPP is a multiple of LPP)
         const int kk = key[i];
         int r = 0;
-        for (int j = 0; j < i; ++j) r += key[j] == kk;
-        const int slot = start[kk] + r;
+        for (int j = sub; j < i; j += LPP) r += key[j] == kk;
+        const int slot = start[kk] + grp_sum(r);
         const float px = pts[2 * i], py = pts[2 * i + 1];
         const float x = pcoord(px, size, norm), y = pcoord(py, size, norm);
         const int w = tmpwin[i];
         const int yb = row_base<G, CW>(w & 255, (w >> 8) & 255), xb = row_base<G, CW>((w >> 16) & 255, (w >> 24) & 255);
-        for (int k = 0; k < CW; ++k) {
+        for (int k = sub; k < CW; k += LPP) {
             const float cy = cood(yb + k, size, red, norm), cx = cood(xb + k, size, red, norm);
             const float yd = (-2.0f * (y * cy) + y * y) + cy * cy;
             const float xd = (-2.0f * (x * cx) + x * x) + cx * cx;
             Ey[slot * CW + k] = yb + k < g ? expf(yd / -reg) : 0.f;
             Ex[slot * CW + k] = xb + k < g ? expf(xd / -reg) : 0.f;
         }
-        spts[2 * slot] = px;
-        spts[2 * slot + 1] = py;
-        win[slot] = tmpwin[i];
+        if (sub == 0) {
+            spts[2 * slot] = px;
+            spts[2 * slot + 1] = py;
+            win[slot] = w;
+        }
     }
     __syncthreads();
+    PROF_AT(50);
     for (int i = t; i < n; i += NT) u0[i] = 1.0f / (float)n;
     for (int j = t; j < GG; j += NT) v0[j] = (j / G < g && j % G < g) ? 1.0f / (float)(g * g) : 0.f;
     const float a = 1.0f / (float)n;
@@ -551,8 +576,15 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
         }
     }
     int to_eval = eval_freq;
+#ifdef EBC_DACE_PROF
+    unsigned long long pa = 0, pb = 0, pe = 0, tp0 = 0, tp1 = 0, wa = 0, wb = 0;
+    PROF_AT(4);
+#endif
     while (err > stop_thr && it <= max_iter) {               // bregman_pytorch.py:102
         int* fl = flag + (it & 1);
+#ifdef EBC_DACE_PROF
+        tp0 = PROF_T();
+#endif
         // phase A: v = b / (K^T u + eps) (K^T u reused from the err pass)
         int bad = 0;
         for (int blk = t / LPB; blk < NBK; blk += BPP) {
@@ -573,7 +605,13 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
         }
         have_ktu = 0;
         if (bad) *fl = 1;
+#ifdef EBC_DACE_PROF
+        wa += PROF_T() - tp0;
+#endif
         __syncthreads();
+#ifdef EBC_DACE_PROF
+        tp1 = PROF_T(); pa += tp1 - tp0;
+#endif
         if (t == 0) flag[(it + 1) & 1] = 0;
         // phase B: u = a / (K v + eps)
         if (kv_regs) {
@@ -638,8 +676,14 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
                 if (!isfinite(val)) *fl = 1;
             }
         }
+#ifdef EBC_DACE_PROF
+        wb += PROF_T() - tp1;
+#endif
         __syncthreads();
         if (*fl) { rolled = 1; break; }                       // keep (u, v): rollback, :111-115
+#ifdef EBC_DACE_PROF
+        tp0 = PROF_T(); pb += tp0 - tp1;
+#endif
         { float* tu = u; u = un; un = tu; float* tv = v; v = vn; vn = tv; }
         if (--to_eval == 0) {                                 // it % eval_freq == 0 (:117-126); K^T u kept
             to_eval = eval_freq;
@@ -662,9 +706,21 @@ __device__ bool sinkhorn_sorted(int n, int g, int size, int red, int norm, float
             err = block_sum(e, misc);
             err_last = err;
             have_ktu = 1;
+#ifdef EBC_DACE_PROF
+            pe += PROF_T() - tp0;
+#endif
         }
         ++it;
     }
+#ifdef EBC_DACE_PROF
+    PROF_AT(5);
+    if (t == 0 && blockIdx.x < 64) {
+        g_dace_prof[blockIdx.x][8] = pa; g_dace_prof[blockIdx.x][9] = pb; g_dace_prof[blockIdx.x][10] = pe;
+        g_dace_prof[blockIdx.x][11] = (unsigned long long)it; g_dace_prof[blockIdx.x][12] = (unsigned long long)n;
+        g_dace_prof[blockIdx.x][13] = (unsigned long long)LPB;
+    }
+    if ((t & 63) == 0 && blockIdx.x < 64) { g_dace_prof[blockIdx.x][16 + t / 64] = wa; g_dace_prof[blockIdx.x][32 + t / 64] = wb; }
+#endif
     if (v != v0) { for (int j = t; j < GG; j += NT) v0[j] = v[j]; }
     if (u != u0) { for (int i = t; i < n; i += NT) u0[i] = u[i]; }
     __syncthreads();
@@ -725,6 +781,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
     float* facc = part + GG;                                  // LDS factors, compact rows (bucketed path)
 
     const int p0 = P.hmeta ? P.hoff[b] : P.offsets[b], n = (P.hmeta ? P.hoff[b + 1] : P.offsets[b + 1]) - p0;
+    PROF_AT(0);
 
     // 1. pred density, target block sums (losses/utils.py:4-9)
     for (int j = t; j < GG; j += NT) { pd[j] = live(j) ? P.pred_density[(size_t)b * gg + gidx(j)] : 0.f; td[j] = 0.f; }
@@ -742,6 +799,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         }
     }
     __syncthreads();
+    PROF_AT(1);
     const float pc = block_sum([&] { float s = 0.f; for (int j = t; j < GG; j += NT) s += pd[j]; return s; }(), misc);
     const float tc = (float)n;
 
@@ -765,6 +823,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
             gc[(size_t)k * gg] = (expf(lg[(size_t)k * gg] - lse) - (k == cls ? 1.f : 0.f)) * invB;
     }
     ce = block_sum(ce, misc);
+    PROF_AT(2);
 
     float cnt_b = 0.f, tv_b = 0.f, ot_b = 0.f, wd_b = 0.f, err_last = -1.f;
     int iters = 0, rolled = 0;
@@ -798,6 +857,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
         const float gcount = dm ? sgnf(pc - tc) * invB : 0.f;
         const float wtv = dm ? P.w_tv : 0.f;
         // 4. Sinkhorn OT (dm_loss.py:49-77)
+        PROF_AT(3);
         if (n > 0) {
             const float* pts = P.points + 2 * (size_t)p0;
             // Inlined copies so each sees one address space for the factors: LDS-resident crops get
@@ -853,6 +913,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
                                                 &iters, &rolled, &err_last);
                 if (!ok) return false;
                 post(cw, Ey, Ex, u0, win, spts);
+                PROF_AT(6);
                 return true;
             };
             bool done = false;
@@ -878,6 +939,7 @@ __device__ void crop_body(const Params& P, int b, float* lds)
             P.grad_density[(size_t)b * gg + gidx(j)] = P.w_count * (P.w_ot * v1[j] + wtv * gtv + gcount);
         }
     }
+    PROF_AT(7);
     if (t == 0) {
         float* st = P.crop_stats + (size_t)b * 8;
         st[0] = ce; st[1] = tv_b; st[2] = cnt_b; st[3] = ot_b; st[4] = wd_b;
@@ -1069,3 +1131,11 @@ extern "C" int ebc_scale2(const float* s, const float* a, float* a_out, long na,
 }
 
 extern "C" int ebc_version(void) { return 1; }
+
+#ifdef EBC_DACE_PROF
+extern "C" int ebc_dace_prof_read(unsigned long long* host, int nbytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dace_prof), std::min<size_t>(nbytes, sizeof(g_dace_prof)), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
