@@ -33,7 +33,10 @@ namespace {
 
 // threads per workgroup (16 waves, 4 per SIMD): r02 measured the 100-iteration floor at 512 and 1024 threads the same,
 // 256 threads 1.5x slower; 1024 keeps one pass over the cells / blocks per phase at G = 28
-constexpr int NT = 1024;
+#ifndef EBC_DACE_NT
+#define EBC_DACE_NT 1024
+#endif
+constexpr int NT = EBC_DACE_NT;
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
 constexpr int SORTED_W16_MIN_POINTS = 257;   // crops from this many points: 16 lanes per block (r02 probe)

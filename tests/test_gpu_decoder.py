@@ -341,3 +341,30 @@ def test_conv3x3_wgrad_abi_matches_torch(B, plan):
     print(f"B={B}: wgrad rel-L2 vs f64 {err:.2e}")
     assert err < 1e-5
     assert int(ws[:16384].view(torch.int32).abs().sum()) == 0          # arrival counters re-armed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,B", [(torch.float16, 16), (torch.bfloat16, 3), (torch.float32, 2)])
+def test_transpose3_matches_definition(dtype, B):
+    """ebc_dec_transpose3 bit for bit against its definition: xT3[kx][c][pos] = xpad[(b Hp + yp) Wp + x + kx][c] for
+    pos = b Pimg + yp W + x (b < B), 0 past the last image; the pad cells are copied as they are."""
+    from ebc_amd import _lib
+    import ctypes
+    L = _lib.lib()
+    H, W, C = 28, 28, 768
+    code = {torch.float16: _lib.EBC_F16, torch.bfloat16: _lib.EBC_BF16, torch.float32: _lib.EBC_F32}[dtype]
+    dev = torch.device("cuda")
+    geo = (ctypes.c_long * 6)()
+    _lib.check(L.ebc_dec_geometry(code, B, H, W, C, geo), "geo")
+    Hp, Wp, HWp, Kq, Q, Qs = (int(v) for v in geo)
+    g = torch.Generator(device=dev).manual_seed(7 + B)
+    xpad = torch.randn(B, Hp, Wp, C, generator=g, device=dev).to(dtype)      # pad cells non-zero too: copied as they are
+    xT3 = torch.full((3, C, Qs), 7.0, device=dev, dtype=dtype)
+    _lib.check(L.ebc_dec_transpose3(code, _lib.ptr(xpad), _lib.ptr(xT3), B, H, W, C, _lib.stream()), "t3")
+    torch.cuda.synchronize()
+    ref = torch.zeros(3, C, Qs, dtype=dtype)
+    xp = xpad.cpu()
+    for kx in range(3):
+        blk = xp[:, :, kx:kx + W, :]                                            # [B, Hp, W, C]: x + kx
+        ref[kx, :, :B * Hp * W] = blk.reshape(B * Hp * W, C).t()
+    assert torch.equal(xT3.cpu(), ref)
