@@ -39,7 +39,10 @@ namespace {
 constexpr int NT = EBC_DACE_NT;
 constexpr int LDS_MAX = 160 * 1024;
 constexpr float M_EPS = 1e-16f;          // bregman_pytorch.py:8
-constexpr int SORTED_W16_MIN_POINTS = 257;   // crops from this many points: 16 lanes per block (r02 probe)
+#ifndef EBC_DACE_W16_MIN
+#define EBC_DACE_W16_MIN 257
+#endif
+constexpr int SORTED_W16_MIN_POINTS = EBC_DACE_W16_MIN;   // crops from this many points: 16 lanes per block (r02 probe)
 constexpr float EPS = 1e-8f;             // dm_loss.py:7
 
 // Lab-only phase timer (-DEBC_DACE_PROF, tools/dbg/dace_prof.py): thread 0 of each crop's workgroup records core-clock

@@ -7,7 +7,7 @@ import sys
 
 import numpy as np
 
-CONFIGS = [("16x0", [0] * 16), ("16x20", [20] * 16), ("16x100", [100] * 16), ("16x300", [300] * 16),
+CONFIGS = [("16x0", [0] * 16), ("16x20", [20] * 16), ("16x100", [100] * 16), ("16x150", [150] * 16), ("16x200", [200] * 16), ("16x300", [300] * 16),
            ("16x600", [600] * 16), ("16x1000", [1000] * 16)]
 g = np.random.default_rng(0)
 for s in range(3):
