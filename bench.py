@@ -72,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--prefetch", action="store_true",
                     help="A/B: the next batch's frozen patch embedding on a side stream beside this step's loss "
                          "(CLIP_EBC.prefetch_patch_embed) instead of inline in its forward (r05: measured 1.2 %% slower)")
+    ap.add_argument("--hiprio", action="store_true",
+                    help="A/B: run the step on a high-priority stream (with --prefetch: the side stream's work then yields "
+                         "the CUs to the loss kernel)")
     ap.add_argument("--no-ln-fold-bwd", action="store_true",
                     help="A/B: ln_2's backward as a LayerNorm launch instead of in the c_fc dX product's epilogue")
     ap.add_argument("--optim", default="hip", choices=["hip", "torch"],
@@ -629,6 +632,8 @@ def main():
             dist.destroy_process_group()
         return
     from ebc_amd import _lib
+    if getattr(args, "hiprio", False):
+        torch.cuda.set_stream(torch.cuda.Stream(device, priority=-1))   # A/B: the step on a high-priority stream
     step = setup(args, rank, world, local, device)
     B = args.crops_per_gpu
 
