@@ -69,12 +69,6 @@ def parse(argv=None):
                     help="A/B: ln_1 / ln_2 as LayerNorm launches instead of folded into the QKV / c_fc products")
     ap.add_argument("--touch", type=int, default=None, choices=[0, 1],
                     help="A/B: the attention launches' weight touch off / on (ebc_set_weight_touch)")
-    ap.add_argument("--prefetch", action="store_true",
-                    help="A/B: the next batch's frozen patch embedding on a side stream beside this step's loss "
-                         "(CLIP_EBC.prefetch_patch_embed) instead of inline in its forward (r05: measured 1.2 %% slower)")
-    ap.add_argument("--hiprio", action="store_true",
-                    help="A/B: run the step on a high-priority stream (with --prefetch: the side stream's work then yields "
-                         "the CUs to the loss kernel)")
     ap.add_argument("--no-ln-fold-bwd", action="store_true",
                     help="A/B: ln_2's backward as a LayerNorm launch instead of in the c_fc dX product's epilogue")
     ap.add_argument("--optim", default="hip", choices=["hip", "torch"],
@@ -283,19 +277,10 @@ def setup(args, rank, world, local, device):
     npool = min(args.pool, args.warmup + args.steps)
     pool = [make_batch(B, rank, s, device, args.size) for s in range(npool)]
 
-    # --prefetch (input pipelining): the next batch's frozen patch embedding (conv1) enqueued on a side stream right
-    # before this step's loss, whose kernel leaves 240 of the 256 CUs idle; the next forward starts from it (same bits).
-    # Same box r05: 4.27 vs 4.22 ms a step -- slower (the side stream's workgroups are dispatched as the loss kernel is,
-    # on the CUs it needs), so off by default
-    core = getattr(model, "module", model)
-    prefetch = getattr(args, "prefetch", False) and hasattr(core, "prefetch_patch_embed")
-
     def step(i):
         img, pts, dens, _ = pool[i % len(pool)]
         with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
             logits, exp = model(img)
-            if prefetch:
-                core.prefetch_patch_embed(pool[(i + 1) % len(pool)][0])
             loss, info = loss_fn(logits, exp, dens, pts)
         opt.zero_grad(set_to_none=True)
         scaler.scale(loss).backward()
@@ -632,8 +617,6 @@ def main():
             dist.destroy_process_group()
         return
     from ebc_amd import _lib
-    if getattr(args, "hiprio", False):
-        torch.cuda.set_stream(torch.cuda.Stream(device, priority=-1))   # A/B: the step on a high-priority stream
     step = setup(args, rank, world, local, device)
     B = args.crops_per_gpu
 

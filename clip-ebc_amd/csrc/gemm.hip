@@ -23,6 +23,12 @@
 
 using namespace ebc;
 
+// Phase stamps for tools/lab/gemm_tl_lab.hip (a per-workgroup timeline: entry, first k-tile landed, K loop done,
+// epilogue issued); nothing in the library build
+#ifndef EBC_GEMM_STAMP
+#define EBC_GEMM_STAMP(phase, tile) ((void)0)
+#endif
+
 namespace {
 
 constexpr int LN_PMAX = ebc::GEMM_LN_PMAX;   // EPI_LN: at most 16 row partials (N / BN * 2 of the producing product)
@@ -302,6 +308,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             tn = r / gm;
         }
         const int m0 = tm * BM, n0 = tn * BN;
+        EBC_GEMM_STAMP(0, tile);
 
         // per-lane source rows for the LDS-DMA staging (fixed across k; the k-tile offset is added by stage())
         const T* src[NLD];
@@ -575,6 +582,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         for (int s = 0; s < S - 1; ++s)
             if (s < nk) stage(s, s);
         sync_tile(0, std::true_type{});
+        EBC_GEMM_STAMP(1, tile);
         if (S - 1 < nk) stage(S - 1, S - 1);
         typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
         load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
@@ -658,6 +666,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         int kt0 = 0;
         for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
         for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
+        EBC_GEMM_STAMP(2, tile);
 
         if (SPL && g.splits > 1 && g.cnt == nullptr) {
             // split-K without a last arriver (deep splits of the weight-gradient products): every split stores its
@@ -1115,6 +1124,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             }
             }   // staged epilogue (MODE 1 / 2)
         }   // fin
+        EBC_GEMM_STAMP(3, tile);
         return nk;
     };
     const unsigned nk1 = (unsigned)segment(it_beg);
@@ -1137,11 +1147,9 @@ int launch_gemm_k(const GemmArgs& g, hipStream_t st)
     constexpr int BPB = MODE == 0 && EPI == EPI_GELU_BWD ? RING + 2 * ((BN * 4 + 1023) / 1024) * 1024 : 0;
     constexpr int LNB = LNB0 > BPB ? LNB0 : BPB;
     constexpr int LDS = gemm_lds_bytes<BM, BN, S, ROWB, WM>() > LNB ? gemm_lds_bytes<BM, BN, S, ROWB, WM>() : LNB;
-    // (the LN_BWD instances of the 256-wide tiles would need more: that epilogue runs on the N = 768 tiles only)
-    static_assert(LDS <= 160 * 1024 || EPI == EPI_LN_BWD, "LDS");
-    if constexpr (LDS > 160 * 1024) {
-        return EBC_E_UNSUPPORTED;
-    } else {
+    // (the LN_BWD instances of the 256-row tiles would need more: dispatch_tile never instantiates them)
+    static_assert(LDS <= 160 * 1024, "LDS");
+    {
     constexpr int BK = ROWB / E::BYTES;
     if (!ensure_lds<gemm_nt_kernel<E, TO, EPI, BM, BN, S, WGM, WGN, ROWB, MODE, SPL, NLW>>(LDS, st)) return EBC_E_LAUNCH;
     if (g.N % BN || g.kslice % BK || g.kslice * g.splits != g.K) return EBC_E_UNSUPPORTED;
@@ -1261,7 +1269,11 @@ template <class E, class TO, int EPI>
 int dispatch_tile(GemmArgs g, void* /*ws*/, size_t /*ws_bytes*/, hipStream_t st)
 {
     constexpr bool SIXTEEN = E::BYTES == 2;
-    const int cfg = select_cfg(SIXTEEN, g.M, g.N, g.K);
+    int cfg = select_cfg(SIXTEEN, g.M, g.N, g.K);
+    // EPI_LN_BWD stages BM rows x 32 partial pairs past the ring: the 256-row tiles the many-tile shapes pick (M >= ~24k
+    // rows, e.g. 30 crops of 448) would need 180 KB of LDS, so those shapes run the 128x96 tile (several waves of
+    // tiles there).  The tile of this product is free: the partials' count comes from the GELU' product's tiling.
+    if (EPI == EPI_LN_BWD && (cfg == 3 || cfg == 7)) cfg = 5;
     const TileCfg* c = find_cfg(cfg);
     g.splits = 1;
     g.kslice = g.K;
@@ -1269,10 +1281,14 @@ int dispatch_tile(GemmArgs g, void* /*ws*/, size_t /*ws_bytes*/, hipStream_t st)
     switch (cfg) {
         case 1: return launch_gemm<E, TO, EPI, 128, 128, 2>(g, st);
         case 2: return launch_gemm<E, TO, EPI, 128, 64, 2>(g, st);
-        case 3: return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2>(g, st);
         case 4: return launch_gemm<E, TO, EPI, 192, 192, 2, 4, 2>(g, st);
         case 5: return launch_gemm<E, TO, EPI, 128, 96, 2>(g, st);
-        case 7: return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2>(g, st);
+    }
+    if constexpr (EPI != EPI_LN_BWD) {
+        switch (cfg) {
+            case 3: return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2>(g, st);
+            case 7: return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2>(g, st);
+        }
     }
     if constexpr (SIXTEEN) {
         switch (cfg) {

@@ -144,44 +144,11 @@ extern "C" size_t ebc_vit_workspace_bytes(int B, int H, int W, int layers, int n
     return carve(nullptr, B, L, G, layers, dtype, training).bytes;
 }
 
-// The frozen patch embedding (conv1 as im2col + GEMM, image_encoder.py:141) on its own: it depends on the image only,
-// so a training loop can run the NEXT batch's on a side stream while this step's loss kernel holds 16 CUs
-// (ebc_amd.model.VitPrefetch); ebc_vit_forward_pe then starts from it.  Same launches, same bits as inside the forward.
-extern "C" size_t ebc_vit_patch_embed_workspace_bytes(int B, int H, int W, int dtype)
-{
-    const int G = (H / 16) * (W / 16);
-    const size_t es = dtype == EBC_F32 ? 4 : 2;
-    const size_t t = (((size_t)B * G * WIDTH * es) + 255) / 256 * 256;
-    return t + std::max<size_t>(ebc::gemm_workspace_bytes(dtype, B * G, WIDTH, WIDTH), 16 * 1024);
-}
-extern "C" int ebc_vit_patch_embed(const EbcVitWeights* w, const float* image, int B, int H, int W, int dtype,
-                                   float* patch_f, void* ws, size_t ws_bytes, ebc_stream_t stream)
-{
-    if (!check_weights(w) || !image || !patch_f || !ws || B <= 0 || H % 16 || W % 16) return EBC_E_ARG;
-    if (ws_bytes < ebc_vit_patch_embed_workspace_bytes(B, H, W, dtype)) return EBC_E_ARG;
-    hipStream_t st = (hipStream_t)stream;
-    const int G = (H / 16) * (W / 16);
-    const size_t es = dtype == EBC_F32 ? 4 : 2;
-    const size_t t = (((size_t)B * G * WIDTH * es) + 255) / 256 * 256;
-    void* patch_t = ws;
-    void* gws = (char*)ws + t;
-    EBC_TRY(ebc::im2col(dtype, image, patch_t, B, H, W, 16, st));
-    return ebc::gemm_nt(dtype, EBC_EPI_STORE, 1, patch_t, w->w_patch, patch_f, nullptr, nullptr, nullptr, B * G, WIDTH,
-                        WIDTH, st, gws, ws_bytes - t);
-}
-
 extern "C" int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B, int H, int W,
                                const float* const* vpt, long vpt_bstride, int dtype, int training,
                                void* ws, size_t ws_bytes, float* feat, ebc_stream_t stream)
 {
-    return ebc_vit_forward_pe(w, image, B, H, W, vpt, vpt_bstride, dtype, training, ws, ws_bytes, feat, nullptr, stream);
-}
-
-extern "C" int ebc_vit_forward_pe(const EbcVitWeights* w, const float* image, int B, int H, int W,
-                                  const float* const* vpt, long vpt_bstride, int dtype, int training,
-                                  void* ws, size_t ws_bytes, float* feat, const float* patch_f, ebc_stream_t stream)
-{
-    if (!check_weights(w) || (!image && !patch_f) || !ws || !feat || B <= 0 || H % 16 || W % 16) return EBC_E_ARG;
+    if (!check_weights(w) || !image || !ws || !feat || B <= 0 || H % 16 || W % 16) return EBC_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     const int NV = w->num_vpt, G = (H / 16) * (W / 16), L = 1 + NV + G, layers = w->layers;
     if (L > 16384) return EBC_E_UNSUPPORTED;                 // attention.hip L_MAX
@@ -195,15 +162,11 @@ extern "C" int ebc_vit_forward_pe(const EbcVitWeights* w, const float* image, in
         return ebc::gemm_nt(dtype, epi, out_f32, A, Bm, C, bias, resid, aux, m, n, k, st, lay.gws, lay.gws_bytes);
     };
 
-    // patch embedding: im2col + GEMM with conv1 weight [768, 3*16*16] (image_encoder.py:141), unless the caller ran it
-    // already (ebc_vit_patch_embed, patch_f)
-    if (!patch_f) {
-        EBC_TRY(ebc::im2col(dtype, image, lay.patch_t, B, H, W, 16, st));
-        EBC_TRY(gemm(EBC_EPI_STORE, 1, lay.patch_t, w->w_patch, lay.patch_f, nullptr, nullptr, nullptr, B * G, WIDTH, WIDTH));
-        patch_f = lay.patch_f;
-    }
+    // patch embedding: im2col + GEMM with conv1 weight [768, 3*16*16] (image_encoder.py:141)
+    EBC_TRY(ebc::im2col(dtype, image, lay.patch_t, B, H, W, 16, st));
+    EBC_TRY(gemm(EBC_EPI_STORE, 1, lay.patch_t, w->w_patch, lay.patch_f, nullptr, nullptr, nullptr, B * G, WIDTH, WIDTH));
     // CLS + pos + ln_pre, VPT_0 rows (model.py:150-168)
-    EBC_TRY(ebc::embed_tokens(patch_f, w->cls, w->pos, w->ln_pre_g, w->ln_pre_b, NV ? vpt[0] : nullptr,
+    EBC_TRY(ebc::embed_tokens(lay.patch_f, w->cls, w->pos, w->ln_pre_g, w->ln_pre_b, NV ? vpt[0] : nullptr,
                               vpt_bstride, lay.X[0], B, L, G, NV, WIDTH, st));
     // one block on crops [b0, b0 + nb) (rows r0 = b0 * L of every [B][L][*] buffer) on stream sx
     const size_t es = dtype == EBC_F32 ? 4 : 2;

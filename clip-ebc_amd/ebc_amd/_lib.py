@@ -81,9 +81,6 @@ SIGNATURES = {
     "ebc_transpose": (_I, [_I, _P, _P, _I, _I, _L, _P]),
     "ebc_vit_workspace_bytes": (_Z, [_I, _I, _I, _I, _I, _I, _I]),
     "ebc_vit_forward": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_long, _I, _I, _P, _Z, _P, _P]),
-    "ebc_vit_forward_pe": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_long, _I, _I, _P, _Z, _P, _P, _P]),
-    "ebc_vit_patch_embed_workspace_bytes": (_Z, [_I, _I, _I, _I]),
-    "ebc_vit_patch_embed": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "ebc_vit_backward": (_I, [_P, _I, _I, _I, _I, _P, _Z, _P, _P, ctypes.c_long, _I, _P]),
     "ebc_set_weight_touch": (_I, [_I]),
     "ebc_layernorm_fwd": (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P]),

@@ -189,36 +189,6 @@ class _EncoderCache:
         return self.structs[(gh, gw)][0]
 
 
-class VitPrefetch:
-    """The frozen patch embedding (conv1: im2col + GEMM, image_encoder.py:141) of a FUTURE batch, run on a side stream
-    (CLIP_EBC.prefetch_patch_embed): it depends on the image only, so a training loop enqueues the next batch's right
-    before this step's loss, whose kernel holds 16 of the 256 CUs for ~0.2 ms; the next forward on the same image tensor
-    then starts from it (ebc_vit_forward_pe, the same launches and bits).  One pending entry: (key, patch_f, done event,
-    image); patch_f is allocated on the compute stream, which waits on the event before it reads or frees it."""
-
-    def __init__(self):
-        self.stream: Optional[torch.cuda.Stream] = None
-        self.entry = None
-        self.ws: Dict[Tuple[torch.device, int], Tensor] = {}
-
-    @staticmethod
-    def key(img: Tensor, dt: int):
-        return (img.data_ptr(), tuple(img.shape), img._version, dt)
-
-    def drop(self, main: torch.cuda.Stream) -> None:
-        if self.entry is not None:
-            main.wait_event(self.entry[2])
-            self.entry = None
-
-    def take(self, img: Tensor, dt: int, main: torch.cuda.Stream) -> Optional[Tensor]:
-        e = self.entry
-        if e is None or e[0] != self.key(img, dt):
-            return None
-        self.entry = None
-        main.wait_event(e[2])
-        return e[1]
-
-
 class _VitFn(torch.autograd.Function):
     """ebc_vit_forward / ebc_vit_backward: image -> ln_post(patch tokens) [B, G, 768] f32."""
 
@@ -241,10 +211,8 @@ class _VitFn(torch.autograd.Function):
         vp = [v.detach().float().contiguous() for v in vpts]
         arr = (_VP * cache.layers)(*([_p(v) for v in vp] + [None] * (cache.layers - len(vp))))
         w = cache.weights(gh, gw)
-        pf = getattr(cache, "prefetch", None)
-        patch_f = pf.take(image, dt, torch.cuda.current_stream(dev)) if pf is not None else None
-        rc = L.ebc_vit_forward_pe(ctypes.byref(w), _lib.ptr(image), B, H, W, arr, vpt_bstride, dt, int(training),
-                                  _lib.ptr(ws), nbytes, _lib.ptr(feat), _lib.ptr(patch_f), _lib.stream(dev))
+        rc = L.ebc_vit_forward(ctypes.byref(w), _lib.ptr(image), B, H, W, arr, vpt_bstride, dt, int(training),
+                               _lib.ptr(ws), nbytes, _lib.ptr(feat), _lib.stream(dev))
         _lib.check(rc, "ebc_vit_forward")
         ctx.cache, ctx.ws, ctx.shape, ctx.bstride = cache, ws, (B, H, W), vpt_bstride
         ctx.vpt_shapes = [v.shape for v in vpts]
@@ -727,45 +695,6 @@ class CLIP_EBC(nn.Module):
             vpts = [F.dropout(v.unsqueeze(0).expand(B, -1, -1), self.vpt_drop, True).contiguous() for v in vpts]
             return vpts, self.num_vpt * WIDTH
         return vpts, 0
-
-    def prefetch_patch_embed(self, x: Tensor) -> None:
-        """Enqueue the frozen patch embedding of a future batch `x` on a side stream, behind everything enqueued on the
-        current stream so far (call it right before the loss: it then runs on the CUs the loss kernel leaves idle); the
-        next forward on the same tensor (same dtype / autocast state) starts from it.  ViT + VPT backbone only; a no-op
-        otherwise.  Numerics are unchanged (tests/test_gpu_model.py::test_patch_embed_prefetch_is_bitwise)."""
-        if self.backbone == "resnet50" or not x.is_cuda or self.num_vpt <= 0:
-            return
-        B, _, H, W = x.shape
-        cdt = self._compute_dtype(x)
-        cache = self._encoder_cache(cdt, x.device)
-        if getattr(self, "_prefetch", None) is None:
-            self._prefetch = VitPrefetch()
-        pf = self._prefetch
-        cache.prefetch = pf
-        L = _lib.lib()
-        dt = _lib.dtype_code(cdt)
-        dev = x.device
-        with _lib.on(x):
-            main = torch.cuda.current_stream(dev)
-            if pf.stream is None:
-                pf.stream = torch.cuda.Stream(dev)
-            pf.drop(main)
-            img = x.detach().float().contiguous()
-            nb = L.ebc_vit_patch_embed_workspace_bytes(B, H, W, dt)
-            ws = pf.ws.get((dev, nb))
-            if ws is None:
-                ws = pf.ws[(dev, nb)] = torch.zeros(nb, device=dev, dtype=torch.uint8)   # split-K counters start 0
-            patch_f = torch.empty(B * (H // PATCH) * (W // PATCH), WIDTH, device=dev, dtype=torch.float32)
-            ready = torch.cuda.Event()
-            ready.record(main)
-            pf.stream.wait_event(ready)
-            w = cache.weights(H // PATCH, W // PATCH)
-            rc = L.ebc_vit_patch_embed(ctypes.byref(w), _lib.ptr(img), B, H, W, dt, _lib.ptr(patch_f), _lib.ptr(ws), nb,
-                                       ctypes.c_void_p(pf.stream.cuda_stream))
-            _lib.check(rc, "ebc_vit_patch_embed")
-            done = torch.cuda.Event()
-            done.record(pf.stream)
-            pf.entry = (VitPrefetch.key(img, dt), patch_f, done, img)
 
     def _forward_vpt_nhwc(self, x: Tensor) -> Tensor:
         """[B,3,H,W] -> ln_post patch tokens [B,H/16,W/16,768] f32 (NHWC), models/clip/model.py:142-189."""

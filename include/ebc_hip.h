@@ -180,18 +180,6 @@ size_t ebc_vit_workspace_bytes(int B, int H, int W, int layers, int num_vpt, int
 int ebc_vit_forward(const EbcVitWeights* w, const float* image, int B, int H, int W,
                     const float* const* vpt, long vpt_bstride, int dtype, int training,
                     void* workspace, size_t workspace_bytes, float* feat, ebc_stream_t stream);
-/* The frozen patch embedding alone (conv1 = im2col + GEMM, image_encoder.py:141): image [B,3,H,W] f32 -> patch_f
- * [B*(H/16)*(W/16), 768] f32, the same launches and bits as inside ebc_vit_forward.  It depends on the image only, so a
- * training loop may run the next batch's on a side stream beside this step's loss (ebc_amd.model.VitPrefetch).
- * workspace: ebc_vit_patch_embed_workspace_bytes, its first 16 KiB zeroed once (split-K counters, left zero). */
-size_t ebc_vit_patch_embed_workspace_bytes(int B, int H, int W, int dtype);
-int ebc_vit_patch_embed(const EbcVitWeights* w, const float* image, int B, int H, int W, int dtype, float* patch_f,
-                        void* workspace, size_t workspace_bytes, ebc_stream_t stream);
-/* ebc_vit_forward starting from a precomputed patch embedding (patch_f from ebc_vit_patch_embed; NULL: computed from
- * image as ebc_vit_forward does; image may then be NULL). */
-int ebc_vit_forward_pe(const EbcVitWeights* w, const float* image, int B, int H, int W,
-                       const float* const* vpt, long vpt_bstride, int dtype, int training,
-                       void* workspace, size_t workspace_bytes, float* feat, const float* patch_f, ebc_stream_t stream);
 /* dfeat [B, G, 768] f32 -> dvpt[l] ([num_vpt,768] f32, summed over crops; per crop if vpt_bstride).
  * Layer 0's backward stops at its prompt rows (the frozen embedding below takes no gradient: dQ/dK/dV of the first
  * query/key block, dH and ln_1' of the prompt rows only); flags & EBC_VIT_BWD_FULL_LAYER0 runs it over every row
