@@ -202,6 +202,50 @@ template <> __device__ __forceinline__ void load8f<float>(const float* p, float*
     load4<float>(p + 4, v + 4);
 }
 
+// Epilogue output stores with a cache-policy immediate.  STORE_POL != 0: buffer stores through a resource based at the
+// tile's first output row (wave-uniform; 32-bit offsets inside the tile's rows), 16 = sc1 (write-through at the XCD
+// L2), 2 = nt
+#ifndef EBC_GEMM_STORE_POL
+#define EBC_GEMM_STORE_POL 0
+#endif
+constexpr int STORE_POL = EBC_GEMM_STORE_POL;
+// The MLP pre-activation the c_fc product saves for the backward (EPI_GELU / EPI_LN_GELU aux, 22.5 MB a layer at 16
+// crops) is read again only by the GELU' product a whole forward later: written through (sc1) it does not sit dirty in
+// the L2s at the launch's end, where a launch boundary pays ~B / 6 TB/s for B dirty bytes (MI355X_MICROARCH.md
+// "boundary"; tools/lab/gemm_tl_lab.hip: c_fc with every store sc1 29.0 -> 26.8 us).  Same-box bench A/B (r06c, 4
+// interleaved pairs): 3678 -> 3690 crops/s.  The f32 residual-stream outputs (RESID / LN_BWD C, read two or three
+// launches later) written through as well measured 3 % SLOWER (3579): their readers still found them in the L2s.
+#ifndef EBC_GEMM_AUX_POL
+#define EBC_GEMM_AUX_POL 16
+#endif
+constexpr int AUX_POL = EBC_GEMM_AUX_POL;
+template <class TO, int W, int POL = STORE_POL> __device__ __forceinline__ void pstore(TO* base, unsigned off, const float* v) {
+    static_assert(W == 4 || W == 8, "4 or 8 elements");
+    if constexpr (POL == 0) {
+        if constexpr (W == 8) store8<TO>(base + off, v);
+        else store4<TO>(base + off, v);
+    } else {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+        const unsigned bo = off * (unsigned)sizeof(TO);
+        if constexpr (std::is_same<TO, float>::value) {
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                                         __float_as_uint(v[3])}, rs, bo, 0, POL);
+            if constexpr (W == 8)
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
+                                                             __float_as_uint(v[7])}, rs, bo + 16, 0, POL);
+        } else {
+            typedef TO tw __attribute__((ext_vector_type(W)));
+            tw r;
+#pragma unroll
+            for (int i = 0; i < W; ++i) r[i] = (TO)v[i];
+            if constexpr (W == 8) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), rs, bo, 0, POL);
+            else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, r), rs, bo, 0, POL);
+        }
+    }
+}
+
 // The epilogue stages the f32 tile through LDS in passes of EPR rows: all BM rows when they fit the
 // ring's bytes (or 64 KiB), else halves, quarters, ... (never below one wave's WM rows).
 template <int BM, int BN, int S, int ROWB, int WM> constexpr int ep_rows() {
@@ -894,6 +938,15 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 bool vr = false;                     // RESID: the row is a replaced prompt row
                 // RESID with rpart: the lane's partial sum / sum of squares of its row's output values
                 float rsum = 0.f, rsq = 0.f;
+                const size_t tb = (size_t)m0 * g.N;          // the tile's first output row (pstore bases)
+                auto put = [&](auto* base, size_t off, const float* v, int w, auto polc) {
+                    using TT = typename std::remove_pointer<decltype(base)>::type;
+                    constexpr int POL = decltype(polc)::value;
+                    if (w == 8) pstore<TT, 8, POL>(base + tb, (unsigned)(off - tb), v);
+                    else pstore<TT, 4, POL>(base + tb, (unsigned)(off - tb), v);
+                };
+                using PolC = std::integral_constant<int, STORE_POL>;
+                using PolA = std::integral_constant<int, AUX_POL>;
                 auto finish = [&](float* v, int w, const float* bias, const float* lwv, const auto& pre, size_t off,
                                   const auto& xs) {
                     if constexpr (LN) {
@@ -901,27 +954,21 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                     }
                     for (int i = 0; i < w; ++i) v[i] += bias[i];
                     if constexpr (GE) {
-                        if (g.aux) {
-                            if (w == 8) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
-                            else store4<T>(reinterpret_cast<T*>(g.aux) + off, v);
-                        }
+                        if (g.aux) put(reinterpret_cast<T*>(g.aux), off, v, w, PolA{});
                         for (int i = 0; i < w; ++i) v[i] = quick_gelu(v[i]);
                     } else if constexpr (EPI == EPI_GELU_BWD) {
                         for (int i = 0; i < w; ++i) v[i] *= quick_gelu_grad((float)pre[i]);
                     } else if constexpr (LNB) {
                         for (int i = 0; i < w; ++i) v[i] = fmaf(lr, v[i] - la - (xs[i] - lm) * lb, (float)pre[i]);
-                        if (w == 8) store8<T>(reinterpret_cast<T*>(g.xh) + off, v);
-                        else store4<T>(reinterpret_cast<T*>(g.xh) + off, v);
+                        put(reinterpret_cast<T*>(g.xh), off, v, w, PolC{});
                     } else if constexpr (EPI == EPI_RESID) {
                         for (int i = 0; i < w; ++i) v[i] = vr ? (float)pre[i] : v[i] + pre[i];
                         if (VREP && g.rpart) {
                             for (int i = 0; i < w; ++i) { rsum += v[i]; rsq = fmaf(v[i], v[i], rsq); }
-                            if (w == 8) store8<T>(reinterpret_cast<T*>(g.xh) + off, v);
-                            else store4<T>(reinterpret_cast<T*>(g.xh) + off, v);
+                            put(reinterpret_cast<T*>(g.xh), off, v, w, PolC{});
                         }
                     }
-                    if (w == 8) store8<TO>(C + off, v);
-                    else store4<TO>(C + off, v);
+                    put(C, off, v, w, PolC{});
                 };
                 static_for<0, PH>([&](auto phc) {
                     constexpr int a0 = decltype(phc)::value * TMP;
@@ -1040,6 +1087,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             typedef PA pa8 __attribute__((ext_vector_type(8)));
             typedef T t8v __attribute__((ext_vector_type(8)));
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            const size_t tb = (size_t)m0 * g.N;              // the tile's first output row (pstore bases)
 #pragma unroll 1
             for (int pass = 0; pass < BM / EPR; ++pass) {
                 pa8 pre[PRE ? NIT : 1];
@@ -1085,7 +1133,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                         v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
                     }
                     if constexpr (EPI == EPI_GELU) {
-                        if (g.aux) store8<T>(reinterpret_cast<T*>(g.aux) + off, v);
+                        if (g.aux) pstore<T, 8, AUX_POL>(reinterpret_cast<T*>(g.aux) + tb, (unsigned)(off - tb), v);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] = quick_gelu(v[i]);
                     } else if constexpr (EPI == EPI_GELU_BWD) {
@@ -1099,7 +1147,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
 #pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] += pre[k][i];
                     }
-                    store8<TO>(C + off, v);
+                    pstore<TO, 8>(C + tb, (unsigned)(off - tb), v);
                 }
                 if constexpr (EPI == EPI_STATS) {
                     // BatchNorm batch statistics of the conv output (models/utils.py:254-303 bn1/bn2): per-tile
