@@ -46,6 +46,7 @@ ANCHORS_NWPU = [0.0, 1.0, 2.0, 3.0, 4.21931]     # configs/reduction_8.json ["4"
 ANCHORS_SHA = [0.0, 1.0, 2.0, 3.0, 4.29992]      # configs/reduction_8.json ["4"]["sha"]["average"]
 FLOP_PER_CROP = 135.63e9                          # 58.33 fwd + 77.30 bwd GFLOP
 MFMA_PEAK_TF = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.3}   # MI355X dense (MI355X_MICROARCH.md)
+EVAL_FLOP_PER_TILE = 58.33e9                       # one 224x224 forward
 HBM_PEAK_GBS = 8000.0
 METRIC = "train crops/sec clip_vit_b_16 224px @1/2/4/8 MI355X; MAE parity"
 
@@ -79,6 +80,10 @@ def parse(argv=None):
     ap.add_argument("--classes-out", default=None,
                     help="write the kernel class of every instrumented launch of one step, in launch order, as JSON "
                          "(tools/pmc_step.py maps rocprofv3 --pmc dispatches to classes with it)")
+    ap.add_argument("--syncbn-world1", action="store_true",
+                    help="measurement: the multi-GPU rank's path at world size 1 -- a one-rank RCCL process group, DDP + "
+                         "SyncBatchNorm (wrap_ddp), and the decoder's SyncBatchNorm (unfused conv / all-reduce / finalize) "
+                         "path forced although the group has one rank (VERDICT r05 item 9)")
     ap.add_argument("--eval", action="store_true",
                     help="SURVEY §8(d) config 5 instead: sliding-window eval of 2048x3072 images (window = stride = 224, "
                          "140 tiles per image, tiles sharded over ranks); --steps images timed; --dtype fp32 is the "
@@ -260,9 +265,14 @@ def setup(args, rank, world, local, device):
         from ebc_amd import _lib as _l
         _l.check(_l.lib().ebc_set_weight_touch(args.touch), "ebc_set_weight_touch")
     model.train()
-    if world > 1:
+    if world > 1 or getattr(args, "syncbn_world1", False):
         from ebc_amd.distributed import wrap_ddp       # SyncBatchNorm + DDP, as trainer.py:147
         model = wrap_ddp(model, device.index)
+        if world == 1:
+            # --syncbn-world1: the decoder takes its SyncBatchNorm path (f64 sums all-reduced over the group between the
+            # conv and the finalize) although the group has one rank -- the N > 1 rank's launches, RCCL calls included
+            import ebc_amd.model as _em
+            _em._bn_group = lambda bn: (bn.process_group or dist.group.WORLD) if isinstance(bn, torch.nn.SyncBatchNorm) else None
     loss_fn = DACELoss(BINS, 8, weight_count_loss=1.0, count_loss="dmcount", input_size=args.size).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
     amp_dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.dtype]
@@ -288,7 +298,7 @@ def setup(args, rank, world, local, device):
         scaler.update()
         # one packed all-reduce of the 5 loss_info scalars (reference: 5 separate + .item(), train.py:62): the
         # loss's own [5] term vector (loss, ot, tv, count, ce), no stack launch
-        if world > 1:
+        if dist.is_initialized():
             dist.all_reduce(loss_fn.last_terms)
     step.pool = pool
     step.loss_fn = loss_fn
@@ -584,6 +594,11 @@ def run_eval(args, rank, world, device):
             "value": round(tiles * args.steps / elapsed, 2), "unit": "tiles/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_image": round(elapsed / args.steps * 1e3, 3),
             "images_per_s": round(args.steps / elapsed, 3), "higher_is_better": True, "scaling": "strong",
+            "roofline": {"bound": "mfma", "flop_per_tile": EVAL_FLOP_PER_TILE,
+                         "achieved": round(tiles * args.steps / elapsed * EVAL_FLOP_PER_TILE / 1e12 / world, 2),
+                         "peak": MFMA_PEAK_TF[args.dtype], "unit": "TFLOP/s",
+                         "frac": round(tiles * args.steps / elapsed * EVAL_FLOP_PER_TILE / 1e12 / world / MFMA_PEAK_TF[args.dtype], 4),
+                         "note": "per GPU; end to end (tile gather, forward, assembly, D2H copy)"},
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (uniform pixels, ImageNet-normalised)",
             "config": {"workload": f"SURVEY §8(d) config 5: {tiles} tiles per image sharded over {world} rank(s)",
                        "tiles_per_image": tiles, "density_map": list(out.shape)}}), flush=True)
@@ -608,6 +623,10 @@ def main():
         dist.init_process_group(backend, device_id=torch.device(f"cuda:{dev_index}") if backend == "nccl" else None)
     torch.cuda.set_device(dev_index)
     device = torch.device(f"cuda:{dev_index}")
+    if world == 1 and args.syncbn_world1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
     if args.augment or args.eval:
         if args.augment:
             run_augment(args, rank, device)
@@ -707,8 +726,10 @@ def main():
                 out["cpu_baseline"] = cpu_baseline_resnet(args, 2, 5)
             else:
                 out["cpu_baseline"] = cpu_baseline(args, args.cpu_crops, args.cpu_steps)
+        if args.syncbn_world1:
+            out["config"]["workload"] += "; --syncbn-world1: DDP + SyncBatchNorm path on a one-rank RCCL group"
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -595,7 +595,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         constexpr bool PREF_G = MODE == 0 && EPI == EPI_GELU_BWD && NW >= 8 && TM % 2 == 0 && (TN & 1) == 0;
         typedef T gp8_t __attribute__((ext_vector_type(8)));
         gp8_t gp8[PREF_G ? TM / 2 : 1][TN / 2 > 0 ? TN / 2 : 1];
-        if constexpr (PREF_G) {
+        auto prefetch_g = [&]() {
             const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
             const T* aux = reinterpret_cast<const T*>(g.aux);
 #pragma unroll
@@ -604,8 +604,8 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
 #pragma unroll
                 for (int q = 0; q < TN / 2; ++q) gp8[a][q] = *reinterpret_cast<const gp8_t*>(aux + ro + q * 32 + fq * 8);
             }
-        }
-        if constexpr (PREF) {
+        };
+        auto prefetch_r = [&]() {
             const int mb = m0 + wm * WM + (lane & 15), nb = n0 + wn * WN, fq = lane >> 4;
 #pragma unroll
             for (int a = 0; a < TM; ++a) {
@@ -614,7 +614,22 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 for (int q = 0; q < TN / 2; ++q) rp8[a][q] = *reinterpret_cast<const rp8_t*>(src + q * 32 + fq * 8);
                 if constexpr (TN & 1) rp4[a] = *reinterpret_cast<const rp4_t*>(src + (TN / 2) * 32 + fq * 4);
             }
-        }
+        };
+        // Where the epilogue prefetches are issued (r06, tools/lab/gemm_tl_lab.hip: issued ahead of the ring they delayed
+        // tile 0 by 1.3-1.4 us -- GELU' prologue 2.9 vs 1.6 us for c_fc, RESID 3.2 vs 1.8 us for the plain product):
+        //  * loader-wave tiles: the compute waves issue theirs after tile 0 has landed (their vmcnt counts no ring piece);
+        //  * the 8-wave GELU' tiles (2-stage ring): right behind tile 0's pieces, which are then waited for with a vmcnt
+        //    that leaves the NPF younger prefetch loads in flight (tile 1's wait, vmcnt(0), covers them);
+        //  * 4-wave tiles without loader waves: ahead of the ring as before (later, every counted ring wait would have to
+        //    count them).
+#ifndef EBC_GEMM_PREF_LATE
+#define EBC_GEMM_PREF_LATE 1
+#endif
+        constexpr bool LATE_G = EBC_GEMM_PREF_LATE && PREF_G && NLW == 0 && S == 2;
+        constexpr bool LATE_R = EBC_GEMM_PREF_LATE && PREF && NLW > 0;
+        constexpr int NPF = (TM / 2) * (TN / 2) * (int)sizeof(gp8_t) / 16;   // 16-B loads of prefetch_g
+        if constexpr (PREF_G && !LATE_G) prefetch_g();
+        if constexpr (PREF && !LATE_R) prefetch_r();
         // EPI_LN: the workgroup's rows' partials (gemm_nt_ln; lnparts float2 a row, rows m0 .. m0 + BM contiguous) are
         // copied by LDS-DMA into LDS past the ring ahead of tile 0 -- counted loads of the issuing waves, older than
         // every ring piece, so landed once tile 0 has -- and reduced in the epilogue.  (Register loads of them, 2-4 per
@@ -625,7 +640,17 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
 #pragma unroll
         for (int s = 0; s < S - 1; ++s)
             if (s < nk) stage(s, s);
-        sync_tile(0, std::true_type{});
+        if constexpr (LATE_G) {
+            prefetch_g();
+            // tile 0 landed (its pieces are older than the NPF prefetch loads), every wave past the barrier
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NPF) : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        } else {
+            sync_tile(0, std::true_type{});
+        }
+        if constexpr (LATE_R) prefetch_r();
         EBC_GEMM_STAMP(1, tile);
         if (S - 1 < nk) stage(S - 1, S - 1);
         typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
@@ -1683,6 +1708,17 @@ int gemm_nt(int dtype, int epi, int out_f32, const void* A, const void* B, void*
         case EBC_BF16: return dispatch_epi<EBF16>(g, epi, out_f32, ws, ws_bytes, st);
     }
     return EBC_E_ARG;
+}
+
+bool gemm_ln_bwd_fold_pays(int dtype, int M, int N, int K)
+{
+    // The EPI_LN_BWD product stages BM x 32 row partials (32 KB at BM = 128) past its ring.  On the loader-wave tiles
+    // (cfg 15 / 16: one workgroup a CU anyway, at most one wave of tiles) that costs no occupancy; on the 2-stage 4-wave
+    // tile the many-tile shapes take (cfg 5: two workgroups a CU at 57 KB) it halves the workgroups a CU holds: 32
+    // crops (M = 7328) ran the folded c_fc dX at 86 us against 45 + 16 us for the product + LayerNorm launch pair, bench
+    // 3923 vs 4082 crops/s (r06h, profiles/r06h_ln_bwd_fold_32crops.txt).  The fold is taken where it pays.
+    const int cfg = select_cfg(dtype != EBC_F32, M, N, K);
+    return cfg == 15 || cfg == 16;
 }
 
 int gemm_rowstat_parts(int dtype, int M, int N, int K)

@@ -53,6 +53,8 @@ int gemm_nt_ln(int dtype, int epi, int out_f32, const void* A, const void* B, vo
                const float* resid, void* aux, int M, int N, int K, hipStream_t st, void* ws, size_t ws_bytes,
                const GemmLn& ln);
 int gemm_rowstat_parts(int dtype, int M, int N, int K);
+// whether the c_fc dX product (M x N = 768 x K = 3072) runs the LayerNorm-backward epilogue without losing occupancy
+bool gemm_ln_bwd_fold_pays(int dtype, int M, int N, int K);
 // split-K workspace the heuristic wants for this shape (0: no split); zero-filled counter block first
 size_t gemm_workspace_bytes(int dtype, int M, int N, int K);
 // implicit-GEMM 3x3 convolution geometry (gemm.hip MODE 1 / MODE 2)

@@ -296,7 +296,8 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
     // ln_2's backward, g = dLN2 (.) gamma_2.  The c_fc dX product then multiplies by (W_fc')^T, so its accumulator IS g,
     // and finishes dX1 = dX + rstd (g - mean(g) - xhat mean(g xhat)) in its epilogue (gemm.hip EPI_LN_BWD): no dH write
     // and re-read, no LayerNorm launch.
-    bool fold_b = dtype != EBC_F32 && lay.bpart && !(flags & EBC_VIT_BWD_NO_LN_FOLD);
+    bool fold_b = dtype != EBC_F32 && lay.bpart && !(flags & EBC_VIT_BWD_NO_LN_FOLD) &&
+                  ebc::gemm_ln_bwd_fold_pays(dtype, M, WIDTH, MLP);
     for (int l = 0; l < layers && fold_b; ++l) {
         const EbcVitLayer& p = w->layer[l];
         fold_b = p.wt_fc_ln && p.s_fc_ln && p.b_fc_ln;
