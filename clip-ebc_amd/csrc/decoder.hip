@@ -148,55 +148,78 @@ __device__ __forceinline__ float4 bilinear4(const float* feat, int b, int y, int
 }
 
 // ------------------------------------------------------------------ forward
-template <class T>
+// The row kernels below: one image row per blockIdx.y (b * rows + r: the position / pixel row is wave-uniform),
+// blockIdx.x * 256 + threadIdx.x = (position in the row, a V-channel chunk), 32-bit index math, V = 8 channels a lane
+// (16-B stores of the 16-bit outputs) where C allows.  (r06: the flat form -- one 64-bit division of the element
+// index and two more in interior() per 4 channels -- was VALU-bound: upsample_pad 19.3, bn_relu_pad 13.6,
+// bn_add_relu 18.2 us in-step at 16 crops.)  Same arithmetic per element.
+template <class T, int V> __device__ __forceinline__ void stv(T* p, const float* v) {
+    if constexpr (V == 8) st8(p, v);
+    else st4(p, make_float4(v[0], v[1], v[2], v[3]));
+}
+template <class T, int V>
 __global__ __launch_bounds__(256) void upsample_pad_kernel(const float* __restrict__ feat, T* __restrict__ xpad,
                                                            DGeo g, int h, int w, float scale)
 {
-    const int C4 = g.C / 4;
-    const long e = (long)blockIdx.x * 256 + threadIdx.x;
-    if (e >= g.Q * C4) return;
-    const long q = e / C4;
-    const int c = (int)(e - q * C4) * 4;
-    const long p = interior(g, q);
-    float4 v = f4(0.f);
-    if (p >= 0) {
-        const int hw = g.H * g.W, b = (int)(p / hw), r = (int)(p - (long)b * hw), y = r / g.W, x = r - y * g.W;
-        v = bilinear4(feat, b, y, x, h, w, g.C, c, scale);
+    const int row = blockIdx.y, b = row / g.Hp, yp = row - b * g.Hp;       // padded row yp of image b
+    const int CV = g.C / V, i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= g.Wp * CV) return;
+    const int xp = i / CV, c = (i - xp * CV) * V;
+    float v[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = 0.f;
+    if (yp >= 1 && yp <= g.H && xp >= 1 && xp <= g.W) {
+#pragma unroll
+        for (int k = 0; k < V; k += 4) {
+            const float4 r = bilinear4(feat, b, yp - 1, xp - 1, h, w, g.C, c + k, scale);
+            v[k] = r.x; v[k + 1] = r.y; v[k + 2] = r.z; v[k + 3] = r.w;
+        }
     }
-    st4(xpad + q * g.C + c, v);
+    stv<T, V>(xpad + ((size_t)row * g.Wp + xp) * g.C + c, v);
 }
 
-template <class T>
+template <class T, int V>
 __global__ __launch_bounds__(256) void bn_relu_pad_kernel(const T* __restrict__ z, const float* __restrict__ scale,
                                                           const float* __restrict__ shift, T* __restrict__ hpad, DGeo g)
 {
-    const int C4 = g.C / 4;
-    const long e = (long)blockIdx.x * 256 + threadIdx.x;
-    if (e >= g.Q * C4) return;
-    const long q = e / C4;
-    const int c = (int)(e - q * C4) * 4;
-    const long p = interior(g, q);
-    float4 v = f4(0.f);
-    if (p >= 0) v = relu4(fma4(ld4(z + p * g.C + c), ld4(scale + c), ld4(shift + c)));
-    st4(hpad + q * g.C + c, v);
+    const int row = blockIdx.y, b = row / g.Hp, yp = row - b * g.Hp;
+    const int CV = g.C / V, i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= g.Wp * CV) return;
+    const int xp = i / CV, c = (i - xp * CV) * V;
+    float v[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = 0.f;
+    if (yp >= 1 && yp <= g.H && xp >= 1 && xp <= g.W) {
+        const T* zp = z + ((size_t)(b * g.H + yp - 1) * g.W + xp - 1) * g.C + c;
+#pragma unroll
+        for (int k = 0; k < V; k += 4) {
+            const float4 r = relu4(fma4(ld4(zp + k), ld4(scale + c + k), ld4(shift + c + k)));
+            v[k] = r.x; v[k + 1] = r.y; v[k + 2] = r.z; v[k + 3] = r.w;
+        }
+    }
+    stv<T, V>(hpad + ((size_t)row * g.Wp + xp) * g.C + c, v);
 }
 
-template <class T>
+template <class T, int V>
 __global__ __launch_bounds__(256) void bn_add_relu_kernel(const T* __restrict__ z, const float* __restrict__ scale,
                                                           const float* __restrict__ shift, const float* __restrict__ feat,
-                                                          T* __restrict__ y, long P, int H, int W, int C, int h, int w,
-                                                          float fscale)
+                                                          T* __restrict__ y, int H, int W, int C, int h, int w, float fscale)
 {
-    const int C4 = C / 4;
-    const long e = (long)blockIdx.x * 256 + threadIdx.x;
-    if (e >= P * C4) return;
-    const long p = e / C4;
-    const int c = (int)(e - p * C4) * 4;
-    const int hw = H * W, b = (int)(p / hw), r = (int)(p - (long)b * hw), yy = r / W, xx = r - yy * W;
-    float4 v = fma4(ld4(z + p * C + c), ld4(scale + c), ld4(shift + c));
-    const float4 res = bilinear4(feat, b, yy, xx, h, w, C, c, fscale);       // downsample = Identity: + x
-    v.x += res.x; v.y += res.y; v.z += res.z; v.w += res.w;
-    st4(y + p * C + c, relu4(v));
+    const int row = blockIdx.y, b = row / H, yy = row - b * H;             // pixel row yy of image b
+    const int CV = C / V, i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W * CV) return;
+    const int xx = i / CV, c = (i - xx * CV) * V;
+    const size_t o = ((size_t)row * W + xx) * C + c;
+    float v[V];
+#pragma unroll
+    for (int k = 0; k < V; k += 4) {
+        float4 a = fma4(ld4(z + o + k), ld4(scale + c + k), ld4(shift + c + k));
+        const float4 res = bilinear4(feat, b, yy, xx, h, w, C, c + k, fscale);       // downsample = Identity: + x
+        a.x += res.x; a.y += res.y; a.z += res.z; a.w += res.w;
+        a = relu4(a);
+        v[k] = a.x; v[k + 1] = a.y; v[k + 2] = a.z; v[k + 3] = a.w;
+    }
+    stv<T, V>(y + o, v);
 }
 
 // per-tile column partials [nb][2C] -> f64 column sums [2C]: 64 columns x 16 row groups per block
@@ -699,39 +722,93 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 
 // xT3[kx][c][pos] = xpad[(b * Hp + yp) * Wp + x + kx][c] for pos = b * Pimg + yp * W + x (b < B), else 0: every
 // position of a row (the zero guard rows, the tail past the last image included).  A 64-position x 64-channel tile
-// per block: the three taps' 16-B loads all issued first, then one LDS transpose per tap (both sides 16-B vectors).
+// per block.  The three taps are one row of centre values shifted: tap 1 is column x + 1 of xpad's row, taps 0 / 2
+// the centre of position pos -1 / +1 within the same image row, and at x = 0 / W - 1 xpad's border column 0 / W + 1
+// (staged beside the centres: the pad cells are copied as they are).  So the block loads the 66 centre rows of its
+// positions (one halo position each side) once and transposes them through LDS once for all three taps (r06: the r05
+// form loaded each position's three taps, 3x the rows, and transposed three times).
 template <class T>
 __global__ __launch_bounds__(256) void transpose3_kernel(const T* __restrict__ xpad, T* __restrict__ xT3, DGeo g)
 {
-    __shared__ float sm[TQ][TC + 1];
+    __shared__ float sm[TQ + 2][TC + 1];           // centre of position j0 - 1 + slot
+    __shared__ float se[2][TQ][TC + 1];            // border column 0 / W + 1 of position j0 + slot's row (x = 0 / W - 1)
     const int t = threadIdx.x;
-    const long j0 = (long)blockIdx.x * TQ;
+    const int j0 = blockIdx.x * TQ;                 // (Qs < 2^31: checked by the launcher)
     const int c0 = blockIdx.y * TC;
-    const int ql = t >> 2, cl = (t & 3) * 16;
-    const long pos = j0 + ql;
-    const long b = pos / g.Pimg;
-    const int rem = (int)(pos - b * g.Pimg), yp = rem / g.W, x = rem - yp * g.W;
-    const bool valid = b < g.B && yp < g.Hp;
-    const long q0 = valid ? (b * g.Hp + yp) * g.Wp + x : 0;
-    float v[3][16];
+    const int HpW = g.Hp * g.W, Pimg = (int)g.Pimg;
+    float v[2][16], e[2][16];
+    int pls[2], edg[2];
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-        ld8(xpad + (q0 + kx) * g.C + c0 + cl, v[kx]);
-        ld8(xpad + (q0 + kx) * g.C + c0 + cl + 8, v[kx] + 8);
+    for (int r = 0; r < 2; ++r) {                   // (TQ + 2) x 4 chunks of 16 channels over 256 threads
+        const int k = t + 256 * r, pl = k >> 2, cl = (k & 3) * 16;
+        pls[r] = k < (TQ + 2) * 4 ? pl : -1;
+        edg[r] = -1;
+        const int pos = j0 - 1 + pl;
+        bool ok = pls[r] >= 0 && pos >= 0;
+        long q = 0;
+        int x = 0;
+        if (ok) {
+            const int pb = pos / Pimg, prem = pos - pb * Pimg;
+            ok = pb < g.B && prem < HpW;
+            const int pyp = prem / g.W;
+            x = prem - pyp * g.W;
+            q = ((long)pb * g.Hp + pyp) * g.Wp + x + 1;
+        }
+        if (ok) {
+            ld8(xpad + q * g.C + c0 + cl, v[r]);
+            ld8(xpad + q * g.C + c0 + cl + 8, v[r] + 8);
+            const bool inb = pl >= 1 && pl <= TQ;           // one of the block's own positions
+            if (inb && (x == 0 || x == g.W - 1)) {
+                const long qe = x == 0 ? q - 1 : q + 1;
+                ld8(xpad + qe * g.C + c0 + cl, e[r]);
+                ld8(xpad + qe * g.C + c0 + cl + 8, e[r] + 8);
+                edg[r] = x == 0 ? 0 : 1;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[r][i] = 0.f;
+        }
     }
-    const int cr = t >> 2, jl = (t & 3) * 16;
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-        if (kx) __syncthreads();                  // every thread done reading the previous tap's tile
+    for (int r = 0; r < 2; ++r) {
+        if (pls[r] < 0) continue;
+        const int cl = ((t + 256 * r) & 3) * 16;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sm[ql][cl + i] = valid ? v[kx][i] : 0.f;
-        __syncthreads();
-        float w[16];
+        for (int i = 0; i < 16; ++i) sm[pls[r]][cl + i] = v[r][i];
+        if (edg[r] >= 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = sm[jl + i][cr];
-        T* dst = xT3 + ((size_t)kx * g.C + c0 + cr) * g.Qs + j0 + jl;
-        st8(dst, w);
-        st8(dst + 8, w + 8);
+            for (int i = 0; i < 16; ++i) se[edg[r]][pls[r] - 1][cl + i] = e[r][i];
+        }
+    }
+    __syncthreads();
+    // output: 8 lanes a channel row, each 8 consecutive positions (16-B stores, a whole 128-B line per 8 lanes); this
+    // thread's 8 positions' x and validity walked from the first (no division in the loop)
+    const int jl = (t & 7) * 8;
+    const int p0 = j0 + jl;
+    int b = p0 / Pimg, rem = p0 - b * Pimg, x = rem % g.W;
+    bool lft[8], rgt[8], val[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        val[i] = b < g.B && rem < HpW;
+        lft[i] = x > 0;
+        rgt[i] = x < g.W - 1;
+        if (++rem == Pimg) { rem = 0; x = 0; ++b; }
+        else if (++x == g.W) x = 0;
+    }
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        const int cr = pass * 32 + (t >> 3);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            float w[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float s = kx == 1 ? sm[jl + i + 1][cr] : kx == 0 ? (lft[i] ? sm[jl + i][cr] : se[0][jl + i][cr])
+                                                                      : (rgt[i] ? sm[jl + i + 2][cr] : se[1][jl + i][cr]);
+                w[i] = val[i] ? s : 0.f;
+            }
+            st8(xT3 + ((size_t)kx * g.C + c0 + cr) * g.Qs + j0 + jl, w);
+        }
     }
 }
 
@@ -744,12 +821,12 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__
 {
     constexpr int NCAND = 2 * UP;
     constexpr float scale = 1.0f / (float)UP;
-    const int C4 = C / 4;
-    const long e = (long)blockIdx.x * 256 + threadIdx.x;
-    if (e >= (long)B * h * w * C4) return;
-    const long cell = e / C4;
-    const int c = (int)(e - cell * C4) * 4;
-    const int b = (int)(cell / (h * w)), r = (int)(cell - (long)b * h * w), i = r / w, j = r - i * w;
+    // one input row (b, i) per blockIdx.y, 32-bit index math (r06: was a 64-bit division per 4 channels)
+    const int row = blockIdx.y, b = row / h, i = row - b * h;
+    const int C4 = C / 4, e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= w * C4) return;
+    const int j = e / C4, c = (e - j * C4) * 4;
+    const long cell = (long)row * w + j;
     float wy[NCAND], wx[NCAND];
     int oy[NCAND], ox[NCAND];
 #pragma unroll
@@ -930,10 +1007,11 @@ extern "C" size_t ebc_dec_workspace_bytes(int dtype, int B, int H, int W, int C,
 extern "C" int ebc_dec_upsample_pad(int dtype, const float* feat, void* xpad, int B, int h, int w, int C, int up,
                                     ebc_stream_t stream)
 {
-    if (!feat || !xpad || up < 1 || C % 64) return EBC_E_ARG;
+    if (!feat || !xpad || up < 1 || C % 64 || B <= 0 || (long)B * (h * up + 2) >= 65536) return EBC_E_ARG;
     const Geo g = make_geo(dtype, B, h * up, w * up, C);
     const DGeo d = dgeo(g);
-    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(upsample_pad_kernel<T>, dim3(nblk(g.Q * (C / 4))), dim3(256), 0,
+    const dim3 grid((unsigned)((g.Wp * (C / 8) + 255) / 256), (unsigned)(B * g.Hp));
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_pad_kernel<T, 8>), grid, dim3(256), 0,
                                                (hipStream_t)stream, feat, (T*)xpad, d, h, w, 1.0f / (float)up));
     EBC_CHECK_LAUNCH();
     return EBC_OK;
@@ -1011,10 +1089,11 @@ extern "C" int ebc_bn_finalize(const double* colsum, double count, float eps, fl
 extern "C" int ebc_bn_relu_pad(int dtype, const void* z, const float* scale, const float* shift, void* hpad, int B,
                                int H, int W, int C, ebc_stream_t stream)
 {
-    if (!z || !scale || !shift || !hpad || C % 64) return EBC_E_ARG;
+    if (!z || !scale || !shift || !hpad || C % 64 || B <= 0 || (long)B * (H + 2) >= 65536) return EBC_E_ARG;
     const Geo g = make_geo(dtype, B, H, W, C);
     const DGeo d = dgeo(g);
-    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(bn_relu_pad_kernel<T>, dim3(nblk(g.Q * (C / 4))), dim3(256), 0,
+    const dim3 grid((unsigned)((g.Wp * (C / 8) + 255) / 256), (unsigned)(B * g.Hp));
+    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_relu_pad_kernel<T, 8>), grid, dim3(256), 0,
                                                (hipStream_t)stream, (const T*)z, scale, shift, (T*)hpad, d));
     EBC_CHECK_LAUNCH();
     return EBC_OK;
@@ -1024,10 +1103,17 @@ extern "C" int ebc_bn_add_relu(int dtype, const void* z, const float* scale, con
                                int up, void* y, int B, int H, int W, int C, ebc_stream_t stream)
 {
     if (!z || !scale || !shift || !feat || !y || up < 1 || H % up || W % up || C % 4) return EBC_E_ARG;
-    const long P = (long)B * H * W;
-    EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(bn_add_relu_kernel<T>, dim3(nblk(P * (C / 4))), dim3(256), 0,
-                                               (hipStream_t)stream, (const T*)z, scale, shift, feat, (T*)y, P, H, W, C,
-                                               H / up, W / up, 1.0f / (float)up));
+    if (B <= 0 || H <= 0 || W <= 0 || (long)W * C >= (1L << 31) || (long)B * H >= 65536) return EBC_E_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    if (C % 8 == 0) {
+        const dim3 grid((unsigned)((W * (C / 8) + 255) / 256), (unsigned)(B * H));
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_add_relu_kernel<T, 8>), grid, dim3(256), 0, st, (const T*)z, scale,
+                                                   shift, feat, (T*)y, H, W, C, H / up, W / up, 1.0f / (float)up));
+    } else {
+        const dim3 grid((unsigned)((W * (C / 4) + 255) / 256), (unsigned)(B * H));
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((bn_add_relu_kernel<T, 4>), grid, dim3(256), 0, st, (const T*)z, scale,
+                                                   shift, feat, (T*)y, H, W, C, H / up, W / up, 1.0f / (float)up));
+    }
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -1087,6 +1173,7 @@ extern "C" int ebc_dec_transpose3(int dtype, const void* xpad, void* xT3, int B,
     const DGeo d = dgeo(g);
     // (r05: a register-transpose form without LDS -- a lane's 4 positions x 8 channels, 8-B stores -- ran 26.1 vs 23.4 us
     // in-step, not kept)
+    if (g.Qs >= (1L << 31) - TQ || W < 2) return EBC_E_ARG;
     const dim3 grid((unsigned)(g.Qs / TQ), (unsigned)(C / TC));
     EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL(transpose3_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream,
                                                (const T*)xpad, (T*)xT3, d));
@@ -1099,14 +1186,14 @@ extern "C" int ebc_dec_upsample_bwd(int dtype, const void* g, float* dfeat, int 
 {
     if (!g || !dfeat || C % 4) return EBC_E_ARG;
     if (up != 1 && up != 2) return EBC_E_UNSUPPORTED;
-    const long cells = (long)B * h * w;
-    const unsigned grid = nblk(cells * (C / 4));
+    if (B <= 0 || h <= 0 || w <= 0 || (long)w * C >= (1L << 31) || (long)B * h >= 65536) return EBC_E_ARG;
+    const dim3 grid((unsigned)((w * (C / 4) + 255) / 256), (unsigned)(B * h));
     const hipStream_t st = (hipStream_t)stream;
     if (up == 2) {
-        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 2>), dim3(grid), dim3(256), 0, st,
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 2>), grid, dim3(256), 0, st,
                                                    (const T*)g, dfeat, B, h, w, 2 * h, 2 * w, C));
     } else {
-        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 1>), dim3(grid), dim3(256), 0, st,
+        EBC_DTYPE_SWITCH(dtype, hipLaunchKernelGGL((upsample_bwd_kernel<T, 1>), grid, dim3(256), 0, st,
                                                    (const T*)g, dfeat, B, h, w, h, w, C));
     }
     EBC_CHECK_LAUNCH();

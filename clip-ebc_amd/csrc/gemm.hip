@@ -28,6 +28,18 @@ using namespace ebc;
 #ifndef EBC_GEMM_STAMP
 #define EBC_GEMM_STAMP(phase, tile) ((void)0)
 #endif
+// Anatomy switches for the lab harnesses (tools/lab/*_tl_lab.hip, r06): the K loop without its MFMAs, without its
+// LDS-DMA pieces (the fragments read stale LDS), and the segment ending right after the K loop (no epilogue, no
+// split-K / stream-K hand-off); all 0 in the library build
+#ifndef EBC_GEMM_LAB_NOMFMA
+#define EBC_GEMM_LAB_NOMFMA 0
+#endif
+#ifndef EBC_GEMM_LAB_NOLOAD
+#define EBC_GEMM_LAB_NOLOAD 0
+#endif
+#ifndef EBC_GEMM_LAB_NOEPI
+#define EBC_GEMM_LAB_NOEPI 0
+#endif
 
 namespace {
 
@@ -114,6 +126,9 @@ struct GemmArgs {
 // swizzled on the DMA source address so the ds_read_b128 fragment reads are conflict free
 // (brute-force checked against the MI355X_MICROARCH.md §LDS lane groups).
 template <int ROWB> __device__ __forceinline__ int swz_row(int row) {
+    // 256-B rows (BK = 128, 16-bit): chunk ^ (row & 15) -- the 16 lanes of a ds_read_b128 lane group then read 4
+    // aligned blocks of 4 chunks (c0, c0^4, c0^8, c0^12): all 64 banks
+    if constexpr (ROWB == 256) return row & 15;
     if constexpr (ROWB == 128) return (row >> 1) & 7;
     else return (0x1320 >> (((row >> 2) & 3) * 4)) & 3;      // [0,2,3,1][(row >> 2) & 3]
 }
@@ -209,6 +224,11 @@ template <> __device__ __forceinline__ void load8f<float>(const float* p, float*
 #define EBC_GEMM_STORE_POL 0
 #endif
 constexpr int STORE_POL = EBC_GEMM_STORE_POL;
+// ... of the 16-bit outputs (C and the compute-dtype copies xh)
+#ifndef EBC_GEMM_STORE_POL_H
+#define EBC_GEMM_STORE_POL_H EBC_GEMM_STORE_POL
+#endif
+constexpr int STORE_POL_H = EBC_GEMM_STORE_POL_H;
 // The MLP pre-activation the c_fc product saves for the backward (EPI_GELU / EPI_LN_GELU aux, 22.5 MB a layer at 16
 // crops) is read again only by the GELU' product a whole forward later: written through (sc1) it does not sit dirty in
 // the L2s at the launch's end, where a launch boundary pays ~B / 6 TB/s for B dirty bytes (MI355X_MICROARCH.md
@@ -398,6 +418,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
             if constexpr (MODE == 2) cpk |= (unsigned)(ko / (16 / EB)) << (4 * i);
         }
         auto stage_pieces = [&](int buf, int kt) {
+            if constexpr (EBC_GEMM_LAB_NOLOAD) return;
             const int ktg = ktbase + kt;
             long oa, ob;
             if constexpr (MODE == 1) {
@@ -491,7 +512,7 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         // two fragment register sets (next step's reads under this step's MFMAs) unless the wave tile's
         // accumulators leave no room (2 waves/SIMD: 256 registers per lane in all)
         constexpr bool DB = TM * TN * 4 + 2 * (TM + TN) * (EB == 2 ? 4 : 8) <= 200;
-        static_assert(!DB || KS == 2 || S % 2 == 0, "register-set alternation");
+        static_assert(!DB || KS % 2 == 0 || S % 2 == 0, "register-set alternation");
         const int fr = lane & 15, fg = lane >> 4;
         // Fragment addressing is lane-constant: every fragment row is 16-aligned + fr, so the XOR
         // swizzle term is swz_row(fr) for all of them.  Per lane one VGPR offset per (k32 step,
@@ -656,6 +677,13 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         typename E::Frag a0[TM], b0[TN], a1[TM], b1[TN];
         load_frags(std::integral_constant<int, 0>{}, 0, a0, b0);
         auto mma_all = [&](typename E::Frag (&af)[TM], typename E::Frag (&bf)[TN]) {
+            if constexpr (EBC_GEMM_LAB_NOMFMA) {          // keep the fragment reads: one VALU add each
+#pragma unroll
+                for (int a = 0; a < TM; ++a) acc[a][0][0] += (float)af[a][0];
+#pragma unroll
+                for (int b = 0; b < TN; ++b) acc[0][b][1] += (float)bf[b][0];
+                return;
+            }
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -721,9 +749,12 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 if (!decltype(tailc)::value || kt < nk) {
                     if constexpr (!DB) {
                         static_for<0, KS>([&](auto kc) { step(sc, tailc, kt, decltype(kc)::value, a0, b0, a0, b0); });
-                    } else if constexpr (KS == 2) {
-                        step(sc, tailc, kt, 0, a0, b0, a1, b1);
-                        step(sc, tailc, kt, 1, a1, b1, a0, b0);
+                    } else if constexpr (KS % 2 == 0) {       // 128-B rows: 2 k32 steps a tile; 256-B rows: 4
+                        static_for<0, KS / 2>([&](auto hc) {
+                            constexpr int h = decltype(hc)::value;
+                            step(sc, tailc, kt, 2 * h, a0, b0, a1, b1);
+                            step(sc, tailc, kt, 2 * h + 1, a1, b1, a0, b0);
+                        });
                     } else if constexpr ((s & 1) == 0) {
                         step(sc, tailc, kt, 0, a0, b0, a1, b1);
                     } else {
@@ -736,6 +767,14 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
         for (; kt0 + 2 * S <= nk; kt0 += S) group(kt0, std::false_type{});
         for (; kt0 < nk; kt0 += S) group(kt0, std::true_type{});
         EBC_GEMM_STAMP(2, tile);
+        if constexpr (EBC_GEMM_LAB_NOEPI) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b) asm volatile("" :: "v"(acc[a][b]));
+            EBC_GEMM_STAMP(3, tile);
+            return nk;
+        }
 
         if (SPL && g.splits > 1 && g.cnt == nullptr) {
             // split-K without a last arriver (deep splits of the weight-gradient products): every split stores its
@@ -966,7 +1005,8 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NLW)) void gemm_nt_kernel(GemmArg
                 const size_t tb = (size_t)m0 * g.N;          // the tile's first output row (pstore bases)
                 auto put = [&](auto* base, size_t off, const float* v, int w, auto polc) {
                     using TT = typename std::remove_pointer<decltype(base)>::type;
-                    constexpr int POL = decltype(polc)::value;
+                    constexpr int POL = std::is_same<TT, float>::value ? decltype(polc)::value
+                                        : (decltype(polc)::value == STORE_POL ? STORE_POL_H : decltype(polc)::value);
                     if (w == 8) pstore<TT, 8, POL>(base + tb, (unsigned)(off - tb), v);
                     else pstore<TT, 4, POL>(base + tb, (unsigned)(off - tb), v);
                 };

@@ -123,6 +123,29 @@ int main(int argc, char** argv)
         g.A = A; g.C = C;
         return launch_gemm_k<EF16, _Float16, EPI_STORE, 128, 96, 3, 2, 2, 128, 0, false, 4>(g, 0); }, nt(128, 96, 768)});
 
+    // r06: 256-B K rows (BK = 128), 2 stages: half the k-tiles (barriers) of the 128-B rings at the same LDS
+    vars.push_back({"c_proj+res R256 S2+4L", 768, 3072, [&](GemmArgs& g) {
+        g.A = Cfc; g.resid = R; g.C = C;
+        return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 2, 2, 2, 256, 0, false, 4>(g, 0); }, nt(128, 96, 768)});
+    vars.push_back({"c_proj store R256 S2+4L", 768, 3072, [&](GemmArgs& g) {
+        g.A = Cfc; g.C = C;
+        return launch_gemm_k<EF16, _Float16, EPI_STORE, 128, 96, 2, 2, 2, 256, 0, false, 4>(g, 0); }, nt(128, 96, 768)});
+    vars.push_back({"dH K2304 R256 S2+4L", 768, 2304, [&](GemmArgs& g) {
+        g.A = Cfc; g.C = C;
+        return launch_gemm_k<EF16, _Float16, EPI_STORE, 128, 96, 2, 2, 2, 256, 0, false, 4>(g, 0); }, nt(128, 96, 768)});
+    vars.push_back({"out+res R256 S2+4L", 768, 768, [&](GemmArgs& g) {
+        g.A = A; g.resid = R; g.C = C;
+        return launch_gemm_k<EF16, float, EPI_RESID, 128, 96, 2, 2, 2, 256, 0, false, 4>(g, 0); }, nt(128, 96, 768)});
+    vars.push_back({"dO store R256 S2+4L", 768, 768, [&](GemmArgs& g) {
+        g.A = A; g.C = C;
+        return launch_gemm_k<EF16, _Float16, EPI_STORE, 128, 96, 2, 2, 2, 256, 0, false, 4>(g, 0); }, nt(128, 96, 768)});
+    vars.push_back({"c_proj store R256 S2", 768, 3072, [&](GemmArgs& g) {
+        g.A = Cfc; g.C = C;
+        return launch_gemm_k<EF16, _Float16, EPI_STORE, 128, 96, 2, 2, 2, 256, 0, false, 0>(g, 0); }, nt(128, 96, 768)});
+    vars.push_back({"QKV R256 128x192 S2", 2304, 768, [&](GemmArgs& g) {
+        g.A = A; g.C = C;
+        return launch_gemm_k<EF16, _Float16, EPI_STORE, 128, 192, 2, 2, 4, 256, 0, false, 0>(g, 0); }, nt(128, 192, 2304)});
+
     GemmArgs gfc{A, W, Cfc, bias, nullptr, Afc, M, 3072, 768};
     gfc.kslice = 768;
     auto cfc = [&]() { return launch_gemm_k<EF16, _Float16, EPI_GELU, 256, 192, 2, 4, 2, 128, 0, false, 0>(gfc, 0); };
