@@ -1448,11 +1448,19 @@ int launch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st)
 {
     if (cfg == 2) return launch_gemm<E, TO, EPI, 128, 64, 2, 2, 2, 128, MODE>(g, st);
     if constexpr (E::BYTES == 2) {
+#if EBC_CONV_LAB_W4   // lab only (0 in the library): 4-wave conv tiles, one 128x96 / 112x96 wave tile a SIMD
+        if (cfg == 3) return launch_gemm<E, TO, EPI, 256, 192, 2, 2, 2, 128, MODE>(g, st);
+#else
         if (cfg == 3) return launch_gemm<E, TO, EPI, 256, 192, 2, 4, 2, 128, MODE>(g, st);
+#endif
         if (cfg == 7) return launch_gemm<E, TO, EPI, 256, 256, 2, 4, 2, 128, MODE>(g, st);
         if (cfg == 13) return launch_gemm<E, TO, EPI, 128, 96, 3, 2, 2, 128, MODE>(g, st);
         if constexpr (MODE == 1) {
+#if EBC_CONV_LAB_W4
+            if (cfg == 17) return launch_gemm<E, TO, EPI, 224, 192, 2, 2, 2, 128, MODE>(g, st);
+#else
             if (cfg == 17) return launch_gemm<E, TO, EPI, 224, 192, 2, 2, 4, 128, MODE>(g, st);
+#endif
         }
     }
     return EBC_E_UNSUPPORTED;
