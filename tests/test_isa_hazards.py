@@ -7,10 +7,10 @@ v_mfma_f32_16x16x32_f16 accumulator 1 wait state after it and saw the registers'
 bits: running maxima of 1e3..3e3).  tools/lab/mfma_raw_lab.hip measures the result readable from 7 wait states on gfx950.
 This test runs the path-aware scan (tools/dbg/mfma_raw_paths.py) over every code object of clip-ebc_amd/lib/
 libebc_hip.so, so a build whose schedule reintroduces such a read fails here instead of producing NaN rows."""
+import importlib.util
 import os
 import shutil
 import subprocess
-import sys
 import tempfile
 
 import pytest
@@ -18,13 +18,15 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "clip-ebc_amd", "lib", "libebc_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
-sys.path.insert(0, os.path.join(REPO, "tools", "dbg"))
 
 
 def _code_objects(lib, work):
     """The gfx950 code objects of the library's .hip_fatbin (one offload bundle per translation unit)."""
     fb = os.path.join(work, "fb.bin")
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", lib], check=True, capture_output=True)
+    # an explicit output file: without one objcopy rewrites its input in place -- here the library this very process
+    # may have mapped (test_abi loads it), which crashed a later test
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", lib, os.path.join(work, "copy.so")], check=True,
+                   capture_output=True)
     data = open(fb, "rb").read()
     magic = b"__CLANG_OFFLOAD_BUNDLE__"
     starts = []
@@ -48,7 +50,10 @@ def _code_objects(lib, work):
 @pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists(f"{LLVM}/llvm-objdump") or not shutil.which("objcopy"),
                     reason="needs the built library and the ROCm LLVM tools")
 def test_no_mfma_result_read_within_7_wait_states():
-    from mfma_raw_paths import kernels, short_reads
+    spec = importlib.util.spec_from_file_location("mfma_raw_paths", os.path.join(REPO, "tools", "dbg", "mfma_raw_paths.py"))
+    mrp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mrp)
+    kernels, short_reads = mrp.kernels, mrp.short_reads
     work = tempfile.mkdtemp()
     try:
         cos = _code_objects(LIB, work)
