@@ -26,6 +26,11 @@
 
 using namespace ebc;
 
+// lab-only phase stamps (tools/lab/attn_tl_lab.hip): 0 entry, 1 operands staged (after the barrier), 2 a wave's end
+#ifndef EBC_ATTN_STAMP
+#define EBC_ATTN_STAMP(phase) ((void)0)
+#endif
+
 namespace {
 
 constexpr int HD = 64;          // head dim
@@ -187,6 +192,30 @@ __device__ __forceinline__ void touch_wait(const TouchSink& s) { asm volatile(""
 // reductions across the four 16-lane rows by v_permlane16_swap / v_permlane32_swap (each lane receives its own and its
 // partner's value, in either order, so max / + of the pair is the same on both lanes).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// softmax pair arithmetic as two single-lane instructions (EBC_ATTN_SCALAR 1; the Makefile builds this file with
+// -fno-slp-vectorize so they stay single) or packed f32 (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32, 0).  Beside the
+// MFMAs a packed f32 instruction costs more issue than the two it replaces (MI355X_MICROARCH.md per-instruction
+// constants); r06, tools/lab/attn_tl_lab.hip, 16 crops: forward 11.8 -> 11.5 us, backward 25.3 -> 24.7 us
+#ifndef EBC_ATTN_SCALAR
+#define EBC_ATTN_SCALAR 1
+#endif
+// backward: the MFMA chain of dP starts from -delta (cdna_hip_programming.md "row constants as the initial accumulator"),
+// so dS = p dP' needs no subtraction (r06: backward 24.7 -> 24.0 us, compute phase 14.9 -> 14.3 us)
+#ifndef EBC_ATTN_DINIT
+#define EBC_ATTN_DINIT 1
+#endif
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) {
+    if constexpr (EBC_ATTN_SCALAR) return f32x2{__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y)};
+    else return __builtin_elementwise_fma(a, b, c);
+}
+__device__ __forceinline__ f32x2 add2(f32x2 a, f32x2 b) {
+    if constexpr (EBC_ATTN_SCALAR) return f32x2{a.x + b.x, a.y + b.y};
+    else return a + b;
+}
+__device__ __forceinline__ f32x2 mul2(f32x2 a, f32x2 b) {
+    if constexpr (EBC_ATTN_SCALAR) return f32x2{a.x * b.x, a.y * b.y};
+    else return a * b;
+}
 __device__ __forceinline__ float max3f(float a, float b, float c) {
     return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
@@ -214,6 +243,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     const int L = LFIX > 0 ? LFIX : L_;                        // compile-time sequence: tile loops and masks fold
     using T = typename E::T;
     using C = AttnCfg<E>;
+    EBC_ATTN_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
@@ -241,11 +271,13 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     rows_store<E, NWV>(Ks, fk);
     rows_store<E, NWV>(Vs, fv);
     __syncthreads();
+    EBC_ATTN_STAMP(1);
 
     TouchSink tsink;
     if (touch.n) touch_issue<NWV>(touch, tsink);               // every wave takes its share of the touch lines
     if (q0 >= L) {                                             // no live query in this wave (no barrier follows)
         if (touch.n) touch_wait(tsink);
+        EBC_ATTN_STAMP(2);
         return;
     }
     // key tiles past L are skipped; only the ragged last tile is masked; the softmax scale is folded
@@ -293,12 +325,12 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
             if (kt < nkt) {
 #pragma unroll
                 for (int i = 0; i < 4; i += 2) {
-                    f32x2 e = __builtin_elementwise_fma(f32x2{s[t][kt][i], s[t][kt][i + 1]}, c2v, mcv);
+                    f32x2 e = fma2(f32x2{s[t][kt][i], s[t][kt][i + 1]}, c2v, mcv);
                     e.x = __builtin_amdgcn_exp2f(e.x);
                     e.y = __builtin_amdgcn_exp2f(e.y);
                     s[t][kt][i] = e.x;
                     s[t][kt][i + 1] = e.y;
-                    acc += e;
+                    acc = add2(acc, e);
                 }
             }
         }
@@ -342,6 +374,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
         if (fg == 0 && qme < L && lse) lse[((size_t)b * H + h) * L + qme] = mx[t] * scale + logf(sum[t]);   // natural-log units
     }
     if (touch.n) touch_wait(tsink);
+    EBC_ATTN_STAMP(2);
 }
 
 // ------------------------------------------------------------------------------ backward dQ
@@ -651,6 +684,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     const int L = LFIX > 0 ? LFIX : L_;
     using T = typename E::T;
     using C = AttnCfg<E>;
+    EBC_ATTN_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Ks = reinterpret_cast<T*>(smem);
     T* Vs = reinterpret_cast<T*>(smem + C::TILE_BYTES);
@@ -680,6 +714,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     static_assert(64 * NWV >= 4 * LP, "a lane quad per padded query");
     if (qj == 0) { ls[qd] = lsv; dl[qd] = dlv; }
     __syncthreads();
+    EBC_ATTN_STAMP(1);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
     const int lim = rows > 0 && rows < L ? rows : L;
@@ -689,6 +724,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
     if (touch.n) touch_issue<NWV>(touch, tsink);
     if (16 * w >= lim) {
         if (touch.n) touch_wait(tsink);
+        EBC_ATTN_STAMP(2);
         return;
     }
     const int nkt = (L + 15) >> 4;
@@ -728,7 +764,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
         f32x4 sv[2][2], pv[2][2];                              // [pair parity][tile of the pair]
         auto sdp = [&](int kt, f32x4& s_, f32x4& p_) {
             s_ = f32x4{0.f, 0.f, 0.f, 0.f};
-            p_ = f32x4{0.f, 0.f, 0.f, 0.f};
+            p_ = EBC_ATTN_DINIT ? f32x4{-dq, -dq, -dq, -dq} : f32x4{0.f, 0.f, 0.f, 0.f};   // dP - delta from the MFMA chain
             if (kt < nkt) {
 #pragma unroll
                 for (int ks = 0; ks < 2; ++ks) {
@@ -755,12 +791,13 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
                 const int kt = 2 * st + hf;
 #pragma unroll
                 for (int i = 0; i < 4; i += 2) {
-                    f32x2 p = __builtin_elementwise_fma(f32x2{sv[cur][hf][i], sv[cur][hf][i + 1]}, c2v, nlv);
+                    f32x2 p = fma2(f32x2{sv[cur][hf][i], sv[cur][hf][i + 1]}, c2v, nlv);
                     p.x = __builtin_amdgcn_exp2f(p.x);
                     p.y = __builtin_amdgcn_exp2f(p.y);
                     if (kt >= nkt || (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i >= L)) p.x = 0.f;
                     if (kt >= nkt || (ragged && kt == nkt - 1 && 16 * kt + 4 * fg + i + 1 >= L)) p.y = 0.f;
-                    const f32x2 d = p * (f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]} + ndv);
+                    const f32x2 d = EBC_ATTN_DINIT ? mul2(p, f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]})
+                                                   : mul2(p, add2(f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]}, ndv));
                     ds[4 * hf + i] = d.x;
                     ds[4 * hf + i + 1] = d.y;
                 }
@@ -794,7 +831,12 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
         f32x4 sv[2][2], pv[2][2];                              // pipelined as the dQ phase, over query-tile pairs
         auto sdp = [&](int qt, f32x4& s_, f32x4& p_) {
             s_ = f32x4{0.f, 0.f, 0.f, 0.f};
-            p_ = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (EBC_ATTN_DINIT) {                    // dP^T - delta of the tile's queries from the MFMA chain
+                const float4 d4 = *reinterpret_cast<const float4*>(dl + 16 * qt + 4 * fg);
+                p_ = f32x4{-d4.x, -d4.y, -d4.z, -d4.w};
+            } else {
+                p_ = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
             if (qt < nqt) {
 #pragma unroll
                 for (int ks = 0; ks < 2; ++ks) {
@@ -824,10 +866,11 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
 #pragma unroll
                 for (int i = 0; i < 4; i += 2) {
                     // lse = +inf (padding) -> p = 0
-                    f32x2 p = __builtin_elementwise_fma(f32x2{sv[cur][hf][i], sv[cur][hf][i + 1]}, c2v, -lq[i / 2]);
+                    f32x2 p = fma2(f32x2{sv[cur][hf][i], sv[cur][hf][i + 1]}, c2v, -lq[i / 2]);
                     p.x = __builtin_amdgcn_exp2f(p.x);
                     p.y = __builtin_amdgcn_exp2f(p.y);
-                    const f32x2 d = p * (f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]} - dq[i / 2]);
+                    const f32x2 d = EBC_ATTN_DINIT ? mul2(p, f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]})
+                                                   : mul2(p, add2(f32x2{pv[cur][hf][i], pv[cur][hf][i + 1]}, -dq[i / 2]));
                     pp[4 * hf + i] = p.x;
                     pp[4 * hf + i + 1] = p.y;
                     ds[4 * hf + i] = d.x;
@@ -853,6 +896,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
         }
     }
     if (touch.n) touch_wait(tsink);
+    EBC_ATTN_STAMP(2);
 }
 
 // ------------------------------------------------------------------------------ sequences longer than LP
