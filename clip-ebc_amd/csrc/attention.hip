@@ -134,6 +134,23 @@ __device__ __forceinline__ void store4(typename E::T* p, float a, float b, float
     *reinterpret_cast<t4*>(p) = t4{E::from(a), E::from(b), E::from(c), E::from(d)};
 }
 
+// Two 16-column blocks' outputs of one row as 16-B stores (cdna_hip_programming.md T21): lane group fg holds columns
+// 4 fg .. 4 fg + 3 of blocks da and db (x sa, x sb); v_permlane16_swap (odd 16-lane rows of the first operand <-> even
+// rows of the second) leaves each lane 8 contiguous columns -- block (fg odd ? db : da), columns 8 (fg >> 1) .. -- one
+// dwordx4 store where two dwordx2 stores were (r06).  `row` is the output row's first element; the swaps run on every
+// lane (call it outside divergent code), the store only where `live`.
+template <class E>
+__device__ __forceinline__ void store8_pair(typename E::T* row, bool live, const f32x4& a, const f32x4& b, float sa, float sb,
+                                            int da, int db) {
+    typedef typename E::T t4 __attribute__((ext_vector_type(4)));
+    const int fg = (threadIdx.x & 63) >> 4;
+    const uint2 pa = __builtin_bit_cast(uint2, t4{E::from(a[0] * sa), E::from(a[1] * sa), E::from(a[2] * sa), E::from(a[3] * sa)});
+    const uint2 pb = __builtin_bit_cast(uint2, t4{E::from(b[0] * sb), E::from(b[1] * sb), E::from(b[2] * sb), E::from(b[3] * sb)});
+    const auto r0 = __builtin_amdgcn_permlane16_swap(pa.x, pb.x, false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(pa.y, pb.y, false, false);
+    if (live) *reinterpret_cast<uint4*>(row + 16 * ((fg & 1) ? db : da) + 8 * (fg >> 1)) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+}
+
 template <class E>
 __device__ __forceinline__ typename E::Frag lds_rowfrag(const typename E::T* base, int row, int col) {
     return load8<E>(base + attn_off<E>(row, col));
@@ -364,7 +381,11 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(const typename E::T*
     for (int t = 0; t < QT; ++t) {
         const float inv = 1.0f / sum[t];
         const int q = q0 + 16 * t + fr;
-        if (q < L) {
+        if constexpr (E::BYTES == 2) {
+            T* orow = out + ((size_t)b * L + q) * D + h * HD;
+            store8_pair<E>(orow, q < L, o[t][0], o[t][1], inv, inv, 0, 1);
+            store8_pair<E>(orow, q < L, o[t][2], o[t][3], inv, inv, 2, 3);
+        } else if (q < L) {
             T* orow = out + ((size_t)b * L + q) * D + h * HD + 4 * fg;
 #pragma unroll
             for (int dt = 0; dt < HD / 16; ++dt)
@@ -807,12 +828,10 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
             for (int dt = 0; dt < HD / 16; ++dt) dq_acc[dt] = mma(colfrag_at<E>(Kc[dt], 0, st), dsf, dq_acc[dt]);   // dQ^T
         }
         // dq_acc[dt][i] = dQ[q0 + fr][16 dt + 4 fg + i]
-        if (qme < L) {
-            T* row = dqkv + ((size_t)b * L + qme) * D3 + h * HD + 4 * fg;
-#pragma unroll
-            for (int dt = 0; dt < HD / 16; ++dt)
-                store4<E>(row + 16 * dt, dq_acc[dt][0] * scale, dq_acc[dt][1] * scale, dq_acc[dt][2] * scale,
-                          dq_acc[dt][3] * scale);
+        {
+            T* row = dqkv + ((size_t)b * L + qme) * D3 + h * HD;
+            store8_pair<E>(row, qme < L, dq_acc[0], dq_acc[1], scale, scale, 0, 1);
+            store8_pair<E>(row, qme < L, dq_acc[2], dq_acc[3], scale, scale, 2, 3);
         }
     }
     {
@@ -886,13 +905,12 @@ __global__ __launch_bounds__(1024) void attn_bwd_one_kernel(const typename E::T*
         }
         // dk / dv[dt][i] = dK / dV[k0 + fr][16 dt + 4 fg + i]
         const int key = k0 + fr;
-        if (key < L) {
-            T* row = dqkv + ((size_t)b * L + key) * D3 + h * HD + 4 * fg;
-#pragma unroll
-            for (int dt = 0; dt < HD / 16; ++dt) {
-                store4<E>(row + D + 16 * dt, dk[dt][0] * scale, dk[dt][1] * scale, dk[dt][2] * scale, dk[dt][3] * scale);
-                store4<E>(row + 2 * D + 16 * dt, dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
-            }
+        {
+            T* row = dqkv + ((size_t)b * L + key) * D3 + h * HD;
+            store8_pair<E>(row + D, key < L, dk[0], dk[1], scale, scale, 0, 1);
+            store8_pair<E>(row + D, key < L, dk[2], dk[3], scale, scale, 2, 3);
+            store8_pair<E>(row + 2 * D, key < L, dv[0], dv[1], 1.0f, 1.0f, 0, 1);
+            store8_pair<E>(row + 2 * D, key < L, dv[2], dv[3], 1.0f, 1.0f, 2, 3);
         }
     }
     if (touch.n) touch_wait(tsink);

@@ -8,6 +8,7 @@ mkdir -p build/$n lib/$n
 git show $rev:clip-ebc_amd/csrc/$src.hip > csrc/_old_$src.hip
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics"
 [ "$src" = gemm ] && FLAGS="$FLAGS -mllvm -amdgpu-mfma-vgpr-form=1"
+[ "$src" = attention ] && FLAGS="$FLAGS -fno-slp-vectorize"   # as the Makefile
 /opt/rocm/bin/hipcc $FLAGS -c csrc/_old_$src.hip -o build/$n/$src.o; rm -f csrc/_old_$src.hip
 objs=""
 for o in build/*.o; do b=$(basename $o .o); [ -f build/$n/$b.o ] && objs="$objs build/$n/$b.o" || objs="$objs $o"; done
