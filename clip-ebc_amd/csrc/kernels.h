@@ -13,6 +13,8 @@ struct TouchList {
     int n;
     void add(const void* p, size_t b) { if (p && b >= 128 && n < 8) { ptr[n] = p; bytes[n] = b; ++n; } }
 };
+// ebc_set_weight_touch: the touch lists are issued (attention.hip g_touch_mode == 1)
+bool touch_enabled();
 // in-step launch timing (probe.hip): probe_start returns a record index (or -1 when not armed)
 bool probe_on();
 int probe_start(int kind, int epi, int bm, int bn, int mode, int m, int n, int k, hipStream_t st);
@@ -77,7 +79,8 @@ constexpr size_t CONV_WS_STATS_OFFSET = 16 * 1024;
 int layernorm_fwd(int dtype, const float* x, int rpg, int gstride, int goff, const float* gamma, const float* beta,
                   void* out, float* outf, float* mean, float* rstd, int M, int D, hipStream_t st);
 int layernorm_bwd_fill(int dtype, const float* dy, const float* x, int rpg, int gstride, int goff, const float* mean,
-                       const float* rstd, const float* gamma, float* dx_out, void* dx_out_t, int M, int D, hipStream_t st);
+                       const float* rstd, const float* gamma, float* dx_out, void* dx_out_t, int M, int D, hipStream_t st,
+                       const TouchList* touch = nullptr);
 int layernorm_bwd(int dtype, int dy_f32, const void* dy, const float* x, int rpg, int gstride, int goff,
                   const float* mean, const float* rstd, const float* gamma, const float* dx_in, float* dx_out,
                   void* dx_out_t, int M, int D, hipStream_t st);

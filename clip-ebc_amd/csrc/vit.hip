@@ -305,9 +305,9 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
     // block l's attention backward reads onto the die the transposed weights of the dX products after it: its QKV dX
     // and block l-1's c_proj / c_fc / out-proj ones (see ebc_vit_forward)
     const size_t es = dtype == EBC_F32 ? 4 : 2;
-    auto touch_bwd = [&](int l) {
+    auto touch_bwd = [&](int l) {                  // l == layers: the last block's dX weights alone
         ebc::TouchList t{};
-        t.add(w->layer[l].wt_qkv, (size_t)WIDTH * QKVW * es);
+        if (l < layers) t.add(w->layer[l].wt_qkv, (size_t)WIDTH * QKVW * es);
         if (l > 0) {
             const EbcVitLayer& q = w->layer[l - 1];
             t.add(q.wt_proj, (size_t)MLP * WIDTH * es);
@@ -316,9 +316,11 @@ extern "C" int ebc_vit_backward(const EbcVitWeights* w, int B, int H, int W, int
         }
         return t;
     };
-    // (the CLS / prompt rows of dX, dXt are written as zeros by the same launch: no memsets)
+    // (the CLS / prompt rows of dX, dXt are written as zeros by the same launch: no memsets); it reads onto the die
+    // the last block's c_proj / c_fc / out-proj dX weights, which no attention backward precedes
+    const ebc::TouchList tl_top = touch_bwd(layers);
     EBC_TRY(ebc::layernorm_bwd_fill(dtype, dfeat, lay.X[layers], G, L, 1 + NV, lay.mpost, lay.rpost, w->ln_post_g, dX,
-                                    lay.dXt, B * G, WIDTH, st));
+                                    lay.dXt, B * G, WIDTH, st, dtype != EBC_F32 ? &tl_top : nullptr));
     for (int l = layers - 1; l >= 0; --l) {
         const EbcVitLayer& p = w->layer[l];
         LayerSave& s = lay.s[l];

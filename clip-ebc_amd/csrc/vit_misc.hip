@@ -12,6 +12,7 @@
 #include "ebc_common.h"
 #include "kernels.h"
 #include "mfma.h"
+#include "touch.h"
 
 using namespace ebc;
 
@@ -136,19 +137,30 @@ struct VptOut {
 };
 
 // RD: rows-dense output (layer 0's prompt rows): x, dx_in, mean and rstd at the mapped row, dy and dx_out dense
+// touch (ZF, ln_post's backward, the ViT backward's first launch): the first block's dX weights read onto the die
+// (touch.h) -- the later blocks' are touched by the attention backward above them, the first block's had none (r06
+// kernel trace: its c_fc dX product 38.3 us against 29 us for the others)
 template <class T, class DY, int NV, bool ZF = false, bool RD = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, const float* __restrict__ x, RowMap map,
                                                      const float* mean_in, const float* rstd_in, const float* gamma,
-                                                     const float* dx_in, float* dx_out, T* dx_out_t, int M, VptOut vo)
+                                                     const float* dx_in, float* dx_out, T* dx_out_t, int M, VptOut vo,
+                                                     TouchList touch)
 {
     constexpr int D = 256 * NV;
     constexpr float inv = 1.0f / (float)D;
     int r = row_block() * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    // the touch loads first: in flight beside the row's loads (issued after them, hipcc's waits for the row data at
+    // the kernel-argument branches below drained them too), waited at the wave's end
+    TouchSink ts;
+    if constexpr (ZF) { if (touch.n) touch_issue1<4>(touch, ts); }
     if constexpr (ZF) {
         // grid over every destination row (M = groups * gstride): rows outside the mapped groups get a zero
         // gradient (ln_post: the CLS / prompt rows), the others run as mapped row r = their index in the groups
-        if (r >= M) return;
+        if (r >= M) {
+            if (touch.n) touch_wait(ts);
+            return;
+        }
         const int grp = r / map.gstride, l = r - grp * map.gstride;
         if (l < map.goff || l >= map.goff + map.rpg) {
 #pragma unroll
@@ -157,6 +169,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
                 *reinterpret_cast<float4*>(dx_out + (size_t)r * D + c) = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (dx_out_t) st4<T>(dx_out_t + (size_t)r * D + c, make_float4(0.f, 0.f, 0.f, 0.f));
             }
+            if (touch.n) touch_wait(ts);
             return;
         }
         r = grp * map.rpg + l - map.goff;
@@ -201,6 +214,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
         *reinterpret_cast<float4*>(dx_out + orow + c) = o;
         if (!RD && dx_out_t) st4<T>(dx_out_t + xr + c, o);
     }
+    if constexpr (ZF) { if (touch.n) touch_wait(ts); }
 }
 
 // dvpt_l[r][c] = sum_b rows_l[b][r][c] for every layer l with a destination (crop order), one launch
@@ -645,9 +659,9 @@ static int ln_bwd_t(int dy_f32, const void* dy, const float* x, RowMap map, cons
     const int pi = probe_on() ? probe_start(EBC_PROBE_LN_BWD, 0, 0, 0, 0, M, 768, 0, st) : -1;
     struct Stop { int i; hipStream_t s; ~Stop() { probe_stop(i, s); } } stop{pi, st};
     if (dy_f32)
-        hipLaunchKernelGGL((ln_bwd_kernel<T, float, 3>), grid, dim3(256), 0, st, (const float*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M, vo);
+        hipLaunchKernelGGL((ln_bwd_kernel<T, float, 3>), grid, dim3(256), 0, st, (const float*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M, vo, TouchList{});
     else
-        hipLaunchKernelGGL((ln_bwd_kernel<T, T, 3>), grid, dim3(256), 0, st, (const T*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M, vo);
+        hipLaunchKernelGGL((ln_bwd_kernel<T, T, 3>), grid, dim3(256), 0, st, (const T*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (T*)dx_out_t, M, vo, TouchList{});
     EBC_CHECK_LAUNCH();
     return EBC_OK;
 }
@@ -655,21 +669,26 @@ static int ln_bwd_t(int dy_f32, const void* dy, const float* x, RowMap map, cons
 // ln_post's backward (dy f32 over the patch rows, no incoming dx): also writes the zero gradient of every row
 // outside the groups, so dx_out / dx_out_t need no memset: one launch over all M / rpg * gstride rows
 int layernorm_bwd_fill(int dtype, const float* dy, const float* x, int rpg, int gstride, int goff, const float* mean,
-                       const float* rstd, const float* gamma, float* dx_out, void* dx_out_t, int M, int D, hipStream_t st)
+                       const float* rstd, const float* gamma, float* dx_out, void* dx_out_t, int M, int D, hipStream_t st,
+                       const TouchList* touch)
 {
     if (D != 768 || M <= 0 || rpg <= 0 || M % rpg || goff + rpg > gstride) return EBC_E_UNSUPPORTED;
     const RowMap map{rpg, gstride, goff};
     const VptOut vo{nullptr, 1, 0};
+    TouchList t = touch && touch_enabled() ? *touch : TouchList{};
+    size_t lines = 0;                                   // at most one line a lane (touch_issue1)
+    for (int i = 0; i < t.n; ++i) lines += t.bytes[i] >> 7;
     const int Mf = M / rpg * gstride;
     const dim3 grid((Mf + 3) / 4);
+    if (lines > (size_t)grid.x * 256) t = TouchList{};
     const int pi = probe_on() ? probe_start(EBC_PROBE_LN_BWD, 0, 0, 0, 0, Mf, 768, 0, st) : -1;
     switch (dtype) {
         case EBC_F32: hipLaunchKernelGGL((ln_bwd_kernel<float, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean, rstd,
-                                         gamma, nullptr, dx_out, (float*)dx_out_t, Mf, vo); break;
+                                         gamma, nullptr, dx_out, (float*)dx_out_t, Mf, vo, t); break;
         case EBC_F16: hipLaunchKernelGGL((ln_bwd_kernel<_Float16, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean,
-                                         rstd, gamma, nullptr, dx_out, (_Float16*)dx_out_t, Mf, vo); break;
+                                         rstd, gamma, nullptr, dx_out, (_Float16*)dx_out_t, Mf, vo, t); break;
         case EBC_BF16: hipLaunchKernelGGL((ln_bwd_kernel<__bf16, float, 3, true>), grid, dim3(256), 0, st, dy, x, map, mean,
-                                          rstd, gamma, nullptr, dx_out, (__bf16*)dx_out_t, Mf, vo); break;
+                                          rstd, gamma, nullptr, dx_out, (__bf16*)dx_out_t, Mf, vo, t); break;
         default: probe_stop(pi, st); return EBC_E_ARG;
     }
     probe_stop(pi, st);
@@ -746,11 +765,11 @@ int layernorm_bwd_rows(int dtype, const void* dy, const float* x, int rpg, int g
     struct Stop { int i; hipStream_t s; ~Stop() { probe_stop(i, s); } } stop{pi, st};
     switch (dtype) {
         case EBC_F32: hipLaunchKernelGGL((ln_bwd_kernel<float, float, 3, false, true>), grid, dim3(256), 0, st, (const float*)dy,
-                                         x, map, mean, rstd, gamma, dx_in, dx_out, (float*)nullptr, M, vo); break;
+                                         x, map, mean, rstd, gamma, dx_in, dx_out, (float*)nullptr, M, vo, TouchList{}); break;
         case EBC_F16: hipLaunchKernelGGL((ln_bwd_kernel<_Float16, _Float16, 3, false, true>), grid, dim3(256), 0, st,
-                                         (const _Float16*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (_Float16*)nullptr, M, vo); break;
+                                         (const _Float16*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (_Float16*)nullptr, M, vo, TouchList{}); break;
         case EBC_BF16: hipLaunchKernelGGL((ln_bwd_kernel<__bf16, __bf16, 3, false, true>), grid, dim3(256), 0, st,
-                                          (const __bf16*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (__bf16*)nullptr, M, vo); break;
+                                          (const __bf16*)dy, x, map, mean, rstd, gamma, dx_in, dx_out, (__bf16*)nullptr, M, vo, TouchList{}); break;
         default: return EBC_E_ARG;
     }
     EBC_CHECK_LAUNCH();
