@@ -1,5 +1,6 @@
-"""Per-kernel-name averages of rocprofv3 --pmc counters (lab): FETCH_SIZE / WRITE_SIZE (KB, gfx950 TCC units as the
-bench's pmc_step.py reads them) for every kernel whose name matches a pattern.
+"""Per-kernel-name averages of rocprofv3 --pmc counters (lab) for every kernel whose name matches a pattern: FETCH_SIZE
+and WRITE_SIZE as MB (FETCH_SIZE x 1024 x 2 bytes -- gfx950 counts half of wide coalesced reads -- and WRITE_SIZE x 1024,
+as tools/pmc_step.py), other counters raw.
     python tools/lab/pmc_bytes.py DB [DB ...] --match prep_weights transpose im2col"""
 import argparse
 import collections
@@ -22,6 +23,7 @@ for db in a.dbs:
     for (did, name), cs in per.items():
         for cn, v in cs.items():
             acc[name[:90]][cn].append(v)
+SCALE = {"FETCH_SIZE": 2048 / 1e6, "WRITE_SIZE": 1024 / 1e6}
 for name, cs in sorted(acc.items()):
-    parts = [f"{cn} {sum(v) / len(v):.4g}" for cn, v in sorted(cs.items())]
+    parts = [f"{cn}{' MB' if cn in SCALE else ''} {sum(v) / len(v) * SCALE.get(cn, 1.0):.4g}" for cn, v in sorted(cs.items())]
     print(f"{name}\n    n={len(next(iter(cs.values())))}  " + "  ".join(parts))
