@@ -227,20 +227,21 @@ __global__ void vpt_sum_kernel(const float* __restrict__ rows, VptSum vs, int la
     const int l = blockIdx.y;
     if (e >= n4 || !vs.dst[l]) return;
     const float4* src = reinterpret_cast<const float4*>(rows) + (size_t)l * B * n4 + e;
-    // eight rows' loads in flight before their adds (r06: one dependent HBM round trip per crop took 10 us a step);
-    // the adds keep crop order, so the sums keep their bits
-    float4 acc = src[0];
-    int b = 1;
-    for (; b + 8 <= B; b += 8) {
-        float4 v[8];
+    // sixteen crops' loads in flight before their adds (r06: one dependent HBM round trip per crop took 10 us a step;
+    // batches of eight left the 16-crop step's last seven crops one load at a time): indices past B re-read the last
+    // crop and are not added, and the adds keep crop order, so the sums keep their bits
+    constexpr int NB = 16;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int b0 = 0; b0 < B; b0 += NB) {
+        float4 v[NB];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = src[(size_t)(b + i) * n4];
+        for (int i = 0; i < NB; ++i) v[i] = src[(size_t)min(b0 + i, B - 1) * n4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w; }
-    }
-    for (; b < B; ++b) {
-        const float4 v = src[(size_t)b * n4];
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        for (int i = 0; i < NB; ++i) {
+            const int b = b0 + i;
+            if (b == 0) acc = v[i];
+            else if (b < B) { acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w; }
+        }
     }
     reinterpret_cast<float4*>(vs.dst[l])[e] = acc;
 }
