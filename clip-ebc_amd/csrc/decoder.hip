@@ -153,6 +153,14 @@ __device__ __forceinline__ float4 bilinear4(const float* feat, int b, int y, int
 // (16-B stores of the 16-bit outputs) where C allows.  (r06: the flat form -- one 64-bit division of the element
 // index and two more in interior() per 4 channels -- was VALU-bound: upsample_pad 19.3, bn_relu_pad 13.6,
 // bn_add_relu 18.2 us in-step at 16 crops.)  Same arithmetic per element.
+// XCD order for the 2-D row grids (mfma.h xcd_remap on the dispatch-linear id, x fastest): each XCD takes a contiguous
+// run of image rows, so the bilinear taps that neighbouring rows share are fetched into one XCD's L2 (r06 PMC: the
+// dispatch order spread them over the XCDs -- upsample_pad fetched 4x, bn_add_relu 7x, upsample_bwd 3x its bytes)
+__device__ __forceinline__ void xcd_block2d(int& bx, int& by) {
+    const int nx = (int)gridDim.x, id = xcd_remap((int)(blockIdx.y * gridDim.x + blockIdx.x), nx * (int)gridDim.y);
+    by = id / nx;
+    bx = id - by * nx;
+}
 template <class T, int V> __device__ __forceinline__ void stv(T* p, const float* v) {
     if constexpr (V == 8) st8(p, v);
     else st4(p, make_float4(v[0], v[1], v[2], v[3]));
@@ -161,8 +169,10 @@ template <class T, int V>
 __global__ __launch_bounds__(256) void upsample_pad_kernel(const float* __restrict__ feat, T* __restrict__ xpad,
                                                            DGeo g, int h, int w, float scale)
 {
-    const int row = blockIdx.y, b = row / g.Hp, yp = row - b * g.Hp;       // padded row yp of image b
-    const int CV = g.C / V, i = blockIdx.x * 256 + threadIdx.x;
+    int bx, row;
+    xcd_block2d(bx, row);
+    const int b = row / g.Hp, yp = row - b * g.Hp;                         // padded row yp of image b
+    const int CV = g.C / V, i = bx * 256 + threadIdx.x;
     if (i >= g.Wp * CV) return;
     const int xp = i / CV, c = (i - xp * CV) * V;
     float v[V];
@@ -205,8 +215,10 @@ __global__ __launch_bounds__(256) void bn_add_relu_kernel(const T* __restrict__ 
                                                           const float* __restrict__ shift, const float* __restrict__ feat,
                                                           T* __restrict__ y, int H, int W, int C, int h, int w, float fscale)
 {
-    const int row = blockIdx.y, b = row / H, yy = row - b * H;             // pixel row yy of image b
-    const int CV = C / V, i = blockIdx.x * 256 + threadIdx.x;
+    int bx, row;
+    xcd_block2d(bx, row);
+    const int b = row / H, yy = row - b * H;                                // pixel row yy of image b
+    const int CV = C / V, i = bx * 256 + threadIdx.x;
     if (i >= W * CV) return;
     const int xx = i / CV, c = (i - xx * CV) * V;
     const size_t o = ((size_t)row * W + xx) * C + c;
@@ -822,8 +834,10 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* __restrict__
     constexpr int NCAND = 2 * UP;
     constexpr float scale = 1.0f / (float)UP;
     // one input row (b, i) per blockIdx.y, 32-bit index math (r06: was a 64-bit division per 4 channels)
-    const int row = blockIdx.y, b = row / h, i = row - b * h;
-    const int C4 = C / 4, e = blockIdx.x * 256 + threadIdx.x;
+    int bx, row;
+    xcd_block2d(bx, row);
+    const int b = row / h, i = row - b * h;
+    const int C4 = C / 4, e = bx * 256 + threadIdx.x;
     if (e >= w * C4) return;
     const int j = e / C4, c = (e - j * C4) * 4;
     const long cell = (long)row * w + j;
