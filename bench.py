@@ -446,7 +446,7 @@ def probe_steps(step, first, n, device, trace=True, classes_out=None):
     return out, dace_steps
 
 
-PMC_FILE = os.path.join("profiles", "r06fin3_pmc_step.json")
+PMC_FILE = os.path.join("profiles", "r06fin4_pmc_step.json")
 
 
 def committed_pmc(kernel_key):
